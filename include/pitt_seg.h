@@ -1,0 +1,207 @@
+/*
+ * pitt_seg.h -- C ABI of the MI355X-native RANSAC-plane / support / Euclidean-cluster path.
+ *
+ * Drop-in boundary for the PCL calls inside the reference's segmentation services
+ * (paths relative to the reference root, TheEngineRoom-UniGe/pitt_object_table_segmentation):
+ *
+ *   pitt_plane_segment / _batch   replaces  seg.segment(*inliers, *coefficients)
+ *        src/segmentation_services/plane_segmentation_srv.cpp:52-67   (SACMODEL_PLANE, SAC_RANSAC,
+ *        optimize = true; FromNormals falls through to the plain plane model for SACMODEL_PLANE)
+ *        src/segmentation_services/supports_segmentation_srv.cpp:89-111 (ransacPlaneSegmentator)
+ *   pitt_extract_indices          replaces  ExtractIndices<PointXYZ>::filter (positive / negative)
+ *        src/segmentation_services/supports_segmentation_srv.cpp:114-127 (removePlaneInliner)
+ *   pitt_find_supports            replaces  the body of findSupports
+ *        src/segmentation_services/supports_segmentation_srv.cpp:241-361
+ *   pitt_euclidean_clusters       replaces  EuclideanClusterExtraction::extract + KdTree
+ *        src/segmentation_services/cluster_segmentation_srv.cpp:54-69
+ *
+ * Conventions: plain pointers and sizes, no C++ types, no exceptions.  Every call returns an
+ * int status (PITT_OK, PITT_NO_MODEL, or a negative PITT_E_*).  A context is not thread-safe;
+ * one context per thread (the reference's handlers run serially under ros::spin, s3.3).
+ * "No model" mirrors PCL's cleared outputs: n_inliers = 0, n_coeff = 0.
+ * Core results keep exact PCL semantics; the reference's post-processing quirks (drop index 0,
+ * centroid / (n+1)) are applied by the service mirror (pitt_srv.h), never here.
+ */
+#ifndef PITT_SEG_H
+#define PITT_SEG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PITT_ABI_VERSION 1
+/* Points per scoring tile; frames are scored in tiles of this many points. */
+#define PITT_TILE_POINTS 2048
+
+enum {
+    PITT_OK = 0,
+    PITT_NO_MODEL = 1,        /* not an error: RANSAC found no model (PCL clears outputs) */
+    PITT_E_INVALID = -1,      /* bad argument (null pointer, misaligned offset, capacity)  */
+    PITT_E_HIP = -2,          /* HIP runtime error                                          */
+    PITT_E_NOMEM = -3,        /* device or host allocation failed                           */
+    PITT_E_SAMPLER = -4,      /* sampler table exhausted (> slack rejected samples)         */
+    PITT_E_NODEVICE = -5      /* no gfx950 device / kernels not loadable                    */
+};
+
+/* A3: reduction order of the 4-lane Eigen dot / squaredNorm in the reference's PCL build. */
+enum { PITT_REDUCE_SSE2 = 0, PITT_REDUCE_HADD = 1, PITT_REDUCE_SEQ = 2 };
+/* A9: Eigen 3.2 `v /= s` multiplies by 1/s (default); Eigen >= 3.3 divides. */
+enum { PITT_DIV_EIGEN32 = 0, PITT_DIV_TRUE = 1 };
+
+typedef struct pitt_ctx pitt_ctx;
+
+/* Parameters of one SACSegmentation call (sac_segmentation.h members the reference sets). */
+typedef struct {
+    double   threshold;       /* setDistanceThreshold; compared as fabs(float) < double      */
+    int32_t  max_iterations;  /* setMaxIterations; RANSAC evaluates at most max_it+1 models  */
+    double   probability;     /* RandomSampleConsensus probability_ (PCL default 0.99)       */
+    uint32_t seed;            /* model rng seed; PCL uses 12345 (random_ == false)           */
+    int32_t  optimize;        /* setOptimizeCoefficients                                     */
+    int32_t  reduce_order;    /* PITT_REDUCE_*                                               */
+    int32_t  div_mode;        /* PITT_DIV_*                                                  */
+    int32_t  sampler_slack;   /* extra sampler attempts beyond max_it+1 for rejected samples */
+} pitt_sac_params;
+
+/* plane_segmentation_srv.cpp:19-21 defaults: th 0.007, 1000 iterations, seed 12345. */
+void pitt_sac_params_default(pitt_sac_params* p);
+
+/* Per-frame outcome of a plane segmentation (batch or single). */
+typedef struct {
+    float    coefficients[4];      /* a, b, c, d (refined when optimize)                 */
+    int32_t  n_coeff;              /* 4, or 0 when no model                              */
+    int32_t  status;               /* PITT_OK / PITT_NO_MODEL / PITT_E_*                 */
+    int64_t  n_inliers;            /* final inlier count                                 */
+    int32_t  hypotheses;           /* models PCL's RANSAC evaluates (T)                  */
+    int32_t  best_hypothesis;      /* index of the winning model                         */
+    int64_t  best_count;           /* inliers of the winning (unrefined) model           */
+    int32_t  rejected_samples;     /* isSampleGood rejections before the last hypothesis */
+    int32_t  flags;                /* PITT_FLAG_*                                        */
+} pitt_plane_result;
+
+enum {
+    PITT_FLAG_K_NEAR_INTEGER = 1   /* adaptive k within 1e-12 of an integer: libm-sensitive */
+};
+
+/* A batch of frames resident in device memory as structure-of-arrays float planes.
+ * Frame f holds counts[f] points at x/y/z[offsets[f] ... offsets[f]+counts[f]).
+ * offsets[f] must be a multiple of 4 (16-byte aligned rows) and every frame must stay readable
+ * up to offsets[f] + round_up(counts[f], PITT_TILE_POINTS) <= capacity (tail is masked). */
+typedef struct {
+    const float*   x;
+    const float*   y;
+    const float*   z;
+    const int64_t* offsets;   /* host array [n_frames] */
+    const int64_t* counts;    /* host array [n_frames] */
+    int32_t        n_frames;
+    int64_t        capacity;  /* points readable in each plane */
+} pitt_frames;
+
+/* --- context --------------------------------------------------------------------------- */
+int  pitt_create(pitt_ctx** out, int hip_device);
+void pitt_destroy(pitt_ctx* ctx);
+/* Run on a caller-owned hipStream_t (NULL = the context's own stream). */
+int  pitt_set_stream(pitt_ctx* ctx, void* hip_stream);
+void* pitt_get_stream(pitt_ctx* ctx);
+const char* pitt_last_error(pitt_ctx* ctx);
+int  pitt_abi_version(void);
+
+/* --- plane segmentation ------------------------------------------------------------------ */
+/* Single cloud from host memory, PCL layout: stride 16 (PointXYZ: x, y, z, pad) or 12.
+ * inliers_out (host, capacity n) receives the ascending inlier indices. */
+int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                       const pitt_sac_params* p, int32_t* inliers_out, int64_t* n_inliers,
+                       float coeff_out[4], int32_t* n_coeff);
+
+/* Batch of device-resident frames.  results: host [n_frames].  inliers_dev (optional, device
+ * int32 [capacity]): frame f's ascending inliers are written at inliers_dev + offsets[f].
+ * Synchronous: returns when results are on the host. */
+int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
+                             pitt_plane_result* results, int32_t* inliers_dev);
+
+/* Debug / parity hooks: per-hypothesis inlier counts of the last batch (host [n_frames*cap]),
+ * hypotheses beyond a frame's T are unspecified. */
+int pitt_last_hypothesis_counts(pitt_ctx* ctx, int32_t frame, int32_t* counts, int32_t cap);
+
+/* --- ExtractIndices ----------------------------------------------------------------------- */
+/* Device SoA in/out.  negative == 0: out = in[indices] (in index order);
+ * negative == 1: out = in minus indices, order preserving.  indices ascending, unique. */
+int pitt_extract_indices(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                         const int32_t* indices_dev, int64_t n_indices, int32_t negative,
+                         float* ox, float* oy, float* oz, int64_t* n_out);
+
+/* --- support segmentation (findSupports) -------------------------------------------------- */
+typedef struct {
+    float   min_iterative_cloud_percentage;  /* default 0.03  (:30)               */
+    float   min_iterative_plane_percentage;  /* default 0.03  (:31)               */
+    float   horizontal_variance_threshold;   /* default 0.09  (:33)               */
+    float   ransac_distance_threshold;       /* default 0.02f (:35)               */
+    int32_t ransac_max_iterations;           /* default 10    (:37)               */
+    float   horizontal_axis[3];              /* default 0, 0, -1 (:38)            */
+    float   edge_remove_offset[3];           /* default 0.02, 0.02, 0.005 (:39)   */
+    int32_t reduce_order;
+    int32_t div_mode;
+} pitt_support_params;
+void pitt_support_params_default(pitt_support_params* p);
+
+typedef struct {
+    int32_t      n_points;          /* original cloud size                                  */
+    const int32_t* idx_map;         /* Support::inliers: n_points ints (level tags / ranks)  */
+    float        coefficients[4];   /* support_coefficient_a..d (refined)                   */
+    int64_t      n_support;         /* support_cloud size                                    */
+    const float* support_xyz;       /* host, 3*n_support (SoA: x block, y block, z block)    */
+    int64_t      n_on_support;      /* on_support_cloud size                                 */
+    const float* on_support_xyz;    /* host, 3*n_on_support (SoA)                            */
+} pitt_support;
+
+typedef struct {
+    int32_t            n_supports;
+    const pitt_support* supports;   /* valid until the next call on the context */
+    int32_t            iterations;  /* RANSAC rounds run by the loop            */
+} pitt_support_list;
+
+/* xyz: host SoA (x[n], y[n], z[n]). */
+int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                       const pitt_support_params* p, pitt_support_list* out);
+
+/* --- Euclidean clusters -------------------------------------------------------------------- */
+typedef struct {
+    int64_t        size;
+    const int32_t* indices;   /* ascending */
+    float          sum_xyz[3];/* float sums in index order (the handler derives its centroid) */
+} pitt_cluster;
+
+typedef struct {
+    int32_t             n_clusters;
+    const pitt_cluster* clusters;   /* size-descending (PCL order); valid until next call */
+} pitt_cluster_list;
+
+/* xyz: host SoA.  tolerance as ClusterTolerance (double, cast to float by PCL);
+ * min_size/max_size as setMin/MaxClusterSize. */
+int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const float* y, const float* z,
+                            int64_t n, double tolerance, int32_t min_size, int32_t max_size,
+                            pitt_cluster_list* out);
+
+/* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
+enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };
+/* 640x480 Kinect-like pinhole cloud in the camera optical frame, row-major pixel order.
+ * Writes width*height points into x, y, z. */
+int pitt_synth_frame(int32_t scene, uint64_t scene_seed, int32_t width, int32_t height,
+                     float* x, float* y, float* z);
+/* `views` views of one table scene, transformed to a z-up world frame and concatenated. */
+int pitt_synth_fused(uint64_t scene_seed, int32_t views, int32_t width, int32_t height,
+                     float* x, float* y, float* z);
+
+/* --- profiling ------------------------------------------------------------------------------ */
+/* When enabled, every kernel launch is bracketed by hipEvents on the launch stream. */
+int pitt_profile_enable(pitt_ctx* ctx, int32_t on);
+/* Per-kernel totals since enable: launches, total milliseconds, algorithmic bytes. */
+int pitt_profile_get(pitt_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms,
+                     double* algorithmic_bytes);
+int pitt_profile_reset(pitt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PITT_SEG_H */

@@ -1,0 +1,689 @@
+// pitt_oracle.cpp -- CPU restatement of the reference's PCL path.  TEST INFRASTRUCTURE ONLY:
+// the parity checker for the HIP path and the CPU baseline of bench.py.  Never shipped.
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off, no fast-math: PCL's x86-64 SSE build rounds
+// every product and sum separately and keeps denormals).
+//
+// Reference call sites restated here (paths relative to the reference root):
+//   src/segmentation_services/plane_segmentation_srv.cpp:52-67   SACSegmentationFromNormals::segment
+//   src/segmentation_services/supports_segmentation_srv.cpp:89-361  support loop + helpers
+//   src/segmentation_services/cluster_segmentation_srv.cpp:38-104   EuclideanClusterExtraction
+// The PCL 1.7 semantics they call into (external, not in the container) are restated from the
+// published PCL 1.7 algorithms, as pinned in SURVEY.md Appendix A1-A8 (+A9 below):
+//   sample_consensus/impl/sac_model_plane.hpp  (isSampleGood, computeModelCoefficients,
+//       countWithinDistance, selectWithinDistance, optimizeModelCoefficients)
+//   sample_consensus/sac_model.h               (drawIndexSample, getSamples, rng seeding)
+//   sample_consensus/impl/ransac.hpp           (RandomSampleConsensus::computeModel)
+//   segmentation/impl/sac_segmentation.hpp     (segment, initSACModel fall-through A1)
+//   common/impl/centroid.hpp                   (computeMeanAndCovarianceMatrix, 9 float accus)
+//   common/impl/eigen.hpp                      (eigen33, computeRoots, computeRoots2)
+//   segmentation/impl/extract_clusters.hpp     (extractEuclideanClusters, sorted KdTree)
+// A9 (Eigen 3.2): `v /= s` on a float vector multiplies by (1/s) (SelfCwiseBinaryOp picks
+// scalar_product_op with Scalar(1)/other for non-integer scalars); the binary `v / s` divides.
+// Eigen >= 3.3 divides in both.  Selected by div_mode.
+#include "pitt_oracle.h"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <random>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// A3: the 4-lane reduction of Eigen's vectorised redux (predux) in the PCL binary.
+//   SSE2 predux: (a0 + a2) + (a1 + a3); SSE3 hadd: (a0 + a1) + (a2 + a3); scalar: sequential.
+inline float red4(float a0, float a1, float a2, float a3, int order) {
+    switch (order) {
+    case ORC_REDUCE_HADD: return (a0 + a1) + (a2 + a3);
+    case ORC_REDUCE_SEQ:  return ((a0 + a1) + a2) + a3;
+    default:              return (a0 + a2) + (a1 + a3);
+    }
+}
+
+// VectorXf(4).dot(Vector4f(x, y, z, 1)): products rounded separately (no FMA), reduced by red4.
+inline float plane_dot(const float c[4], float x, float y, float z, int order) {
+    return red4(c[0] * x, c[1] * y, c[2] * z, c[3] * 1.0f, order);
+}
+
+// `fabs(dot) < threshold` with threshold a double: the float is promoted (A4).
+inline bool within(float d, double th) { return (double)std::fabs(d) < th; }
+
+struct Cloud {
+    const float* x;
+    const float* y;
+    const float* z;
+    int64_t n;
+};
+
+// ------------------------------------------------------------------------------------------
+// A2: SampleConsensusModel<PointT> sampler.  rng_alg_ = boost::mt19937 seeded 12345 (random_ ==
+// false), rnd() = uniform_int<>(0, INT_MAX)(mt) which for a 32-bit engine is mt() >> 1
+// (bucket_size 2).  shuffled_indices_ = 0..N-1, rebuilt on every segment() (the model object is
+// re-created by initSACModel).
+struct Sampler {
+    std::mt19937 mt;
+    std::vector<int> shuffled;
+    explicit Sampler(int64_t n, uint32_t seed) : mt(seed), shuffled((size_t)n) {
+        std::iota(shuffled.begin(), shuffled.end(), 0);
+    }
+    int rnd() { return (int)(mt() >> 1); }
+    // drawIndexSample: for i < 3: swap(s[i], s[i + rnd() % (N - i)]); sample = s[0..2].
+    void draw(int out[3]) {
+        size_t N = shuffled.size();
+        for (unsigned i = 0; i < 3; ++i)
+            std::swap(shuffled[i], shuffled[i + ((size_t)rnd() % (N - i))]);
+        out[0] = shuffled[0];
+        out[1] = shuffled[1];
+        out[2] = shuffled[2];
+    }
+};
+
+// SampleConsensusModelPlane::isSampleGood: dy1dy2 = (p1-p0)/(p2-p0) (Array4f, componentwise);
+// good iff (dy1dy2[0] != dy1dy2[1]) || (dy1dy2[2] != dy1dy2[1])  (NaN => good).
+bool sample_good(const Cloud& c, const int s[3]) {
+    float d1x = c.x[s[1]] - c.x[s[0]], d1y = c.y[s[1]] - c.y[s[0]], d1z = c.z[s[1]] - c.z[s[0]];
+    float d2x = c.x[s[2]] - c.x[s[0]], d2y = c.y[s[2]] - c.y[s[0]], d2z = c.z[s[2]] - c.z[s[0]];
+    float rx = d1x / d2x, ry = d1y / d2y, rz = d1z / d2z;
+    return (rx != ry) || (rz != ry);
+}
+
+// SampleConsensusModelPlane::computeModelCoefficients.
+bool plane_from3(const float p0[3], const float p1[3], const float p2[3], int order, int div_mode,
+                 float out[4]) {
+    float d1x = p1[0] - p0[0], d1y = p1[1] - p0[1], d1z = p1[2] - p0[2];
+    float d2x = p2[0] - p0[0], d2y = p2[1] - p0[1], d2z = p2[2] - p0[2];
+    float rx = d1x / d2x, ry = d1y / d2y, rz = d1z / d2z;
+    if ((rx == ry) && (rz == ry)) return false;  // collinear
+    float c[4];
+    c[0] = d1y * d2z - d1z * d2y;
+    c[1] = d1z * d2x - d1x * d2z;
+    c[2] = d1x * d2y - d1y * d2x;
+    c[3] = 0.0f;
+    // model_coefficients.normalize(): *this /= norm(); norm() = sqrt(squaredNorm()) with the
+    // squaredNorm reduced by predux (dynamic-size VectorXf of size 4).
+    float nrm = std::sqrt(red4(c[0] * c[0], c[1] * c[1], c[2] * c[2], c[3] * c[3], order));
+    if (div_mode == ORC_DIV_EIGEN32) {
+        float r = 1.0f / nrm;
+        for (int i = 0; i < 4; ++i) c[i] = c[i] * r;
+    } else {
+        for (int i = 0; i < 4; ++i) c[i] = c[i] / nrm;
+    }
+    // model_coefficients[3] = -1 * head<4>().dot(p0) with p0 = (x, y, z, 1) and c[3] == 0.
+    c[3] = -1.0f * red4(c[0] * p0[0], c[1] * p0[1], c[2] * p0[2], c[3] * 1.0f, order);
+    std::memcpy(out, c, sizeof c);
+    return true;
+}
+
+bool plane_from_samples(const Cloud& cl, const int s[3], int order, int div_mode, float out[4]) {
+    float p0[3] = {cl.x[s[0]], cl.y[s[0]], cl.z[s[0]]};
+    float p1[3] = {cl.x[s[1]], cl.y[s[1]], cl.z[s[1]]};
+    float p2[3] = {cl.x[s[2]], cl.y[s[2]], cl.z[s[2]]};
+    return plane_from3(p0, p1, p2, order, div_mode, out);
+}
+
+int64_t count_within(const Cloud& c, const float coef[4], double th, int order) {
+    int64_t nr = 0;
+    for (int64_t i = 0; i < c.n; ++i)
+        if (within(plane_dot(coef, c.x[i], c.y[i], c.z[i], order), th)) ++nr;
+    return nr;
+}
+
+void select_within(const Cloud& c, const float coef[4], double th, int order,
+                   std::vector<int>& out) {
+    out.clear();
+    for (int64_t i = 0; i < c.n; ++i)
+        if (within(plane_dot(coef, c.x[i], c.y[i], c.z[i], order), th)) out.push_back((int)i);
+}
+
+// ------------------------------------------------------------------------------------------
+// A7: pcl::computeRoots2 / computeRoots / eigen33 (common/impl/eigen.hpp), float Scalar.
+float trig_atan2(float y, float x, int mode) {
+    return mode == ORC_TRIG_LIBM ? atan2f(y, x) : (float)std::atan2((double)y, (double)x);
+}
+float trig_cos(float t, int mode) { return mode == ORC_TRIG_LIBM ? cosf(t) : (float)std::cos((double)t); }
+float trig_sin(float t, int mode) { return mode == ORC_TRIG_LIBM ? sinf(t) : (float)std::sin((double)t); }
+
+void compute_roots2(float b, float c, float roots[3]) {
+    roots[0] = 0.0f;
+    float d = (float)((double)(b * b) - 4.0 * (double)c);  // Scalar(b * b - 4.0 * c)
+    if (d < 0.0) d = 0.0f;
+    float sd = std::sqrt(d);
+    roots[2] = 0.5f * (b + sd);
+    roots[1] = 0.5f * (b - sd);
+}
+
+// m is row-major 3x3 (symmetric).
+void compute_roots(const float m[9], float roots[3], int trig) {
+    const float m00 = m[0], m01 = m[1], m02 = m[2], m11 = m[4], m12 = m[5], m22 = m[8];
+    float c0 = m00 * m11 * m22 + 2.0f * m01 * m02 * m12 - m00 * m12 * m12 - m11 * m02 * m02 -
+               m22 * m01 * m01;
+    float c1 = m00 * m11 - m01 * m01 + m00 * m22 - m02 * m02 + m11 * m22 - m12 * m12;
+    float c2 = m00 + m11 + m22;
+    if (std::fabs(c0) < std::numeric_limits<float>::epsilon()) {
+        compute_roots2(c2, c1, roots);
+        return;
+    }
+    const float s_inv3 = (float)(1.0 / 3.0);
+    const float s_sqrt3 = std::sqrt(3.0f);
+    float c2_over_3 = c2 * s_inv3;
+    float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+    if (a_over_3 > 0.0f) a_over_3 = 0.0f;
+    float half_b = 0.5f * (c0 + c2_over_3 * (2.0f * c2_over_3 * c2_over_3 - c1));
+    float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+    if (q > 0.0f) q = 0.0f;
+    float rho = std::sqrt(-a_over_3);
+    float theta = trig_atan2(std::sqrt(-q), half_b, trig) * s_inv3;
+    float cos_theta = trig_cos(theta, trig);
+    float sin_theta = trig_sin(theta, trig);
+    roots[0] = c2_over_3 + 2.0f * rho * cos_theta;
+    roots[1] = c2_over_3 - rho * (cos_theta + s_sqrt3 * sin_theta);
+    roots[2] = c2_over_3 - rho * (cos_theta - s_sqrt3 * sin_theta);
+    if (roots[0] >= roots[1]) std::swap(roots[0], roots[1]);
+    if (roots[1] >= roots[2]) {
+        std::swap(roots[1], roots[2]);
+        if (roots[0] >= roots[1]) std::swap(roots[0], roots[1]);
+    }
+    if (roots[0] <= 0) compute_roots2(c2, c1, roots);
+}
+
+// Vector3f squaredNorm: fixed size 3 is not packet-vectorised, so Eigen's unrolled redux is
+// a0 + (a1 + a2).
+inline float sqnorm3(const float v[3]) { return v[0] * v[0] + (v[1] * v[1] + v[2] * v[2]); }
+inline void cross3(const float a[3], const float b[3], float o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+void eigen33(const float mat[9], int trig, float* eigenvalue, float vec[3]) {
+    float scale = 0.0f;
+    for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(mat[i]));
+    if (scale <= std::numeric_limits<float>::min()) scale = 1.0f;
+    float sm[9];
+    for (int i = 0; i < 9; ++i) sm[i] = mat[i] / scale;  // binary `mat / scale`: divides
+    float roots[3];
+    compute_roots(sm, roots, trig);
+    *eigenvalue = roots[0] * scale;
+    sm[0] -= roots[0];
+    sm[4] -= roots[0];
+    sm[8] -= roots[0];
+    float v1[3], v2[3], v3[3];
+    cross3(&sm[0], &sm[3], v1);
+    cross3(&sm[0], &sm[6], v2);
+    cross3(&sm[3], &sm[6], v3);
+    float l1 = sqnorm3(v1), l2 = sqnorm3(v2), l3 = sqnorm3(v3);
+    const float* v;
+    float l;
+    if (l1 >= l2 && l1 >= l3) { v = v1; l = l1; }
+    else if (l2 >= l1 && l2 >= l3) { v = v2; l = l2; }
+    else { v = v3; l = l3; }
+    float s = std::sqrt(l);
+    for (int i = 0; i < 3; ++i) vec[i] = v[i] / s;  // binary `vec / sqrt(len)`: divides
+}
+
+// SampleConsensusModelPlane::optimizeModelCoefficients (PCL 1.7):
+// < 4 inliers => unchanged; else computeMeanAndCovarianceMatrix (9 float accumulators, sequential
+// in inlier order, `accu /= n`), eigen33, d = -1 * (e, 0).dot(centroid).
+void optimize(const Cloud& c, const int* inl, int64_t n_inl, const float coef[4],
+              const orc_sac_params& p, float out[4]) {
+    if (n_inl < 4) {
+        std::memcpy(out, coef, 4 * sizeof(float));
+        return;
+    }
+    float a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t k = 0; k < n_inl; ++k) {
+        const float x = c.x[inl[k]], y = c.y[inl[k]], z = c.z[inl[k]];
+        a[0] += x * x;
+        a[1] += x * y;
+        a[2] += x * z;
+        a[3] += y * y;
+        a[4] += y * z;
+        a[5] += z * z;
+        a[6] += x;
+        a[7] += y;
+        a[8] += z;
+    }
+    const float fn = (float)n_inl;
+    if (p.div_mode == ORC_DIV_EIGEN32) {
+        const float r = 1.0f / fn;
+        for (int i = 0; i < 9; ++i) a[i] = a[i] * r;
+    } else {
+        for (int i = 0; i < 9; ++i) a[i] = a[i] / fn;
+    }
+    float cov[9];
+    cov[0] = a[0] - a[6] * a[6];
+    cov[1] = a[1] - a[6] * a[7];
+    cov[2] = a[2] - a[6] * a[8];
+    cov[4] = a[3] - a[7] * a[7];
+    cov[5] = a[4] - a[7] * a[8];
+    cov[8] = a[5] - a[8] * a[8];
+    cov[3] = cov[1];
+    cov[6] = cov[2];
+    cov[7] = cov[5];
+    float ev, e[3];
+    eigen33(cov, p.trig_mode, &ev, e);
+    float r[4] = {e[0], e[1], e[2], 0.0f};
+    r[3] = -1.0f * red4(r[0] * a[6], r[1] * a[7], r[2] * a[8], r[3] * 1.0f, p.reduce_order);
+    std::memcpy(out, r, sizeof r);
+}
+
+// ------------------------------------------------------------------------------------------
+// RandomSampleConsensus::computeModel + SACSegmentation::segment (A5).
+struct SegmentOut {
+    bool ok = false;
+    float coef[4] = {0, 0, 0, 0};
+    float best[4] = {0, 0, 0, 0};
+    int hypotheses = 0, best_h = -1, rejected = 0;
+    int64_t best_count = 0;
+    std::vector<int> inliers;
+    std::vector<int> counts;
+};
+
+SegmentOut segment(const Cloud& c, const orc_sac_params& p) {
+    SegmentOut o;
+    if (c.n < 3) return o;  // getSamples: "Can not select 3 unique points" => empty model
+    Sampler smp(c.n, p.seed);
+    int iterations = 0;
+    int n_best = -std::numeric_limits<int>::max();
+    double k = 1.0;
+    const double log_probability = std::log(1.0 - p.probability);
+    const double one_over_indices = 1.0 / (double)c.n;
+    unsigned skipped = 0;
+    const unsigned max_skip = (unsigned)p.max_iterations * 10u;
+    bool have_model = false;
+    int s[3];
+    while (iterations < k && skipped < max_skip) {
+        // getSamples: up to max_sample_checks_ (1000) draws until isSampleGood
+        bool got = false;
+        for (int chk = 0; chk < 1000; ++chk) {
+            smp.draw(s);
+            if (sample_good(c, s)) { got = true; break; }
+            ++o.rejected;
+        }
+        if (!got) break;  // "No samples could be selected!"
+        float coef[4];
+        if (!plane_from_samples(c, s, p.reduce_order, p.div_mode, coef)) {
+            ++skipped;
+            continue;
+        }
+        int n_in = (int)count_within(c, coef, p.threshold, p.reduce_order);
+        o.counts.push_back(n_in);
+        if (n_in > n_best) {
+            n_best = n_in;
+            have_model = true;
+            std::memcpy(o.best, coef, sizeof coef);
+            o.best_h = iterations;
+            double w = (double)n_best * one_over_indices;
+            double p_no_outliers = 1.0 - std::pow(w, 3.0);
+            p_no_outliers = std::max(std::numeric_limits<double>::epsilon(), p_no_outliers);
+            p_no_outliers = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no_outliers);
+            k = log_probability / std::log(p_no_outliers);
+        }
+        ++iterations;
+        if (iterations > p.max_iterations) break;
+    }
+    o.hypotheses = iterations;
+    if (!have_model) return o;
+    o.best_count = n_best;
+    std::vector<int> inl;
+    select_within(c, o.best, p.threshold, p.reduce_order, inl);
+    if (p.optimize) {
+        optimize(c, inl.data(), (int64_t)inl.size(), o.best, p, o.coef);
+        select_within(c, o.coef, p.threshold, p.reduce_order, inl);
+    } else {
+        std::memcpy(o.coef, o.best, sizeof o.coef);
+    }
+    o.inliers.swap(inl);
+    o.ok = true;
+    return o;
+}
+
+// ------------------------------------------------------------------------------------------
+// Support segmentation (supports_segmentation_srv.cpp).
+struct SupportOut {
+    std::vector<int> idx_map;
+    float coef[4];
+    std::vector<float> sx, sy, sz;  // support_cloud
+    std::vector<float> ox, oy, oz;  // on_support_cloud
+};
+
+}  // namespace
+
+struct orc_support_list {
+    std::vector<SupportOut> s;
+};
+
+struct orc_cluster_list {
+    std::vector<std::vector<int>> idx;
+    std::vector<std::array<float, 3>> centroid;
+};
+
+namespace {
+
+// isHorizontalPlane :161-179 (float, open intervals).
+bool is_horizontal(const float c[4], const float axis[3], float var_th) {
+    float div = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    float nx = c[0] / div, ny = c[1] / div, nz = c[2] / div;
+    float cx = ny * axis[2] - nz * axis[1];
+    float cy = nz * axis[0] - nx * axis[2];
+    float cz = nx * axis[1] - ny * axis[0];
+    float lo = -1 * var_th, hi = var_th;
+    return (cx > lo && cx < hi) && (cy > lo && cy < hi) && (cz > lo && cz < hi);
+}
+
+// createNewIdxMap :139-157 with valueBelongsToArray :131-136 as a membership bitmask.
+std::vector<int> new_idx_map(const std::vector<int>& prev, const std::vector<int>& inl, int level,
+                             int64_t n) {
+    std::vector<uint8_t> member((size_t)n, 0);
+    for (int v : inl) member[(size_t)v] = 1;
+    std::vector<int> out(prev.size());
+    int cnt = 0;
+    for (size_t p = 0; p < prev.size(); ++p) {
+        int v = prev[p];
+        if (v > level && v < 0) out[p] = v;
+        else if (v >= 0 && v < n && member[(size_t)v]) out[p] = level;
+        else out[p] = cnt++;
+    }
+    return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+void orc_mt19937(uint32_t seed, int64_t n, uint32_t* out) {
+    std::mt19937 mt(seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = (uint32_t)mt();
+}
+
+void orc_sampler_table(int64_t n, uint32_t seed, int64_t attempts, int32_t* out) {
+    Sampler smp(n, seed);
+    int s[3];
+    for (int64_t a = 0; a < attempts; ++a) {
+        smp.draw(s);
+        out[3 * a] = s[0];
+        out[3 * a + 1] = s[1];
+        out[3 * a + 2] = s[2];
+    }
+}
+
+int orc_plane_coefficients(const float p0[3], const float p1[3], const float p2[3],
+                           int32_t reduce_order, int32_t div_mode, float out[4]) {
+    return plane_from3(p0, p1, p2, reduce_order, div_mode, out) ? 1 : 0;
+}
+
+int64_t orc_count_within(const float* x, const float* y, const float* z, int64_t n,
+                         const float coeff[4], double threshold, int32_t reduce_order) {
+    Cloud c{x, y, z, n};
+    return count_within(c, coeff, threshold, reduce_order);
+}
+
+int64_t orc_select_within(const float* x, const float* y, const float* z, int64_t n,
+                          const float coeff[4], double threshold, int32_t reduce_order,
+                          int32_t* out) {
+    Cloud c{x, y, z, n};
+    std::vector<int> v;
+    select_within(c, coeff, threshold, reduce_order, v);
+    if (out) std::memcpy(out, v.data(), v.size() * sizeof(int));
+    return (int64_t)v.size();
+}
+
+int orc_eigen33(const float cov[9], int32_t trig_mode, int32_t div_mode, float* eigenvalue,
+                float vec[3]) {
+    (void)div_mode;
+    eigen33(cov, trig_mode, eigenvalue, vec);
+    return 0;
+}
+
+int orc_optimize_plane(const float* x, const float* y, const float* z, const int32_t* inliers,
+                       int64_t n_inliers, const float coeff[4], const orc_sac_params* p,
+                       float out[4]) {
+    Cloud c{x, y, z, 0};
+    optimize(c, inliers, n_inliers, coeff, *p, out);
+    return 0;
+}
+
+int orc_plane_segment(const float* x, const float* y, const float* z, int64_t n,
+                      const orc_sac_params* p, int32_t* inliers_out, orc_plane_result* res,
+                      int32_t* hyp_counts) {
+    Cloud c{x, y, z, n};
+    SegmentOut o = segment(c, *p);
+    std::memset(res, 0, sizeof *res);
+    res->hypotheses = o.hypotheses;
+    res->best_hypothesis = o.best_h;
+    res->rejected_samples = o.rejected;
+    res->best_count = o.best_count;
+    std::memcpy(res->best_coefficients, o.best, sizeof o.best);
+    if (hyp_counts)
+        std::memcpy(hyp_counts, o.counts.data(), o.counts.size() * sizeof(int));
+    if (!o.ok) return 1;  // PCL: inliers.indices.clear(); model_coefficients.values.clear()
+    res->n_coeff = 4;
+    std::memcpy(res->coefficients, o.coef, sizeof o.coef);
+    res->n_inliers = (int64_t)o.inliers.size();
+    if (inliers_out) std::memcpy(inliers_out, o.inliers.data(), o.inliers.size() * sizeof(int));
+    return 0;
+}
+
+// findSupports :241-361.
+orc_support_list* orc_find_supports(const float* x, const float* y, const float* z, int64_t n,
+                                    const orc_support_params* sp) {
+    orc_support_list* L = new orc_support_list;
+    orc_sac_params p;
+    p.threshold = (double)sp->ransac_distance_threshold;
+    p.max_iterations = sp->ransac_max_iterations;
+    p.probability = 0.99;
+    p.seed = 12345u;
+    p.optimize = 1;
+    p.reduce_order = sp->reduce_order;
+    p.trig_mode = sp->trig_mode;
+    p.div_mode = sp->div_mode;
+
+    std::vector<float> ix(x, x + n), iy(y, y + n), iz(z, z + n);  // iterativeCloud
+    std::vector<int> prev_map;
+    int level = -2, cnt = 0;
+    const float nf = (float)n;
+    while (true) {
+        Cloud ic{ix.data(), iy.data(), iz.data(), (int64_t)ix.size()};
+        SegmentOut o = segment(ic, p);
+        const std::vector<int>& inl = o.inliers;
+        if (inl.empty()) break;
+        if ((float)ix.size() < nf * sp->min_iterative_cloud_percentage) break;
+        if ((float)inl.size() < nf * sp->min_iterative_plane_percentage) break;
+
+        std::vector<int> inliers_idx;
+        if (!cnt) {
+            inliers_idx.resize((size_t)n);
+            std::iota(inliers_idx.begin(), inliers_idx.end(), 0);
+        } else {
+            inliers_idx = prev_map;
+        }
+        // removePlaneInliner :114-127: positive extract (inlier order), then negative in place.
+        SupportOut so;
+        so.sx.reserve(inl.size());
+        for (int i : inl) {
+            so.sx.push_back(ix[i]);
+            so.sy.push_back(iy[i]);
+            so.sz.push_back(iz[i]);
+        }
+        {
+            std::vector<uint8_t> rm(ix.size(), 0);
+            for (int i : inl) rm[(size_t)i] = 1;
+            size_t w = 0;
+            for (size_t r = 0; r < ix.size(); ++r)
+                if (!rm[r]) { ix[w] = ix[r]; iy[w] = iy[r]; iz[w] = iz[r]; ++w; }
+            ix.resize(w); iy.resize(w); iz.resize(w);
+        }
+        if (is_horizontal(o.coef, sp->horizontal_axis, sp->horizontal_variance_threshold)) {
+            std::vector<int> nm = new_idx_map(inliers_idx, inl, level, n);
+            // getPointOnPlane :187-238 (double bbox with the `else if`, double z sum).
+            const double inf = std::numeric_limits<double>::infinity();
+            double xMax = -inf, yMax = -inf, zMed = 0, xMin = inf, yMin = inf;
+            for (size_t i = 0; i < so.sx.size(); ++i) {
+                if (so.sx[i] > xMax) xMax = so.sx[i];
+                else if (so.sx[i] < xMin) xMin = so.sx[i];
+                if (so.sy[i] > yMax) yMax = so.sy[i];
+                else if (so.sy[i] < yMin) yMin = so.sy[i];
+                zMed += so.sz[i];
+            }
+            xMax -= sp->edge_remove_offset[0];
+            xMin += sp->edge_remove_offset[0];
+            yMax -= sp->edge_remove_offset[1];
+            yMin += sp->edge_remove_offset[1];
+            zMed = zMed / (double)so.sx.size() + sp->edge_remove_offset[2];
+            for (int64_t i = 0; i < n; ++i) {
+                if (nm[(size_t)i] == level) continue;  // removingIdx membership
+                if (x[i] > xMin && x[i] < xMax && z[i] > zMed && y[i] > yMin && y[i] < yMax) {
+                    so.ox.push_back(x[i]);
+                    so.oy.push_back(y[i]);
+                    so.oz.push_back(z[i]);
+                }
+            }
+            std::memcpy(so.coef, o.coef, sizeof so.coef);
+            so.idx_map = nm;
+            prev_map.swap(nm);
+            L->s.push_back(std::move(so));
+        } else {
+            prev_map = new_idx_map(inliers_idx, inl, -1, n);
+        }
+        ++cnt;
+        --level;
+    }
+    return L;
+}
+
+int32_t orc_support_count(const orc_support_list* L) { return (int32_t)L->s.size(); }
+
+int orc_support_get(const orc_support_list* L, int32_t s, int32_t* idx_map, float coeff[4],
+                    int64_t* n_support, int64_t* n_on_support) {
+    if (s < 0 || s >= (int32_t)L->s.size()) return -1;
+    const SupportOut& so = L->s[(size_t)s];
+    if (idx_map) std::memcpy(idx_map, so.idx_map.data(), so.idx_map.size() * sizeof(int));
+    if (coeff) std::memcpy(coeff, so.coef, sizeof so.coef);
+    if (n_support) *n_support = (int64_t)so.sx.size();
+    if (n_on_support) *n_on_support = (int64_t)so.ox.size();
+    return 0;
+}
+
+int orc_support_cloud(const orc_support_list* L, int32_t s, int32_t which, float* x, float* y,
+                      float* z) {
+    if (s < 0 || s >= (int32_t)L->s.size()) return -1;
+    const SupportOut& so = L->s[(size_t)s];
+    const std::vector<float>& a = which ? so.ox : so.sx;
+    const std::vector<float>& b = which ? so.oy : so.sy;
+    const std::vector<float>& c = which ? so.oz : so.sz;
+    std::memcpy(x, a.data(), a.size() * sizeof(float));
+    std::memcpy(y, b.data(), b.size() * sizeof(float));
+    std::memcpy(z, c.data(), c.size() * sizeof(float));
+    return 0;
+}
+
+void orc_support_free(orc_support_list* L) { delete L; }
+
+// clusterize :38-108 + extractEuclideanClusters (A8).
+orc_cluster_list* orc_euclidean_clusters(const float* x, const float* y, const float* z, int64_t n,
+                                         double tolerance, double min_rate, double max_rate,
+                                         int32_t min_input_size) {
+    orc_cluster_list* L = new orc_cluster_list;
+    if (n < (int64_t)min_input_size) return L;  // :54
+    const unsigned min_pts = (unsigned)(int)std::round((double)n * min_rate);  // :64
+    const unsigned max_pts = (unsigned)(int)std::round((double)n * max_rate);  // :65
+    // extract(): tolerance -> float; KdTreeFLANN::radiusSearch: r2 = (float)((double)tol^2).
+    const float tol_f = (float)tolerance;
+    const float r2 = (float)((double)tol_f * (double)tol_f);
+    // Uniform grid (cell slightly above the radius) for candidate generation; the predicate is
+    // FLANN L2_Simple: ((dx*dx + dy*dy) + dz*dz) < r2 in float.
+    double cell = (double)tol_f * 1.01;
+    double mnx = 1e300, mny = 1e300, mnz = 1e300;
+    for (int64_t i = 0; i < n; ++i) {
+        mnx = std::min(mnx, (double)x[i]);
+        mny = std::min(mny, (double)y[i]);
+        mnz = std::min(mnz, (double)z[i]);
+    }
+    auto key = [&](int64_t gx, int64_t gy, int64_t gz) {
+        return (uint64_t)((gx & 0x1FFFFF) | ((gy & 0x1FFFFF) << 21) | ((gz & 0x1FFFFF) << 42));
+    };
+    std::unordered_map<uint64_t, std::vector<int>> grid;
+    std::vector<int64_t> gxs((size_t)n), gys((size_t)n), gzs((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        gxs[i] = (int64_t)std::floor(((double)x[i] - mnx) / cell);
+        gys[i] = (int64_t)std::floor(((double)y[i] - mny) / cell);
+        gzs[i] = (int64_t)std::floor(((double)z[i] - mnz) / cell);
+        grid[key(gxs[i], gys[i], gzs[i])].push_back((int)i);
+    }
+    std::vector<uint8_t> processed((size_t)n, 0);
+    std::vector<std::pair<float, int>> nn;
+    std::vector<std::vector<int>> clusters;
+    for (int64_t i = 0; i < n; ++i) {
+        if (processed[i]) continue;
+        std::vector<int> q;
+        size_t sq = 0;
+        q.push_back((int)i);
+        processed[i] = 1;
+        while (sq < q.size()) {
+            const int qi = q[sq];
+            nn.clear();
+            for (int dx = -1; dx <= 1; ++dx)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dz = -1; dz <= 1; ++dz) {
+                        auto it = grid.find(key(gxs[qi] + dx, gys[qi] + dy, gzs[qi] + dz));
+                        if (it == grid.end()) continue;
+                        for (int j : it->second) {
+                            float ex = x[qi] - x[j], ey = y[qi] - y[j], ez = z[qi] - z[j];
+                            float d = ex * ex + ey * ey + ez * ez;
+                            if (d < r2) nn.emplace_back(d, j);
+                        }
+                    }
+            std::sort(nn.begin(), nn.end());  // sorted results (search::KdTree sorted_ = true)
+            for (size_t j = 1; j < nn.size(); ++j) {  // nn_start_idx = 1
+                const int id = nn[j].second;
+                if (processed[id]) continue;
+                q.push_back(id);
+                processed[id] = 1;
+            }
+            ++sq;
+        }
+        if (q.size() >= min_pts && q.size() <= max_pts) {
+            std::sort(q.begin(), q.end());
+            q.erase(std::unique(q.begin(), q.end()), q.end());
+            clusters.push_back(std::move(q));
+        }
+    }
+    // EuclideanClusterExtraction::extract: std::sort(rbegin, rend, size <)
+    std::sort(clusters.rbegin(), clusters.rend(),
+              [](const std::vector<int>& a, const std::vector<int>& b) { return a.size() < b.size(); });
+    for (auto& c : clusters) {
+        float sx = 0, sy = 0, sz = 0;
+        int cnt = 1;  // Q7: the handler starts its counter at 1
+        for (int id : c) {
+            sx += x[id];
+            sy += y[id];
+            sz += z[id];
+            cnt++;
+        }
+        L->centroid.push_back({sx / cnt, sy / cnt, sz / cnt});
+        L->idx.push_back(std::move(c));
+    }
+    return L;
+}
+
+int32_t orc_cluster_count(const orc_cluster_list* L) { return (int32_t)L->idx.size(); }
+int64_t orc_cluster_size(const orc_cluster_list* L, int32_t c) {
+    return (c < 0 || c >= (int32_t)L->idx.size()) ? -1 : (int64_t)L->idx[(size_t)c].size();
+}
+int orc_cluster_get(const orc_cluster_list* L, int32_t c, int32_t* idx, float centroid[3]) {
+    if (c < 0 || c >= (int32_t)L->idx.size()) return -1;
+    const auto& v = L->idx[(size_t)c];
+    if (idx) std::memcpy(idx, v.data(), v.size() * sizeof(int));
+    if (centroid) std::memcpy(centroid, L->centroid[(size_t)c].data(), 3 * sizeof(float));
+    return 0;
+}
+void orc_cluster_free(orc_cluster_list* L) { delete L; }
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+/*
+ * pitt_oracle.h -- CPU restatement of the reference's PCL path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This library is the parity checker for the MI355X path.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  It is never linked into, or called by, the
+ * product library (pitt_object_table_segmentation_amd/csrc).
+ *
+ * Pinning status: PARTIALLY PINNED.  The reference ships no tests, no fixtures and no golden
+ * vectors, and its arithmetic lives in PCL 1.7 which is absent here (s8c).
+ * What is pinned: the mt19937 stream (C++ standard KAT, 10000th draw of the default seed =
+ * 4123659995) and the reference's rnd() draws for seed 12345; analytic plane / cluster /
+ * support known-answer cases (tests/test_oracle_kat.py).  What is NOT pinnable here: the
+ * float reduction order of PCL's Eigen build (A3), Eigen 3.2 division forms (A9) and the
+ * host libm trig used by eigen33 (A7).  Each of these is a switch below.
+ */
+#ifndef PITT_ORACLE_H
+#define PITT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A3: 4-lane Eigen reduction order of dot()/squaredNorm() in the PCL binary. */
+enum { ORC_REDUCE_SSE2 = 0, ORC_REDUCE_HADD = 1, ORC_REDUCE_SEQ = 2 };
+/* A7: trig used inside eigen33: CR = float result of the double-evaluated function;
+ *     LIBM = the host's atan2f/cosf/sinf (what PCL called on its platform). */
+enum { ORC_TRIG_CR = 0, ORC_TRIG_LIBM = 1 };
+/* A9: Eigen 3.2 compound `v /= s` multiplies by (1/s); Eigen >= 3.3 divides. */
+enum { ORC_DIV_EIGEN32 = 0, ORC_DIV_TRUE = 1 };
+
+typedef struct {
+    double   threshold;       /* SACSegmentation::setDistanceThreshold (double) */
+    int32_t  max_iterations;  /* setMaxIterations */
+    double   probability;     /* RandomSampleConsensus probability_ (PCL default 0.99) */
+    uint32_t seed;            /* SampleConsensusModel rng seed (12345 when random_ == false) */
+    int32_t  optimize;        /* setOptimizeCoefficients */
+    int32_t  reduce_order;    /* ORC_REDUCE_* */
+    int32_t  trig_mode;       /* ORC_TRIG_* */
+    int32_t  div_mode;        /* ORC_DIV_* */
+} orc_sac_params;
+
+typedef struct {
+    float    coefficients[4];      /* final (refined if optimize) coefficients */
+    int32_t  n_coeff;              /* 4, or 0 when no model (PCL clears the vector) */
+    int32_t  hypotheses;           /* T: hypotheses PCL evaluated (countWithinDistance calls) */
+    int64_t  n_inliers;            /* final inlier count */
+    int32_t  best_hypothesis;      /* index of the winning hypothesis */
+    int32_t  rejected_samples;     /* isSampleGood rejections */
+    int64_t  best_count;           /* countWithinDistance of the winning hypothesis */
+    float    best_coefficients[4]; /* unrefined winning coefficients */
+} orc_plane_result;
+
+/* --- RNG / sampler (A2) --- */
+void    orc_mt19937(uint32_t seed, int64_t n, uint32_t* out);
+/* attempts*3 indices of SampleConsensusModel::drawIndexSample for a cloud of n points */
+void    orc_sampler_table(int64_t n, uint32_t seed, int64_t attempts, int32_t* out);
+
+/* --- plane model primitives (SampleConsensusModelPlane) --- */
+int     orc_plane_coefficients(const float p0[3], const float p1[3], const float p2[3],
+                               int32_t reduce_order, int32_t div_mode, float out[4]);
+int64_t orc_count_within(const float* x, const float* y, const float* z, int64_t n,
+                         const float coeff[4], double threshold, int32_t reduce_order);
+int64_t orc_select_within(const float* x, const float* y, const float* z, int64_t n,
+                          const float coeff[4], double threshold, int32_t reduce_order,
+                          int32_t* out);
+int     orc_eigen33(const float cov[9], int32_t trig_mode, int32_t div_mode,
+                    float* eigenvalue, float vec[3]);
+int     orc_optimize_plane(const float* x, const float* y, const float* z,
+                           const int32_t* inliers, int64_t n_inliers, const float coeff[4],
+                           const orc_sac_params* p, float out[4]);
+
+/* --- SACSegmentation::segment (plane, RANSAC) --- */
+int     orc_plane_segment(const float* x, const float* y, const float* z, int64_t n,
+                          const orc_sac_params* p, int32_t* inliers_out /* cap n */,
+                          orc_plane_result* res, int32_t* hyp_counts /* optional, cap max_it+1 */);
+
+/* --- support segmentation service (supports_segmentation_srv.cpp:241-361) --- */
+typedef struct {
+    float   min_iterative_cloud_percentage;  /* 0.03 */
+    float   min_iterative_plane_percentage;  /* 0.03 */
+    float   horizontal_variance_threshold;   /* 0.09 */
+    float   ransac_distance_threshold;       /* 0.02f */
+    int32_t ransac_max_iterations;           /* 10 */
+    float   horizontal_axis[3];              /* 0,0,-1 */
+    float   edge_remove_offset[3];           /* 0.02,0.02,0.005 */
+    int32_t reduce_order, trig_mode, div_mode;
+} orc_support_params;
+
+typedef struct orc_support_list orc_support_list;
+orc_support_list* orc_find_supports(const float* x, const float* y, const float* z, int64_t n,
+                                    const orc_support_params* p);
+int32_t orc_support_count(const orc_support_list*);
+/* copies support s: inliers (idx map, n ints), coefficients[4], sizes of the two clouds */
+int     orc_support_get(const orc_support_list*, int32_t s, int32_t* idx_map /* cap n */,
+                        float coeff[4], int64_t* n_support, int64_t* n_on_support);
+int     orc_support_cloud(const orc_support_list*, int32_t s, int32_t which /*0 support,1 on*/,
+                          float* x, float* y, float* z);
+void    orc_support_free(orc_support_list*);
+
+/* --- Euclidean cluster extraction (cluster_segmentation_srv.cpp:38-108) --- */
+typedef struct orc_cluster_list orc_cluster_list;
+orc_cluster_list* orc_euclidean_clusters(const float* x, const float* y, const float* z, int64_t n,
+                                         double tolerance, double min_rate, double max_rate,
+                                         int32_t min_input_size);
+int32_t orc_cluster_count(const orc_cluster_list*);
+int64_t orc_cluster_size(const orc_cluster_list*, int32_t c);
+int     orc_cluster_get(const orc_cluster_list*, int32_t c, int32_t* idx, float centroid[3]);
+void    orc_cluster_free(orc_cluster_list*);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

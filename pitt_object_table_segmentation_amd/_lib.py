@@ -1,0 +1,179 @@
+"""ctypes binding of the C ABI in include/pitt_seg.h (libpitt_seg.so, built in-tree).
+
+The library is the product: every segmentation call in this package goes through it.  If the
+shared object is missing or cannot be loaded, import fails loudly -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib.util
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpitt_seg.so")
+
+PITT_OK = 0
+PITT_NO_MODEL = 1
+PITT_E_INVALID = -1
+PITT_E_HIP = -2
+PITT_E_NOMEM = -3
+PITT_E_SAMPLER = -4
+PITT_E_NODEVICE = -5
+PITT_TILE_POINTS = 2048
+PITT_FLAG_K_NEAR_INTEGER = 1
+
+REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
+DIV_EIGEN32, DIV_TRUE = 0, 1
+SCENE_TABLE, SCENE_CLUTTER, SCENE_TABLE_NAN = 0, 1, 2
+
+
+class SacParams(ctypes.Structure):
+    _fields_ = [
+        ("threshold", ctypes.c_double),
+        ("max_iterations", ctypes.c_int32),
+        ("probability", ctypes.c_double),
+        ("seed", ctypes.c_uint32),
+        ("optimize", ctypes.c_int32),
+        ("reduce_order", ctypes.c_int32),
+        ("div_mode", ctypes.c_int32),
+        ("sampler_slack", ctypes.c_int32),
+    ]
+
+
+class PlaneResult(ctypes.Structure):
+    _fields_ = [
+        ("coefficients", ctypes.c_float * 4),
+        ("n_coeff", ctypes.c_int32),
+        ("status", ctypes.c_int32),
+        ("n_inliers", ctypes.c_int64),
+        ("hypotheses", ctypes.c_int32),
+        ("best_hypothesis", ctypes.c_int32),
+        ("best_count", ctypes.c_int64),
+        ("rejected_samples", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+    ]
+
+
+class Frames(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("z", ctypes.c_void_p),
+        ("offsets", ctypes.POINTER(ctypes.c_int64)),
+        ("counts", ctypes.POINTER(ctypes.c_int64)),
+        ("n_frames", ctypes.c_int32),
+        ("capacity", ctypes.c_int64),
+    ]
+
+
+class SupportParams(ctypes.Structure):
+    _fields_ = [
+        ("min_iterative_cloud_percentage", ctypes.c_float),
+        ("min_iterative_plane_percentage", ctypes.c_float),
+        ("horizontal_variance_threshold", ctypes.c_float),
+        ("ransac_distance_threshold", ctypes.c_float),
+        ("ransac_max_iterations", ctypes.c_int32),
+        ("horizontal_axis", ctypes.c_float * 3),
+        ("edge_remove_offset", ctypes.c_float * 3),
+        ("reduce_order", ctypes.c_int32),
+        ("div_mode", ctypes.c_int32),
+    ]
+
+
+class Support(ctypes.Structure):
+    _fields_ = [
+        ("n_points", ctypes.c_int32),
+        ("idx_map", ctypes.POINTER(ctypes.c_int32)),
+        ("coefficients", ctypes.c_float * 4),
+        ("n_support", ctypes.c_int64),
+        ("support_xyz", ctypes.POINTER(ctypes.c_float)),
+        ("n_on_support", ctypes.c_int64),
+        ("on_support_xyz", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class SupportList(ctypes.Structure):
+    _fields_ = [
+        ("n_supports", ctypes.c_int32),
+        ("supports", ctypes.POINTER(Support)),
+        ("iterations", ctypes.c_int32),
+    ]
+
+
+class Cluster(ctypes.Structure):
+    _fields_ = [
+        ("size", ctypes.c_int64),
+        ("indices", ctypes.POINTER(ctypes.c_int32)),
+        ("sum_xyz", ctypes.c_float * 3),
+    ]
+
+
+class ClusterList(ctypes.Structure):
+    _fields_ = [
+        ("n_clusters", ctypes.c_int32),
+        ("clusters", ctypes.POINTER(Cluster)),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype, argtypes); every symbol declared in include/pitt_seg.h
+SIGNATURES = {
+    "pitt_abi_version": (_i32, []),
+    "pitt_sac_params_default": (None, [ctypes.POINTER(SacParams)]),
+    "pitt_create": (_i32, [ctypes.POINTER(_vp), _i32]),
+    "pitt_destroy": (None, [_vp]),
+    "pitt_set_stream": (_i32, [_vp, _vp]),
+    "pitt_get_stream": (_vp, [_vp]),
+    "pitt_last_error": (ctypes.c_char_p, [_vp]),
+    "pitt_plane_segment": (_i32, [_vp, _f32p, _i64, _i32, ctypes.POINTER(SacParams), _i32p, _i64p,
+                                  _f32p, _i32p]),
+    "pitt_plane_segment_batch": (_i32, [_vp, ctypes.POINTER(Frames), ctypes.POINTER(SacParams),
+                                        ctypes.POINTER(PlaneResult), _vp]),
+    "pitt_last_hypothesis_counts": (_i32, [_vp, _i32, _i32p, _i32]),
+    "pitt_extract_indices": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _i64p]),
+    "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
+    "pitt_find_supports": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.POINTER(SupportParams),
+                                  ctypes.POINTER(SupportList)]),
+    "pitt_euclidean_clusters": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.c_double, _i32, _i32,
+                                       ctypes.POINTER(ClusterList)]),
+    "pitt_synth_frame": (_i32, [_i32, ctypes.c_uint64, _i32, _i32, _f32p, _f32p, _f32p]),
+    "pitt_synth_fused": (_i32, [ctypes.c_uint64, _i32, _i32, _i32, _f32p, _f32p, _f32p]),
+    "pitt_profile_enable": (_i32, [_vp, _i32]),
+    "pitt_profile_get": (_i32, [_vp, ctypes.c_char_p, _i64p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double)]),
+    "pitt_profile_reset": (_i32, [_vp]),
+}
+
+
+def _preload_torch_hip_runtime() -> None:
+    """Make libpitt_seg.so bind to the HIP runtime torch uses (same SONAME libamdhip64.so.7),
+    so a process that also uses torch holds exactly one HIP runtime."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        return
+    rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+    _preload_torch_hip_runtime()
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = load()

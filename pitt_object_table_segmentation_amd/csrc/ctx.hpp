@@ -1,0 +1,97 @@
+// ctx.hpp -- pitt_ctx: device, stream, scratch arena, sampler-table cache, kernel profiler.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pitt_seg.h"
+
+#define PITT_HIP_TRY(expr)                                                          \
+    do {                                                                            \
+        hipError_t e_ = (expr);                                                     \
+        if (e_ != hipSuccess) {                                                     \
+            return ctx->fail(PITT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+        }                                                                           \
+    } while (0)
+
+namespace pitt {
+
+// One growable device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct ProfRec {
+    std::string name;
+    hipEvent_t a = nullptr, b = nullptr;
+    double bytes = 0;
+};
+
+struct ProfTotal {
+    int64_t launches = 0;
+    double ms = 0;
+    double bytes = 0;
+};
+
+}  // namespace pitt
+
+struct pitt_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // scratch arena: named growable buffers (contents undefined between calls)
+    std::unordered_map<std::string, pitt::DevBuf> bufs;
+    std::unordered_map<std::string, std::pair<void*, size_t>> host_pinned;
+
+    // sampler tables (host) keyed by (n, seed, attempts)
+    std::map<std::tuple<int64_t, uint32_t, int64_t>, std::vector<int32_t>> tables;
+    // device pool of the last batch's tables
+    std::vector<std::tuple<int64_t, uint32_t, int64_t>> pool_keys;
+
+    // profiling
+    bool prof = false;
+    std::vector<pitt::ProfRec> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, pitt::ProfTotal> totals;
+
+    // last batch (debug / parity hooks)
+    int32_t last_hcap = 0;
+    int32_t last_frames = 0;
+
+    // results kept alive for list-returning calls
+    std::vector<std::vector<int32_t>> keep_i32;
+    std::vector<std::vector<float>> keep_f32;
+    std::vector<pitt_support> keep_supports;
+    std::vector<pitt_cluster> keep_clusters;
+
+    int fail(int code, const std::string& msg) {
+        err = msg;
+        return code;
+    }
+    // Device scratch buffer `name` of at least `bytes` (grows, never shrinks).
+    void* buf(const std::string& name, size_t bytes);
+    // Pinned host buffer.
+    void* pinned(const std::string& name, size_t bytes);
+
+    // Profiler hooks around a launch.
+    int prof_begin(const char* name, double bytes);
+    void prof_end(int rec);
+    void prof_set_bytes(int rec, double bytes) {
+        if (rec >= 0 && rec < (int)pending.size()) pending[(size_t)rec].bytes = bytes;
+    }
+    int prof_collect();
+};
+
+namespace pitt {
+// Host sampler table (A2): attempts*3 indices of drawIndexSample for n points.
+const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts);
+// Smallest float t with (double)|d| < th  <=>  |d| < t for every float d (A4).
+float float_threshold(double th);
+}  // namespace pitt

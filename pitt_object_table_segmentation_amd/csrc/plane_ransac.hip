@@ -1,0 +1,746 @@
+// plane_ransac.hip -- SACSegmentation::segment (SACMODEL_PLANE, SAC_RANSAC) for batches of frames
+// on gfx950.  Replaces the PCL call at src/segmentation_services/plane_segmentation_srv.cpp:67 and
+// supports_segmentation_srv.cpp:110 (reference paths).  Pipeline per batch:
+//
+//   k_hypothesize   sampler-table attempts -> isSampleGood -> compacted plane hypotheses (A2)
+//   k_score  x C    inlier counts of H hypotheses per (frame, 2048-point tile), points held in
+//                   VGPRs and reused across the H hypotheses, wave ballot + s_bcnt1 counting
+//   k_replay x C    PCL's serial best / adaptive-k logic over the chunk's counts (A5); builds
+//                   the next chunk's active-frame list on the device (no host round trip)
+//   k_tile_offsets  exclusive scan of the winning hypothesis' per-tile counts
+//   k_select_xyz    ordered compaction of the winning model's inliers (x, y, z)
+//   k_cov_eigen     9 float accumulators in exact PCL order (one lane each) + eigen33 (A6, A7)
+//   k_count_final / k_tile_offsets / k_write_final   refined-model inlier list (ascending)
+//   k_finalize      per-frame pitt_plane_result
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "device_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pitt {
+
+constexpr int kMaxAttempts = 8192;
+constexpr int kMaxAttemptWords = kMaxAttempts / 32;
+constexpr int kCovFramesPerWave = 7;  // 7 frames x 9 accumulators = 63 lanes
+
+struct FrameMeta {
+    int64_t off;    // first point (multiple of 4)
+    int64_t n;      // points
+    int64_t tab;    // sampler table offset (int32 units)
+    int32_t tiles;  // ceil(n / kTile)
+    int32_t pad;
+};
+
+struct FrameState {
+    double k;
+    int32_t it, best_count, best_h, done;
+    int32_t n_avail, exhausted, flags, status;
+    int32_t has_model, need_refine, pad0, pad1;
+};
+
+struct ChunkStat {
+    int32_t frames;
+    int32_t tiles;
+    int64_t points;
+};
+
+// ------------------------------------------------------------------------------------------
+// k_hypothesize: one block per frame.  Attempt a uses table triple a (the sampler's draws depend
+// only on (n, seed) until a sample is rejected; rejected attempts are simply skipped and
+// hypothesis h is the h-th good attempt).  getSamples gives up after 1000 consecutive rejects.
+template <int ORDER, int DIV>
+__global__ __launch_bounds__(kBlock) void k_hypothesize(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const int32_t* __restrict__ tables, int A, int hcap,
+    int runnable_all, float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt,
+    FrameState* __restrict__ st, int32_t* __restrict__ list0, int32_t* __restrict__ cnt0,
+    ChunkStat* __restrict__ stat0) {
+    __shared__ uint32_t bits[kMaxAttemptWords];
+    __shared__ int32_t wpre[kMaxAttemptWords];
+    __shared__ int32_t s_avail, s_exh;
+    const int f = blockIdx.x;
+    const FrameMeta m = meta[f];
+    const int nw = (A + 31) >> 5;
+    for (int i = threadIdx.x; i < nw; i += kBlock) bits[i] = 0u;
+    __syncthreads();
+    const bool runnable = runnable_all && m.n >= 3;
+    const float* x = X + m.off;
+    const float* y = Y + m.off;
+    const float* z = Z + m.off;
+    const int32_t* tab = tables + m.tab;
+    if (runnable) {
+        for (int a = threadIdx.x; a < A; a += kBlock) {
+            const int i0 = tab[3 * a], i1 = tab[3 * a + 1], i2 = tab[3 * a + 2];
+            float3 p0 = make_float3(x[i0], y[i0], z[i0]);
+            float3 p1 = make_float3(x[i1], y[i1], z[i1]);
+            float3 p2 = make_float3(x[i2], y[i2], z[i2]);
+            if (sample_good(p0, p1, p2)) atomicOr(&bits[a >> 5], 1u << (a & 31));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int good = 0, run = 0, avail = -1;
+        for (int w = 0; w < nw; ++w) {
+            const uint32_t word = bits[w];
+            const int nbits = min(32, A - 32 * w);
+            wpre[w] = good;
+            if (avail >= 0) continue;
+            if (word == 0u) {
+                run += nbits;
+                if (run >= 1000) avail = good;
+                continue;
+            }
+            const int tz = __builtin_ctz(word);
+            if (run + tz >= 1000) { avail = good; continue; }
+            good += __builtin_popcount(word);
+            const int hb = 31 - __builtin_clz(word);
+            run = nbits - 1 - hb;
+        }
+        int exh = 0;
+        if (avail < 0) {
+            avail = good;
+            exh = (run < 1000 && good < hcap) ? 1 : 0;
+        }
+        s_avail = min(avail, hcap);
+        s_exh = exh;
+    }
+    __syncthreads();
+    const int avail = s_avail;
+    if (runnable) {
+        for (int a = threadIdx.x; a < A; a += kBlock) {
+            const uint32_t word = bits[a >> 5];
+            if (!((word >> (a & 31)) & 1u)) continue;
+            const int h = wpre[a >> 5] + __builtin_popcount(word & ((1u << (a & 31)) - 1u));
+            if (h >= avail) continue;
+            const int i0 = tab[3 * a], i1 = tab[3 * a + 1], i2 = tab[3 * a + 2];
+            float3 p0 = make_float3(x[i0], y[i0], z[i0]);
+            float3 p1 = make_float3(x[i1], y[i1], z[i1]);
+            float3 p2 = make_float3(x[i2], y[i2], z[i2]);
+            hyp_coef[(int64_t)f * hcap + h] = plane_from3<ORDER, DIV>(p0, p1, p2);
+            hyp_attempt[(int64_t)f * hcap + h] = a;
+        }
+    }
+    if (threadIdx.x == 0) {
+        FrameState s;
+        s.k = 1.0;
+        s.it = 0;
+        s.best_count = -INT_MAX;
+        s.best_h = -1;
+        s.n_avail = avail;
+        s.exhausted = s_exh;
+        s.flags = 0;
+        s.status = PITT_OK;
+        s.has_model = 0;
+        s.need_refine = 0;
+        s.pad0 = s.pad1 = 0;
+        s.done = 0;
+        if (!runnable) {
+            s.done = 1;
+            s.status = PITT_NO_MODEL;
+        } else if (avail == 0) {
+            s.done = 1;
+            s.status = s_exh ? PITT_E_SAMPLER : PITT_NO_MODEL;
+            s.pad0 = s_exh ? 0 : 1;
+        }
+        st[f] = s;
+        if (!s.done) {
+            const int idx = atomicAdd(cnt0, 1);
+            list0[idx] = f;
+            atomicAdd(&stat0->tiles, m.tiles);
+            atomicAdd((unsigned long long*)&stat0->points, (unsigned long long)m.n);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_score: persistent grid over (active frame, tile).  Each thread keeps 8 points (2 x float4 of
+// each coordinate plane) in registers and scores all H hypotheses of the chunk against them:
+// 3 mul + 3 add + 1 cmp per point-hypothesis on the VALU, the count on the scalar unit
+// (ballot -> s_bcnt1), one LDS add per wave and hypothesis.
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_score(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0,
+    int H, float thf, int32_t* __restrict__ tile_counts) {
+    __shared__ int32_t lds_cnt[kMaxChunk];
+    const int lane = threadIdx.x & 63;
+    const int64_t items = (int64_t)(*cnt) * tiles_max;
+    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = __builtin_amdgcn_readfirstlane(list[item / tiles_max]);
+        const int t = (int)(item % tiles_max);
+        const FrameMeta m = meta[f];
+        if (t >= m.tiles) continue;
+        for (int i = threadIdx.x; i < H; i += kBlock) lds_cnt[i] = 0;
+        const int64_t tb = (int64_t)t * kTile;
+        const float* x = X + m.off + tb;
+        const float* y = Y + m.off + tb;
+        const float* z = Z + m.off + tb;
+        float px[8], py[8], pz[8];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int li = g * 1024 + threadIdx.x * 4;
+            const float4 vx = *reinterpret_cast<const float4*>(x + li);
+            const float4 vy = *reinterpret_cast<const float4*>(y + li);
+            const float4 vz = *reinterpret_cast<const float4*>(z + li);
+            px[4 * g + 0] = vx.x; px[4 * g + 1] = vx.y; px[4 * g + 2] = vx.z; px[4 * g + 3] = vx.w;
+            py[4 * g + 0] = vy.x; py[4 * g + 1] = vy.y; py[4 * g + 2] = vy.z; py[4 * g + 3] = vy.w;
+            pz[4 * g + 0] = vz.x; pz[4 * g + 1] = vz.y; pz[4 * g + 2] = vz.z; pz[4 * g + 3] = vz.w;
+        }
+        const int64_t rem = m.n - tb;
+        if (rem < kTile) {  // tail tile: points past the frame never count (NaN fails every test)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    if (g * 1024 + threadIdx.x * 4 + s >= rem) px[4 * g + s] = __builtin_nanf("");
+        }
+        __syncthreads();
+        const float4* hc = hyp_coef + (int64_t)f * hcap + h0;
+        for (int h = 0; h < H; ++h) {
+            const float4 c = hc[h];
+            int wc = 0;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const float d = plane_dot<ORDER>(c, px[p], py[p], pz[p]);
+                wc += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fabsf(d) < thf));
+            }
+            if (lane == 0) atomicAdd(&lds_cnt[h], wc);
+        }
+        __syncthreads();
+        int32_t* out = tile_counts + ((int64_t)f * hcap + h0) * tiles_max + t;
+        for (int i = threadIdx.x; i < H; i += kBlock) out[(int64_t)i * tiles_max] = lds_cnt[i];
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_replay: RandomSampleConsensus::computeModel's serial control over the chunk's counts.
+__global__ __launch_bounds__(kBlock) void k_replay(
+    const int32_t* __restrict__ tile_counts, int hcap, int tiles_max, int h0, int H, int max_iter,
+    double log_probability, const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
+    int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
+    ChunkStat* __restrict__ next_stat) {
+    __shared__ int32_t tot[kMaxChunk];
+    const int f = blockIdx.x;
+    if (st[f].done) return;
+    const FrameMeta m = meta[f];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int h = w; h < H; h += kBlock / 64) {
+        const int32_t* row = tile_counts + ((int64_t)f * hcap + h0 + h) * tiles_max;
+        int s = 0;
+        for (int t = lane; t < m.tiles; t += 64) s += row[t];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+        if (lane == 0) tot[h] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    FrameState s = st[f];
+    const double one_over_indices = 1.0 / (double)m.n;
+    const double eps = 2.220446049250313e-16;
+    for (int h = 0; h < H; ++h) {
+        const int hh = h0 + h;
+        if (!((double)s.it < s.k)) { s.done = 1; break; }
+        if (hh >= s.n_avail) {
+            if (s.exhausted) s.status = PITT_E_SAMPLER;
+            else s.pad0 = 1;  // getSamples: 1000 consecutive rejections, "No samples could be selected!"
+            s.done = 1;
+            break;
+        }
+        const int c = tot[h];
+        hyp_total[(int64_t)f * hcap + hh] = c;
+        if (c > s.best_count) {
+            s.best_count = c;
+            s.best_h = hh;
+            const double w = (double)c * one_over_indices;
+            // w^3 rounded once (pow(w, 3.0)): exact double-double cube, then one rounding.
+            const double w2 = w * w, w2l = fma(w, w, -w2);
+            const double w3 = w2 * w, w3l = fma(w2, w, -w3) + w2l * w;
+            double p = 1.0 - (w3 + w3l);
+            p = fmax(eps, p);
+            p = fmin(1.0 - eps, p);
+            s.k = log_probability / log(p);
+            const double r = rint(s.k);
+            if (fabs(s.k - r) <= 1e-9 * fmax(1.0, s.k) && r >= 1.0 && r <= (double)max_iter + 1.0)
+                s.flags |= PITT_FLAG_K_NEAR_INTEGER;
+        }
+        s.it++;
+        if (s.it > max_iter) { s.done = 1; break; }
+    }
+    if (!s.done && !((double)s.it < s.k)) s.done = 1;
+    st[f] = s;
+    if (!s.done) {
+        const int idx = atomicAdd(next_cnt, 1);
+        next_list[idx] = f;
+        atomicAdd(&next_stat->tiles, m.tiles);
+        atomicAdd((unsigned long long*)&next_stat->points, (unsigned long long)m.n);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// After the last chunk: decide model / refinement per frame (one thread per frame).
+__global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
+                         const float4* __restrict__ hyp_coef, int hcap, int n_frames, int optimize,
+                         float4* __restrict__ best_coef, float4* __restrict__ final_coef) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    FrameState s = st[f];
+    s.has_model = (s.best_h >= 0 && s.status == PITT_OK) ? 1 : 0;
+    if (!s.has_model && s.status == PITT_OK) s.status = PITT_NO_MODEL;
+    s.need_refine = (s.has_model && optimize && s.best_count >= 4) ? 1 : 0;
+    if (s.has_model) {
+        const float4 c = hyp_coef[(int64_t)f * hcap + s.best_h];
+        best_coef[f] = c;
+        final_coef[f] = c;  // overwritten by k_cov_eigen when refined
+    }
+    st[f] = s;
+    (void)meta;
+}
+
+// Exclusive scan of a frame's per-tile counts.  mode 0: winning hypothesis row; mode 1: final.
+__global__ __launch_bounds__(kBlock) void k_tile_offsets(
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const int32_t* __restrict__ tile_counts, int hcap, int tiles_max, int mode,
+    int32_t* __restrict__ offsets /* [f][tiles_max + 1] */) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int f = blockIdx.x;
+    const FrameState s = st[f];
+    if (!s.has_model) return;
+    if (mode == 0 && !s.need_refine) return;
+    const int tiles = meta[f].tiles;
+    const int32_t* row = mode == 0 ? tile_counts + ((int64_t)f * hcap + s.best_h) * tiles_max
+                                   : tile_counts + (int64_t)f * tiles_max;
+    int32_t* out = offsets + (int64_t)f * (tiles_max + 1);
+    int carry = 0;
+    for (int base = 0; base < tiles; base += kBlock) {
+        const int t = base + threadIdx.x;
+        const int v = t < tiles ? row[t] : 0;
+        int total;
+        const int ex = block_exscan(v, lds4, &total);
+        if (t < tiles) out[t] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) out[tiles] = carry;
+}
+
+// Shared tile loader for the compaction kernels: the thread's 8 points (groups of 4 consecutive
+// points at tile offsets 4*tid and 1024 + 4*tid) and their inlier bits.
+struct TilePts {
+    float x[8], y[8], z[8];
+};
+
+template <int ORDER>
+__device__ __forceinline__ uint32_t tile_predicates(const float* x, const float* y, const float* z,
+                                                    int64_t rem, float4 c, float thf, TilePts& P) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const int li = g * 1024 + threadIdx.x * 4;
+        const float4 vx = *reinterpret_cast<const float4*>(x + li);
+        const float4 vy = *reinterpret_cast<const float4*>(y + li);
+        const float4 vz = *reinterpret_cast<const float4*>(z + li);
+        P.x[4 * g + 0] = vx.x; P.x[4 * g + 1] = vx.y; P.x[4 * g + 2] = vx.z; P.x[4 * g + 3] = vx.w;
+        P.y[4 * g + 0] = vy.x; P.y[4 * g + 1] = vy.y; P.y[4 * g + 2] = vy.z; P.y[4 * g + 3] = vy.w;
+        P.z[4 * g + 0] = vz.x; P.z[4 * g + 1] = vz.y; P.z[4 * g + 2] = vz.z; P.z[4 * g + 3] = vz.w;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 4 * g + s;
+            const bool in = (li + s < rem) && (fabsf(plane_dot<ORDER>(c, P.x[k], P.y[k], P.z[k])) < thf);
+            bits |= (in ? 1u : 0u) << k;
+        }
+    }
+    return bits;
+}
+
+// k_select_xyz: compact (x, y, z) of the winning model's inliers, ascending point order.
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_select_xyz(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const float4* __restrict__ best_coef, const int32_t* __restrict__ offsets, int n_frames,
+    int tiles_max, float thf, float* __restrict__ CX, float* __restrict__ CY,
+    float* __restrict__ CZ) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int64_t items = (int64_t)n_frames * tiles_max;
+    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+        const FrameMeta m = meta[f];
+        if (t >= m.tiles || !st[f].need_refine) continue;
+        const int64_t tb = (int64_t)t * kTile;
+        TilePts P;
+        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
+                                                     m.n - tb, best_coef[f], thf, P);
+        const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
+        int total;
+        const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
+        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
+        int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = 4 * g + s;
+                if ((bits >> k) & 1u) {
+                    const int64_t o = ob + pos[g]++;
+                    CX[o] = P.x[k];
+                    CY[o] = P.y[k];
+                    CZ[o] = P.z[k];
+                }
+            }
+        }
+    }
+}
+
+// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order.  Lane (slot, acc) of a wave owns
+// accumulator acc (xx, xy, xz, yy, yz, zz, x, y, z) of frame blockIdx.x * 7 + slot and adds its
+// terms sequentially in inlier order; lane acc == 0 then runs eigen33 and writes the refined plane.
+template <int ORDER, int DIV>
+__global__ __launch_bounds__(64) void k_cov_eigen(
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const float* __restrict__ CX, const float* __restrict__ CY, const float* __restrict__ CZ,
+    int n_frames, float4* __restrict__ final_coef) {
+    const int lane = threadIdx.x;
+    const int slot = lane / 9, acc = lane % 9;
+    const int f = blockIdx.x * kCovFramesPerWave + slot;
+    const bool active = slot < kCovFramesPerWave && f < n_frames && st[f].need_refine;
+    int64_t n = 0;
+    const float *A = CX, *B = CX;
+    bool lin = false;
+    if (active) {
+        const FrameMeta m = meta[f];
+        n = st[f].best_count;
+        const float* planes[3] = {CX + m.off, CY + m.off, CZ + m.off};
+        const int ia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
+        const int ib[9] = {0, 1, 2, 1, 2, 2, 0, 1, 2};
+        A = planes[ia[acc]];
+        B = planes[ib[acc]];
+        lin = acc >= 6;
+    }
+    float s = 0.0f;
+    int64_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(A + i);
+        const float4 b = *reinterpret_cast<const float4*>(B + i);
+        s += a.x * (lin ? 1.0f : b.x);
+        s += a.y * (lin ? 1.0f : b.y);
+        s += a.z * (lin ? 1.0f : b.z);
+        s += a.w * (lin ? 1.0f : b.w);
+    }
+    for (; i < n; ++i) s += A[i] * (lin ? 1.0f : B[i]);
+    // gather the 9 accumulators of this frame into its acc == 0 lane
+    float a9[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, slot * 9 + k, 64);
+    if (!active || acc != 0) return;
+    const float fn = (float)n;
+    if constexpr (DIV == 0) {
+        const float r = 1.0f / fn;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = a9[k] * r;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = a9[k] / fn;
+    }
+    float cov[9];
+    cov[0] = a9[0] - a9[6] * a9[6];
+    cov[1] = a9[1] - a9[6] * a9[7];
+    cov[2] = a9[2] - a9[6] * a9[8];
+    cov[4] = a9[3] - a9[7] * a9[7];
+    cov[5] = a9[4] - a9[7] * a9[8];
+    cov[8] = a9[5] - a9[8] * a9[8];
+    cov[3] = cov[1];
+    cov[6] = cov[2];
+    cov[7] = cov[5];
+    float e[3];
+    eigen33(cov, e);
+    const float d = -1.0f * red4<ORDER>(e[0] * a9[6], e[1] * a9[7], e[2] * a9[8], 0.0f * 1.0f);
+    final_coef[f] = make_float4(e[0], e[1], e[2], d);
+}
+
+// Count the final model's inliers per tile.
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_count_final(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const float4* __restrict__ final_coef, int n_frames, int tiles_max, float thf,
+    int32_t* __restrict__ tile_counts2) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int64_t items = (int64_t)n_frames * tiles_max;
+    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+        const FrameMeta m = meta[f];
+        if (t >= m.tiles || !st[f].has_model) continue;
+        const int64_t tb = (int64_t)t * kTile;
+        TilePts P;
+        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
+                                                     m.n - tb, final_coef[f], thf, P);
+        int total;
+        (void)block_exscan(__builtin_popcount(bits), lds4, &total);
+        if (threadIdx.x == 0) tile_counts2[(int64_t)f * tiles_max + t] = total;
+    }
+}
+
+// Write the final inlier indices (relative to the frame), ascending.
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_write_final(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const float4* __restrict__ final_coef, const int32_t* __restrict__ offsets, int n_frames,
+    int tiles_max, float thf, int32_t* __restrict__ out) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int64_t items = (int64_t)n_frames * tiles_max;
+    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+        const FrameMeta m = meta[f];
+        if (t >= m.tiles || !st[f].has_model) continue;
+        const int64_t tb = (int64_t)t * kTile;
+        TilePts P;
+        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
+                                                     m.n - tb, final_coef[f], thf, P);
+        const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
+        int total;
+        const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
+        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
+        int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int li = (int)tb + g * 1024 + threadIdx.x * 4;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if ((bits >> (4 * g + s)) & 1u) out[ob + pos[g]++] = li + s;
+        }
+    }
+}
+
+__global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __restrict__ hyp_attempt,
+                           const float4* __restrict__ best_coef, const float4* __restrict__ final_coef,
+                           const int32_t* __restrict__ offsets2, int hcap, int tiles_max,
+                           const FrameMeta* __restrict__ meta, int n_frames,
+                           pitt_plane_result* __restrict__ res) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    const FrameState s = st[f];
+    pitt_plane_result r;
+    r.status = s.status;
+    r.hypotheses = s.it;
+    r.best_hypothesis = s.best_h;
+    r.best_count = s.best_h >= 0 ? s.best_count : 0;
+    r.flags = s.flags;
+    // rejections before the last evaluated hypothesis; + 1000 when getSamples gave up
+    int rej = 0;
+    if (s.it > 0) rej = hyp_attempt[(int64_t)f * hcap + s.it - 1] - (s.it - 1);
+    if (s.pad0) rej += 1000;
+    r.rejected_samples = rej;
+    if (s.has_model) {
+        const float4 c = final_coef[f];
+        r.coefficients[0] = c.x;
+        r.coefficients[1] = c.y;
+        r.coefficients[2] = c.z;
+        r.coefficients[3] = c.w;
+        r.n_coeff = 4;
+        r.n_inliers = offsets2[(int64_t)f * (tiles_max + 1) + meta[f].tiles];
+    } else {
+        r.coefficients[0] = r.coefficients[1] = r.coefficients[2] = r.coefficients[3] = 0.0f;
+        r.n_coeff = 0;
+        r.n_inliers = 0;
+    }
+    (void)best_coef;
+    res[f] = r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host orchestration.
+
+template <typename T>
+static T* as(void* p) { return static_cast<T*>(p); }
+
+static int grid_items(int64_t items) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(items, 256 * 8));
+}
+
+template <int ORDER, int DIV>
+static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
+                           pitt_plane_result* results, int32_t* inliers_dev) {
+    const int nf = fr->n_frames;
+    hipStream_t sm = ctx->stream;
+    // --- sizes ---
+    int tiles_max = 1;
+    int64_t total_pts = 0;
+    for (int f = 0; f < nf; ++f) {
+        tiles_max = std::max<int>(tiles_max, (int)((fr->counts[f] + kTile - 1) / kTile));
+        total_pts += fr->counts[f];
+    }
+    const int max_iter = p->max_iterations;
+    const int hcap = max_iter >= 0 ? max_iter + 1 : 1;
+    const int runnable_all = ((unsigned)max_iter * 10u) != 0u ? 1 : 0;
+    const int A = hcap + std::max(0, p->sampler_slack);
+    if (A > kMaxAttempts) return ctx->fail(PITT_E_INVALID, "max_iterations + sampler_slack exceeds 8191");
+    const float thf = float_threshold(p->threshold);
+
+    // --- sampler tables: one per distinct point count ---
+    std::vector<int64_t> distinct;
+    for (int f = 0; f < nf; ++f)
+        if (fr->counts[f] >= 3 &&
+            std::find(distinct.begin(), distinct.end(), fr->counts[f]) == distinct.end())
+            distinct.push_back(fr->counts[f]);
+    const size_t tab_ints = (size_t)A * 3;
+    int32_t* tables = as<int32_t>(ctx->buf("tables", std::max<size_t>(1, distinct.size()) * tab_ints * 4));
+    {
+        std::vector<std::tuple<int64_t, uint32_t, int64_t>> keys;
+        for (int64_t n : distinct) keys.emplace_back(n, p->seed, (int64_t)A);
+        if (keys != ctx->pool_keys) {
+            int32_t* hp = as<int32_t>(ctx->pinned("tables_h", std::max<size_t>(1, distinct.size()) * tab_ints * 4));
+            for (size_t i = 0; i < distinct.size(); ++i) {
+                const std::vector<int32_t>& t = sampler_table(ctx, distinct[i], p->seed, A);
+                std::memcpy(hp + i * tab_ints, t.data(), tab_ints * 4);
+            }
+            if (!distinct.empty())
+                PITT_HIP_TRY(hipMemcpyAsync(tables, hp, distinct.size() * tab_ints * 4, hipMemcpyHostToDevice, sm));
+            ctx->pool_keys = keys;
+        }
+    }
+    // --- frame metadata ---
+    FrameMeta* hm = as<FrameMeta>(ctx->pinned("meta_h", (size_t)nf * sizeof(FrameMeta)));
+    for (int f = 0; f < nf; ++f) {
+        hm[f].off = fr->offsets[f];
+        hm[f].n = fr->counts[f];
+        hm[f].tiles = (int32_t)((fr->counts[f] + kTile - 1) / kTile);
+        hm[f].pad = 0;
+        int64_t ti = 0;
+        for (size_t i = 0; i < distinct.size(); ++i)
+            if (distinct[i] == fr->counts[f]) ti = (int64_t)(i * tab_ints);
+        hm[f].tab = ti;
+    }
+    FrameMeta* meta = as<FrameMeta>(ctx->buf("meta", (size_t)nf * sizeof(FrameMeta)));
+    PITT_HIP_TRY(hipMemcpyAsync(meta, hm, (size_t)nf * sizeof(FrameMeta), hipMemcpyHostToDevice, sm));
+
+    // --- chunk schedule (geometric after the first few HBM-bound 16-hypothesis passes) ---
+    std::vector<int> chunks;
+    for (int h0 = 0, i = 0; h0 < hcap; ++i) {
+        int H = i < 4 ? 16 : std::min(kMaxChunk, 16 << (i - 3));
+        H = std::min(H, hcap - h0);
+        chunks.push_back(H);
+        h0 += H;
+    }
+    const int nchunks = (int)chunks.size();
+
+    // --- scratch ---
+    float4* hyp_coef = as<float4>(ctx->buf("hyp_coef", (size_t)nf * hcap * sizeof(float4)));
+    int32_t* hyp_attempt = as<int32_t>(ctx->buf("hyp_attempt", (size_t)nf * hcap * 4));
+    int32_t* hyp_total = as<int32_t>(ctx->buf("hyp_total", (size_t)nf * hcap * 4));
+    int32_t* tile_counts = as<int32_t>(ctx->buf("tile_counts", (size_t)nf * hcap * tiles_max * 4));
+    FrameState* st = as<FrameState>(ctx->buf("state", (size_t)nf * sizeof(FrameState)));
+    int32_t* lists = as<int32_t>(ctx->buf("lists", (size_t)(nchunks + 1) * nf * 4));
+    // counters + chunk stats in one zeroed block
+    const size_t cnt_bytes = (size_t)(nchunks + 1) * 4;
+    const size_t stat_off = (cnt_bytes + 15) & ~(size_t)15;
+    const size_t zero_bytes = stat_off + (size_t)(nchunks + 1) * sizeof(ChunkStat);
+    char* zblock = as<char>(ctx->buf("zblock", zero_bytes));
+    int32_t* counters = as<int32_t>(zblock);
+    ChunkStat* cstat = as<ChunkStat>(zblock + stat_off);
+    float4* best_coef = as<float4>(ctx->buf("best_coef", (size_t)nf * sizeof(float4)));
+    float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
+    int32_t* offs1 = as<int32_t>(ctx->buf("offs1", (size_t)nf * (tiles_max + 1) * 4));
+    int32_t* offs2 = as<int32_t>(ctx->buf("offs2", (size_t)nf * (tiles_max + 1) * 4));
+    int32_t* counts2 = as<int32_t>(ctx->buf("counts2", (size_t)nf * tiles_max * 4));
+    const size_t cap = (size_t)fr->capacity;
+    float* CX = as<float>(ctx->buf("compact", cap * 3 * sizeof(float)));
+    float* CY = CX + cap;
+    float* CZ = CY + cap;
+    pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
+    if (!hyp_coef || !tile_counts || !CX || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+
+    PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
+
+    int rec;
+    rec = ctx->prof_begin("k_hypothesize", (double)nf * A * 48.0);
+    hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta,
+                       tables, A, hcap, runnable_all, hyp_coef, hyp_attempt, st, lists, counters, cstat);
+    ctx->prof_end(rec);
+    const double log_prob = std::log(1.0 - p->probability);
+    std::vector<int> score_recs;
+    for (int c = 0, h0 = 0; c < nchunks; h0 += chunks[(size_t)c], ++c) {
+        const int H = chunks[(size_t)c];
+        rec = ctx->prof_begin("k_score", 0.0);
+        score_recs.push_back(rec);
+        hipLaunchKernelGGL((k_score<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
+                           fr->x, fr->y, fr->z, meta, hyp_coef, hcap, lists + (size_t)c * nf, counters + c,
+                           tiles_max, h0, H, thf, tile_counts);
+        ctx->prof_end(rec);
+        rec = ctx->prof_begin("k_replay", 0.0);
+        hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, tiles_max, h0, H, max_iter,
+                           log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf, counters + c + 1,
+                           cstat + c + 1);
+        ctx->prof_end(rec);
+    }
+    hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
+                       p->optimize ? 1 : 0, best_coef, final_coef);
+    if (p->optimize) {
+        rec = ctx->prof_begin("k_tile_offsets", 0.0);
+        hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, tile_counts, hcap, tiles_max,
+                           0, offs1);
+        ctx->prof_end(rec);
+        rec = ctx->prof_begin("k_select_xyz", (double)total_pts * 12.0);
+        hipLaunchKernelGGL((k_select_xyz<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
+                           fr->x, fr->y, fr->z, meta, st, best_coef, offs1, nf, tiles_max, thf, CX, CY, CZ);
+        ctx->prof_end(rec);
+        rec = ctx->prof_begin("k_cov_eigen", 0.0);
+        hipLaunchKernelGGL((k_cov_eigen<ORDER, DIV>), dim3((nf + kCovFramesPerWave - 1) / kCovFramesPerWave),
+                           dim3(64), 0, sm, meta, st, CX, CY, CZ, nf, final_coef);
+        ctx->prof_end(rec);
+    }
+    rec = ctx->prof_begin("k_count_final", (double)total_pts * 12.0);
+    hipLaunchKernelGGL((k_count_final<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
+                       fr->x, fr->y, fr->z, meta, st, final_coef, nf, tiles_max, thf, counts2);
+    ctx->prof_end(rec);
+    hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, counts2, hcap, tiles_max, 1,
+                       offs2);
+    if (inliers_dev) {
+        rec = ctx->prof_begin("k_write_final", (double)total_pts * 12.0);
+        hipLaunchKernelGGL((k_write_final<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
+                           fr->x, fr->y, fr->z, meta, st, final_coef, offs2, nf, tiles_max, thf, inliers_dev);
+        ctx->prof_end(rec);
+    }
+    hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, best_coef,
+                       final_coef, offs2, hcap, tiles_max, meta, nf, dres);
+    PITT_HIP_TRY(hipGetLastError());
+    pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
+    ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
+    PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipStreamSynchronize(sm));
+    std::memcpy(results, hres, (size_t)nf * sizeof(pitt_plane_result));
+    // algorithmic bytes of each score launch: 12 B per point of every active frame's tiles
+    // (the full tiles are read) + the per-tile count words written.
+    for (int c = 0; c < nchunks; ++c)
+        ctx->prof_set_bytes(score_recs[(size_t)c], (double)hstat[c].tiles * kTile * 12.0 +
+                                                       (double)hstat[c].tiles * chunks[(size_t)c] * 4.0);
+    ctx->last_hcap = hcap;
+    ctx->last_frames = nf;
+    return PITT_OK;
+}
+
+int plane_segment_batch_impl(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
+                             pitt_plane_result* results, int32_t* inliers_dev) {
+    const int key = p->reduce_order * 2 + (p->div_mode ? 1 : 0);
+    switch (key) {
+    case 0: return run_plane_batch<0, 0>(ctx, fr, p, results, inliers_dev);
+    case 1: return run_plane_batch<0, 1>(ctx, fr, p, results, inliers_dev);
+    case 2: return run_plane_batch<1, 0>(ctx, fr, p, results, inliers_dev);
+    case 3: return run_plane_batch<1, 1>(ctx, fr, p, results, inliers_dev);
+    case 4: return run_plane_batch<2, 0>(ctx, fr, p, results, inliers_dev);
+    case 5: return run_plane_batch<2, 1>(ctx, fr, p, results, inliers_dev);
+    default: return ctx->fail(PITT_E_INVALID, "reduce_order / div_mode out of range");
+    }
+}
+
+}  // namespace pitt

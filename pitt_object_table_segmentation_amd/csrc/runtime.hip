@@ -1,0 +1,304 @@
+// runtime.hip -- pitt_ctx lifecycle, scratch arena, sampler tables, profiler and the C ABI entry
+// points of include/pitt_seg.h for the plane path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <tuple>
+#include <unordered_map>
+
+#include "ctx.hpp"
+
+namespace pitt {
+int plane_segment_batch_impl(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
+                             pitt_plane_result* results, int32_t* inliers_dev);
+
+// A2: drawIndexSample's index triples for a cloud of n points.  The shuffled index vector of
+// SampleConsensusModel is the identity except at the positions the swaps touched, so it is kept
+// sparsely: O(attempts) instead of the O(n) array PCL rebuilds on every segment().
+const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts) {
+    auto key = std::make_tuple(n, seed, attempts);
+    auto it = ctx->tables.find(key);
+    if (it != ctx->tables.end()) return it->second;
+    std::vector<int32_t> t((size_t)attempts * 3);
+    std::mt19937 mt(seed);  // boost::mt19937 and std::mt19937 produce the same stream
+    std::unordered_map<int64_t, int64_t> sh;
+    sh.reserve((size_t)attempts * 4);
+    auto get = [&](int64_t i) {
+        auto f = sh.find(i);
+        return f == sh.end() ? i : f->second;
+    };
+    for (int64_t a = 0; a < attempts; ++a) {
+        for (int64_t i = 0; i < 3; ++i) {
+            const uint32_t r = (uint32_t)mt() >> 1;           // uniform_int<>(0, INT_MAX)
+            const int64_t j = i + (int64_t)((uint64_t)r % (uint64_t)(n - i));
+            const int64_t vi = get(i), vj = get(j);
+            sh[i] = vj;
+            sh[j] = vi;
+        }
+        t[(size_t)a * 3 + 0] = (int32_t)get(0);
+        t[(size_t)a * 3 + 1] = (int32_t)get(1);
+        t[(size_t)a * 3 + 2] = (int32_t)get(2);
+    }
+    return ctx->tables.emplace(key, std::move(t)).first->second;
+}
+
+// A4: fabs(float) < (double)th  <=>  fabs(float) < t, t = the smallest float >= th.
+float float_threshold(double th) {
+    if (std::isnan(th)) return std::nanf("");
+    float f = (float)th;
+    if ((double)f < th) f = std::nextafter(f, INFINITY);
+    return f;
+}
+}  // namespace pitt
+
+void* pitt_ctx::buf(const std::string& name, size_t bytes) {
+    pitt::DevBuf& b = bufs[name];
+    if (b.bytes < bytes || !b.p) {
+        if (b.p) (void)hipFree(b.p);
+        size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
+        nb = (nb + ((size_t)1 << 21) - 1) & ~(((size_t)1 << 21) - 1);
+        if (nb == 0) nb = (size_t)1 << 21;
+        if (hipMalloc(&b.p, nb) != hipSuccess) {
+            b.p = nullptr;
+            b.bytes = 0;
+            return nullptr;
+        }
+        b.bytes = nb;
+        if (name == "tables") pool_keys.clear();  // device table pool lost
+    }
+    return b.p;
+}
+
+void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
+    auto& e = host_pinned[name];
+    if (e.second < bytes || !e.first) {
+        if (e.first) (void)hipHostFree(e.first);
+        size_t nb = std::max<size_t>(bytes, 4096);
+        if (hipHostMalloc(&e.first, nb, hipHostMallocDefault) != hipSuccess) {
+            e.first = nullptr;
+            e.second = 0;
+            return nullptr;
+        }
+        e.second = nb;
+    }
+    return e.first;
+}
+
+int pitt_ctx::prof_begin(const char* name, double bytes) {
+    if (!prof) return -1;
+    pitt::ProfRec r;
+    r.name = name;
+    r.bytes = bytes;
+    for (hipEvent_t* e : {&r.a, &r.b}) {
+        if (!event_pool.empty()) {
+            *e = event_pool.back();
+            event_pool.pop_back();
+        } else {
+            (void)hipEventCreate(e);
+        }
+    }
+    (void)hipEventRecord(r.a, stream);
+    pending.push_back(r);
+    return (int)pending.size() - 1;
+}
+
+void pitt_ctx::prof_end(int rec) {
+    if (rec < 0) return;
+    (void)hipEventRecord(pending[(size_t)rec].b, stream);
+}
+
+int pitt_ctx::prof_collect() {
+    if (pending.empty()) return PITT_OK;
+    if (hipStreamSynchronize(stream) != hipSuccess) return PITT_E_HIP;
+    for (pitt::ProfRec& r : pending) {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, r.a, r.b);
+        pitt::ProfTotal& t = totals[r.name];
+        t.launches += 1;
+        t.ms += ms;
+        t.bytes += r.bytes;
+        event_pool.push_back(r.a);
+        event_pool.push_back(r.b);
+    }
+    pending.clear();
+    return PITT_OK;
+}
+
+extern "C" {
+
+int pitt_abi_version(void) { return PITT_ABI_VERSION; }
+
+void pitt_sac_params_default(pitt_sac_params* p) {
+    if (!p) return;
+    p->threshold = 0.007;        // plane_segmentation_srv.cpp:20
+    p->max_iterations = 1000;    // :21
+    p->probability = 0.99;       // RandomSampleConsensus default
+    p->seed = 12345u;            // SampleConsensusModel, random_ == false
+    p->optimize = 1;             // :55
+    p->reduce_order = PITT_REDUCE_SSE2;
+    p->div_mode = PITT_DIV_EIGEN32;
+    p->sampler_slack = 64;
+}
+
+int pitt_create(pitt_ctx** out, int hip_device) {
+    if (!out) return PITT_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PITT_E_NODEVICE;
+    if (hip_device < 0 || hip_device >= n) return PITT_E_INVALID;
+    if (hipSetDevice(hip_device) != hipSuccess) return PITT_E_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return PITT_E_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return PITT_E_NODEVICE;
+    pitt_ctx* c = new pitt_ctx;
+    c->device = hip_device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PITT_E_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return PITT_OK;
+}
+
+void pitt_destroy(pitt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto& kv : ctx->host_pinned)
+        if (kv.second.first) (void)hipHostFree(kv.second.first);
+    for (auto& r : ctx->pending) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+int pitt_set_stream(pitt_ctx* ctx, void* s) {
+    if (!ctx) return PITT_E_INVALID;
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return PITT_OK;
+}
+
+void* pitt_get_stream(pitt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+const char* pitt_last_error(pitt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
+                             pitt_plane_result* results, int32_t* inliers_dev) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!fr || !p || !results) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (fr->n_frames < 0) return ctx->fail(PITT_E_INVALID, "n_frames < 0");
+    if (fr->n_frames == 0) return PITT_OK;
+    if (!fr->x || !fr->y || !fr->z || !fr->offsets || !fr->counts)
+        return ctx->fail(PITT_E_INVALID, "null frame pointer");
+    if (((uintptr_t)fr->x | (uintptr_t)fr->y | (uintptr_t)fr->z) & 15u)
+        return ctx->fail(PITT_E_INVALID, "x/y/z planes must be 16-byte aligned");
+    if (inliers_dev && ((uintptr_t)inliers_dev & 3u))
+        return ctx->fail(PITT_E_INVALID, "inliers_dev must be 4-byte aligned");
+    if (p->reduce_order < 0 || p->reduce_order > 2 || p->div_mode < 0 || p->div_mode > 1)
+        return ctx->fail(PITT_E_INVALID, "reduce_order / div_mode out of range");
+    for (int f = 0; f < fr->n_frames; ++f) {
+        const int64_t o = fr->offsets[f], n = fr->counts[f];
+        if (o < 0 || n < 0 || (o & 3) != 0) return ctx->fail(PITT_E_INVALID, "frame offset must be >= 0 and a multiple of 4");
+        if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "frame larger than 2^31 points");
+        const int64_t span = (n + PITT_TILE_POINTS - 1) / PITT_TILE_POINTS * PITT_TILE_POINTS;
+        if (o + span > fr->capacity) return ctx->fail(PITT_E_INVALID, "frame tile span exceeds capacity");
+    }
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::plane_segment_batch_impl(ctx, fr, p, results, inliers_dev);
+}
+
+int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                       const pitt_sac_params* p, int32_t* inliers_out, int64_t* n_inliers,
+                       float coeff_out[4], int32_t* n_coeff) {
+    if (!ctx) return PITT_E_INVALID;
+    if ((!xyz && n > 0) || !p || !n_inliers || !n_coeff || n < 0)
+        return ctx->fail(PITT_E_INVALID, "null argument");
+    if (stride_bytes != 12 && stride_bytes != 16) return ctx->fail(PITT_E_INVALID, "stride must be 12 or 16");
+    *n_inliers = 0;
+    *n_coeff = 0;
+    const int64_t cap = std::max<int64_t>(PITT_TILE_POINTS,
+                                          (n + PITT_TILE_POINTS - 1) / PITT_TILE_POINTS * PITT_TILE_POINTS);
+    float* h = (float*)ctx->pinned("single_h", (size_t)cap * 3 * sizeof(float));
+    if (!h) return ctx->fail(PITT_E_NOMEM, "pinned allocation failed");
+    const int sf = stride_bytes / 4;
+    for (int64_t i = 0; i < n; ++i) {
+        h[i] = xyz[i * sf];
+        h[cap + i] = xyz[i * sf + 1];
+        h[2 * cap + i] = xyz[i * sf + 2];
+    }
+    float* d = (float*)ctx->buf("single_xyz", (size_t)cap * 3 * sizeof(float));
+    int32_t* di = (int32_t*)ctx->buf("single_inl", (size_t)cap * sizeof(int32_t));
+    if (!d || !di) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    PITT_HIP_TRY(hipMemcpyAsync(d, h, (size_t)cap * 3 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    int64_t off = 0;
+    pitt_frames fr;
+    fr.x = d;
+    fr.y = d + cap;
+    fr.z = d + 2 * cap;
+    fr.offsets = &off;
+    fr.counts = &n;
+    fr.n_frames = 1;
+    fr.capacity = cap;
+    pitt_plane_result r;
+    int rc = pitt_plane_segment_batch(ctx, &fr, p, &r, di);
+    if (rc < 0) return rc;
+    if (r.status < 0) return ctx->fail(r.status, "plane segmentation failed");
+    if (r.n_coeff == 0) return PITT_NO_MODEL;
+    if (inliers_out && r.n_inliers > 0)
+        PITT_HIP_TRY(hipMemcpy(inliers_out, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
+    *n_inliers = r.n_inliers;
+    *n_coeff = 4;
+    if (coeff_out) std::memcpy(coeff_out, r.coefficients, 4 * sizeof(float));
+    return PITT_OK;
+}
+
+int pitt_last_hypothesis_counts(pitt_ctx* ctx, int32_t frame, int32_t* counts, int32_t cap) {
+    if (!ctx || !counts) return PITT_E_INVALID;
+    if (frame < 0 || frame >= ctx->last_frames) return ctx->fail(PITT_E_INVALID, "frame out of range");
+    auto it = ctx->bufs.find("hyp_total");
+    if (it == ctx->bufs.end()) return ctx->fail(PITT_E_INVALID, "no batch run yet");
+    const int32_t m = std::min(cap, ctx->last_hcap);
+    PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    PITT_HIP_TRY(hipMemcpy(counts, (int32_t*)it->second.p + (size_t)frame * ctx->last_hcap,
+                           (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return PITT_OK;
+}
+
+int pitt_profile_enable(pitt_ctx* ctx, int32_t on) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!on) (void)ctx->prof_collect();
+    ctx->prof = on != 0;
+    return PITT_OK;
+}
+
+int pitt_profile_get(pitt_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms,
+                     double* algorithmic_bytes) {
+    if (!ctx || !kernel) return PITT_E_INVALID;
+    int rc = ctx->prof_collect();
+    if (rc) return rc;
+    auto it = ctx->totals.find(kernel);
+    const pitt::ProfTotal t = it == ctx->totals.end() ? pitt::ProfTotal() : it->second;
+    if (launches) *launches = t.launches;
+    if (total_ms) *total_ms = t.ms;
+    if (algorithmic_bytes) *algorithmic_bytes = t.bytes;
+    return PITT_OK;
+}
+
+int pitt_profile_reset(pitt_ctx* ctx) {
+    if (!ctx) return PITT_E_INVALID;
+    (void)ctx->prof_collect();
+    ctx->totals.clear();
+    return PITT_OK;
+}
+
+}  // extern "C"
