@@ -1,0 +1,205 @@
+"""Benchmark of the MI355X RANSAC-plane path (BASELINE.json metric).
+
+One step = one batch of synthetic 640x480 table-scene clouds per GPU (256 by default, BASELINE
+config 3) through pitt_plane_segment_batch: hypotheses, adaptive RANSAC scoring, refinement and
+the final ascending inlier list, results on the host; with N > 1 ranks the per-frame result
+records are gathered over RCCL (config 4).  Inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  Roofline figures are for the dominant kernel (k_score, the
+inlier-scoring kernel): algorithmic bytes = 12 B per point of every (active frame, tile) a launch
+reads, divided by its average launch time measured with HIP events on its stream.
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "RANSAC frames/sec on 307k-pt clouds @1/2/4/8 GPU; inlier-kernel HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+W, H = 640, 480
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_frames(ids, threads):
+    import pitt_object_table_segmentation_amd as pitt
+    with cf.ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL
+        return list(ex.map(lambda i: pitt.synth_frame(pitt.SCENE_TABLE, 1000 + int(i), W, H), ids))
+
+
+def cpu_baseline(frames, threads, budget_s):
+    """The oracle (CPU restatement of the reference's PCL path) timed on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_binding as orc
+    done = 0
+    t0 = time.perf_counter()
+
+    def one(k):
+        orc.plane_segment(*frames[k % len(frames)])
+        return 1
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        k = 0
+        while time.perf_counter() - t0 < budget_s:
+            done += sum(ex.map(one, range(k, k + threads * 4)))
+            k += threads * 4
+    dt = time.perf_counter() - t0
+    return dict(value=round(done / dt, 2), unit="frames/s", cores=threads, kind="port",
+                sample=f"{done} frames cycled over the first {len(frames)} synthetic 640x480 table frames, "
+                       f"{dt:.1f} s wall, frame-parallel over {threads} threads (oracle/pitt_oracle.cpp, "
+                       f"g++ -O2, PCL-equivalent single-threaded segment() per frame)")
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of k_score from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_score.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-gpu", type=int, default=256)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-inliers", action="store_true", help="skip writing the final inlier lists")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import pitt_object_table_segmentation_amd as pitt
+    from pitt_object_table_segmentation_amd import distributed
+
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 8))))
+    B = args.frames_per_gpu
+    total = B * world
+    start, end = distributed.shard_range(total, world, rank)
+    t_gen = time.perf_counter()
+    frames = make_frames(range(start, end), threads)
+    batch = pitt.FrameBatch.from_host(frames, device=dev)
+    inliers = None if args.no_inliers else torch.empty(batch.capacity, dtype=torch.int32, device=dev)
+    log(f"[rank {rank}] {len(frames)} frames generated + uploaded in {time.perf_counter() - t_gen:.1f} s")
+
+    ctx = pitt.Context(local)
+    stream = torch.cuda.Stream(device=dev)
+    ctx.set_stream(stream)
+    params = pitt.sac_params()
+
+    def step():
+        res = ctx.plane_segment_batch(batch, params, inliers)
+        if world > 1:
+            res = distributed.gather_results(res, start, total, device=dev)
+        return res
+
+    for _ in range(args.warmup):
+        res = step()
+    # parity spot check outside the timed region (first frame of this rank vs the oracle)
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_binding as orc
+        o = orc.plane_segment(*frames[0])
+        ok = (np.array_equal(res[0]["coefficients"], o.coefficients) and res[0]["n_inliers"] == len(o.inliers)
+              and res[0]["hypotheses"] == o.hypotheses)
+        log(f"[rank 0] parity frame 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'} "
+            f"(T={int(res[0]['hypotheses'])}, inliers={int(res[0]['n_inliers'])})")
+
+    ctx.profile(True)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    launches, ms, nbytes = ctx.profile_get("k_score")
+    ctx.profile(False)
+    hyps = res["hypotheses"]
+
+    if rank == 0:
+        avg_ms = ms / max(1, launches)
+        achieved = (nbytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if launches else 0.0
+        traffic = pmc_traffic()
+        line = {
+            "metric": METRIC,
+            "value": round(total * args.steps / dt, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic 640x480 organised table-scene clouds, scene_seed = 1000 + frame id",
+            "config": {
+                "workload": f"batch of {B} synthetic 307k-pt clouds per GPU (BASELINE config 3"
+                            f"{'; config 4: frame-sharded, RCCL all_gather of per-frame records' if world > 1 else ''}),"
+                            " PCL plane RANSAC th 0.007 / 1000 iters / seed 12345 / optimize, final inlier lists",
+                "frames_per_gpu": B,
+                "points_per_frame": W * H,
+                "parallelism": f"frame-sharded x{world}",
+                "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
+            },
+            "roofline": {
+                "kernel": "k_score",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "launches": launches,
+                "avg_launch_us": round(avg_ms * 1e3, 2),
+                "algorithmic_bytes_per_launch": round(nbytes / max(1, launches), 1),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(frames, threads, args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -193,6 +193,13 @@ int pitt_synth_frame(int32_t scene, uint64_t scene_seed, int32_t width, int32_t 
 int pitt_synth_fused(uint64_t scene_seed, int32_t views, int32_t width, int32_t height,
                      float* x, float* y, float* z);
 
+/* --- host helpers (no device needed) ------------------------------------------------------- */
+/* A2: attempts*3 indices that SampleConsensusModel::drawIndexSample yields for a cloud of n points
+ * (mt19937 seeded `seed`, rnd() = mt() >> 1, persistent shuffled index vector). */
+int pitt_sampler_table(int64_t n, uint32_t seed, int64_t attempts, int32_t* out);
+/* A4: the float t with  (double)fabsf(d) < threshold  <=>  fabsf(d) < t  for every float d. */
+float pitt_float_threshold(double threshold);
+
 /* --- profiling ------------------------------------------------------------------------------ */
 /* When enabled, every kernel launch is bracketed by hipEvents on the launch stream. */
 int pitt_profile_enable(pitt_ctx* ctx, int32_t on);

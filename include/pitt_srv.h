@@ -1,0 +1,76 @@
+/*
+ * pitt_srv.h -- C ABI over the C++ service mirror (pitt_srv.hpp), for FFI callers and tests.
+ *
+ * Each handler call runs the reference handler's semantics end to end (parameter resolution,
+ * PCL-equivalent arithmetic on the MI355X, post-processing quirks) and keeps the response inside
+ * the pitt_srv object until the next call; getters copy it out.
+ *   pitt_srv_ransac_plane     <-> ransacPlaneDetaction  plane_segmentation_srv.cpp:27
+ *   pitt_srv_find_supports    <-> findSupports          supports_segmentation_srv.cpp:241
+ *   pitt_srv_clusterize       <-> clusterize            cluster_segmentation_srv.cpp:38
+ *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
+ * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
+ * Handler calls return 1 when the handler returns true, 0 when false, < 0 on an ABI error.
+ */
+#ifndef PITT_SRV_H
+#define PITT_SRV_H
+#include <stdint.h>
+
+#include "pitt_seg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pitt_srv pitt_srv;
+
+pitt_srv* pitt_srv_create(pitt_ctx* ctx);
+void pitt_srv_destroy(pitt_srv* srv);
+
+/* parameter server (roscpp typed-read rules, see pitt_srv.hpp) */
+int pitt_srv_param_set_int(pitt_srv* srv, const char* name, int32_t v);
+int pitt_srv_param_set_double(pitt_srv* srv, const char* name, double v);
+int pitt_srv_param_set_list(pitt_srv* srv, const char* name, const double* v, int32_t n);
+int pitt_srv_param_erase(pitt_srv* srv, const char* name);
+
+/* SupportSegmentation request scalars; negative / wrong-length fields mean "service default" */
+typedef struct {
+    float   min_iterative_cloud_percentual_size;
+    float   min_iterative_plane_percentual_size;
+    float   variance_threshold_for_horizontal;
+    float   ransac_distance_point_in_shape_threshold;
+    float   ransac_model_normal_distance_weigth;
+    int32_t ransac_max_iteration_threshold;
+    int32_t n_horizontal_axis;
+    float   horizontal_axis[8];
+    int32_t n_edge_remove_offset;
+    float   edge_remove_offset[8];
+} pitt_srv_support_request;
+
+int pitt_srv_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
+                          int32_t* inliers_out /* cap n */, int64_t* n_inliers,
+                          float* coefficients_out /* cap 4 */, int32_t* n_coefficients,
+                          float centroid_out[3]);
+
+/* used_out: the response's used_* fields in declaration order:
+ * cloud%, plane%, max var, min var, max iter, distance th, normal weight, axis[3], offset[3] */
+int pitt_srv_find_supports(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
+                           const pitt_srv_support_request* req, int32_t* n_supports, float used_out[13]);
+int pitt_srv_support_get(pitt_srv* srv, int32_t s, int32_t* idx_map /* cap n */, float coef[4],
+                         int64_t* n_support, int64_t* n_on_support);
+int pitt_srv_support_cloud(pitt_srv* srv, int32_t s, int32_t which /* 0 support, 1 on-support */,
+                           float* xyz16_out);
+
+int pitt_srv_clusterize(pitt_srv* srv, const float* xyz16, int64_t n, int32_t* n_clusters);
+int pitt_srv_cluster_get(pitt_srv* srv, int32_t c, int32_t* inliers /* cap size */, int64_t* size,
+                         float centroid[3], float* xyz16_out /* optional, cap size */);
+
+int pitt_srv_segment_objects(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
+                             int32_t* n_outputs);
+int pitt_srv_output_size(pitt_srv* srv, int32_t o, int32_t* n_clusters);
+int pitt_srv_output_cluster(pitt_srv* srv, int32_t o, int32_t c, int32_t* inliers, int64_t* size,
+                            float centroid[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PITT_SRV_H */

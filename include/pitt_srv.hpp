@@ -1,0 +1,208 @@
+// pitt_srv.hpp -- C++ mirror of the reference's segmentation-service layer, ROS-free.
+//
+// The reference's handlers (src/segmentation_services/*.cpp) are `bool h(Req&, Res&)` functions
+// over pitt_msgs messages with parameters read from the ROS parameter server.  This header keeps
+// that interface -- same handler names, message fields, parameter names, defaults, "-1 means
+// default" sentinels and post-processing quirks -- and runs the arithmetic through the C ABI in
+// pitt_seg.h (MI355X).  A maintainer with ROS available swaps `pitt_msgs::*` for the generated
+// message types and `ParamServer` for ros::NodeHandle.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "pitt_seg.h"
+
+namespace pitt_msgs {
+
+// sensor_msgs/PointCloud2 carrying pcl::PointXYZ: point_step 16 (x, y, z, padding).
+struct PointCloud {
+    std::vector<float> data;  // 4 floats per point
+    size_t size() const { return data.size() / 4; }
+    float x(size_t i) const { return data[4 * i]; }
+    float y(size_t i) const { return data[4 * i + 1]; }
+    float z(size_t i) const { return data[4 * i + 2]; }
+    void push_back(float px, float py, float pz) {
+        data.push_back(px);
+        data.push_back(py);
+        data.push_back(pz);
+        data.push_back(1.0f);
+    }
+};
+// sensor_msgs/PointCloud2 carrying pcl::Normal (only its size matters on the plane path, A1).
+struct NormalCloud {
+    size_t n = 0;
+    size_t size() const { return n; }
+};
+
+struct PrimitiveSegmentation {  // plane_segmentation_srv.cpp:27-74
+    struct Request {
+        PointCloud cloud;
+        NormalCloud normals;
+    } request;
+    struct Response {
+        std::vector<int32_t> inliers;
+        std::vector<float> coefficients;
+        float x_centroid = 0, y_centroid = 0, z_centroid = 0;  // never set for planes (Q3)
+    } response;
+};
+
+struct Support {  // supports_segmentation_srv.cpp:313-325
+    std::vector<int32_t> inliers;  // index map over the original cloud
+    PointCloud support_cloud;
+    PointCloud on_support_cloud;
+    float support_coefficient_a = 0, support_coefficient_b = 0, support_coefficient_c = 0,
+          support_coefficient_d = 0;
+};
+
+struct SupportSegmentation {  // supports_segmentation_srv.cpp:241-361
+    struct Request {
+        PointCloud input_cloud;
+        NormalCloud input_norm;
+        float min_iterative_cloud_percentual_size = -1.0f;
+        float min_iterative_plane_percentual_size = -1.0f;
+        float variance_threshold_for_horizontal = -1.0f;
+        float ransac_distance_point_in_shape_threshold = -1.0f;
+        float ransac_model_normal_distance_weigth = -1.0f;
+        int32_t ransac_max_iteration_threshold = -1;
+        std::vector<float> horizontal_axis;
+        std::vector<float> support_edge_remove_offset;
+    } request;
+    struct Response {
+        std::vector<Support> supports_description;
+        float used_min_iterative_cloud_percentual_size = 0;
+        float used_min_iterative_plane_percentual_size = 0;
+        float used_max_variance_threshold_for_horizontal = 0;
+        float used_min_variance_threshold_for_horizontal = 0;
+        int32_t used_ransac_max_iteration_threshold = 0;
+        float used_ransac_distance_point_in_shape_threshold = 0;
+        float used_ransac_model_normal_distance_weigth = 0;
+        std::vector<float> used_horizontal_axis;
+        std::vector<float> used_support_edge_remove_offset;
+    } response;
+};
+
+struct InliersCluster {  // cluster_segmentation_srv.cpp:95-101
+    std::vector<int32_t> inliers;
+    PointCloud cloud;
+    float x_centroid = 0, y_centroid = 0, z_centroid = 0;
+    std::string shape_id;
+};
+
+struct ClusterSegmentation {  // cluster_segmentation_srv.cpp:38-108
+    struct Request {
+        PointCloud cloud;
+    } request;
+    struct Response {
+        std::vector<InliersCluster> cluster_objs;
+    } response;
+};
+
+struct ClustersOutput {  // obj_segmentation.cpp:286-311
+    std::vector<InliersCluster> cluster_objs;
+};
+
+}  // namespace pitt_msgs
+
+namespace srvm {  // src/point_cloud_library/srv_manager.h:25-188 (names, sentinels)
+const std::string SRV_NAME_SUPPORT_FILTER = "support_segmentation_srv";
+const std::string SRV_NAME_CUSTER_FILTER = "cluster_Segmentation_srv";
+const std::string SRV_NAME_RANSAC_PLANE_FILTER = "plane_segmentation_srv";
+const std::string PARAM_NAME_CLUSTER_TOLERANCE = "/pitt/srv/cluster_segmentation/tolerance";
+const std::string PARAM_NAME_CLUSTER_MIN_RATE = "/pitt/srv/cluster_segmentation/min_rate";
+const std::string PARAM_NAME_CLUSTER_MAX_RATE = "/pitt/srv/cluster_segmentation/max_rate";
+const std::string PARAM_NAME_CLUSTER_MIN_INPUT_SIZE = "/pitt/srv/cluster_segmentation/min_input_size";
+const std::string PARAM_NAME_PLANE_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/plane_segmentation/normal_distance_weight";
+const std::string PARAM_NAME_PLANE_DISTANCE_TH = "/pitt/srv/plane_segmentation/distance_th";
+const std::string PARAM_NAME_PLANE_MAX_ITERATION_LIMIT = "/pitt/srv/plane_segmentation/max_iter_limit";
+const std::string PARAM_NAME_PLANE_EPS_ANGLE_TH = "/pitt/srv/plane_segmentation/eps_angle_th";
+const std::string PARAM_NAME_PLANE_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_segmentation/min_opening_angle_deg";
+const std::string PARAM_NAME_PLANE_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_segmentation/max_opening_angle_deg";
+const std::string PARAM_NAME_PLANE_MIN_INLIERS = "/pitt/srv/plane_segmentation/min_inliers";
+const std::string PARAM_NAME_MIN_ITERATIVE_CLOUD_PERCENTAGE = "/pitt/srv/supports_segmentation/min_iter_cloud_percent";
+const std::string PARAM_NAME_MIN_ITERATIVE_SUPPORT_PERCENTAGE = "/pitt/srv/supports_segmentation/min_iter_support_percent";
+const std::string PARAM_NAME_HORIZONTAL_VARIANCE_THRESHOLD = "/pitt/srv/supports_segmentation/horizontal_variance_th";
+const std::string PARAM_NAME_RANSAC_IN_SHAPE_DISTANCE_POINT_THRESHOLD = "/pitt/srv/supports_segmentation/in_shape_distance_th";
+const std::string PARAM_NAME_RANSAC_MODEL_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/supports_segmentation/normal_distance_weight";
+const std::string PARAM_NAME_RANSAC_MAX_ITERATION_THRESHOLD = "/pitt/srv/supports_segmentation/max_iter";
+const std::string PARAM_NAME_HORIZONTAL_AXIS = "/pitt/srv/supports_segmentation/horizontal_axis";
+const std::string PARAM_NAME_SUPPORT_EDGE_REMOVE_OFFSET = "/pitt/srv/supports_segmentation/edge_remove_offset";
+const int DEFAULT_SERVICE_PARAMETER_REQUEST = -1;
+const float DEFAULT_SERVICE_PARAMETER_REQUEST_F = -1.0f;
+
+inline float getServiceFloatParameter(float input, const float defaultValue) {
+    return input >= 0.0f ? input : defaultValue;
+}
+inline int getServiceIntParameter(int input, const int defaultValue) { return input >= 0 ? input : defaultValue; }
+inline std::vector<float> getService3DArrayParameter(const std::vector<float>& input, const float defaultValue[3]) {
+    return input.size() == 3 ? input : std::vector<float>(defaultValue, defaultValue + 3);
+}
+}  // namespace srvm
+
+namespace pitt {
+
+// ROS parameter server stand-in with roscpp's typed-read rules: a double read as int is rounded
+// (fmod < 0.5 -> floor, else ceil), an int read as double converts, a list reads as vector<float>;
+// any other type mismatch leaves the default (NodeHandle::param).
+class ParamServer {
+public:
+    enum Kind { INT, DOUBLE, STRING, LIST, BOOL };
+    struct Value {
+        Kind kind = DOUBLE;
+        int64_t i = 0;
+        double d = 0;
+        std::string s;
+        std::vector<double> list;
+    };
+    void set(const std::string& k, int v) { Value x; x.kind = INT; x.i = v; m_[k] = x; }
+    void set(const std::string& k, double v) { Value x; x.kind = DOUBLE; x.d = v; m_[k] = x; }
+    void set(const std::string& k, const std::string& v) { Value x; x.kind = STRING; x.s = v; m_[k] = x; }
+    void set(const std::string& k, const std::vector<double>& v) { Value x; x.kind = LIST; x.list = v; m_[k] = x; }
+    void erase(const std::string& k) { m_.erase(k); }
+    void clear() { m_.clear(); }
+
+    bool get(const std::string& k, double& out) const;
+    bool get(const std::string& k, float& out) const;
+    bool get(const std::string& k, int& out) const;
+    bool get(const std::string& k, std::vector<float>& out) const;
+    template <class T, class D>
+    void param(const std::string& k, T& out, const D& def) const {
+        if (!get(k, out)) out = def;
+    }
+
+private:
+    std::map<std::string, Value> m_;
+};
+
+// The three services plus the clients' glue, bound to one MI355X context.
+class SegmentationServices {
+public:
+    explicit SegmentationServices(pitt_ctx* ctx) : ctx_(ctx) {}
+    ParamServer& params() { return params_; }
+    int last_status() const { return status_; }
+
+    // plane_segmentation_srv.cpp:27
+    bool ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                              pitt_msgs::PrimitiveSegmentation::Response& res);
+    // supports_segmentation_srv.cpp:241
+    bool findSupports(pitt_msgs::SupportSegmentation::Request& req, pitt_msgs::SupportSegmentation::Response& res);
+    // cluster_segmentation_srv.cpp:38
+    bool clusterize(pitt_msgs::ClusterSegmentation::Request& req, pitt_msgs::ClusterSegmentation::Response& res);
+
+    // ransac_segmentation.cpp:175-199: accept iff the response holds > 0 inliers (local minInliers = 0, Q2)
+    bool callRansacPlaneSegmentation(const pitt_msgs::PointCloud& cloud, const pitt_msgs::NormalCloud& norm,
+                                     pitt_msgs::PrimitiveSegmentation& out);
+    // obj_segmentation.cpp:143-207 + :261-312: supports (request fields from params, -1 = default),
+    // then clusters per support; one ClustersOutput per support with at least one cluster.
+    std::vector<pitt_msgs::ClustersOutput> segmentObjects(const pitt_msgs::PointCloud& world_cloud,
+                                                          const pitt_msgs::NormalCloud& normals);
+
+private:
+    pitt_ctx* ctx_;
+    ParamServer params_;
+    int status_ = PITT_OK;
+};
+
+}  // namespace pitt

@@ -601,7 +601,9 @@ orc_cluster_list* orc_euclidean_clusters(const float* x, const float* y, const f
     // FLANN L2_Simple: ((dx*dx + dy*dy) + dz*dz) < r2 in float.
     double cell = (double)tol_f * 1.01;
     double mnx = 1e300, mny = 1e300, mnz = 1e300;
+    auto finite = [&](int64_t i) { return std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]); };
     for (int64_t i = 0; i < n; ++i) {
+        if (!finite(i)) continue;
         mnx = std::min(mnx, (double)x[i]);
         mny = std::min(mny, (double)y[i]);
         mnz = std::min(mnz, (double)z[i]);
@@ -612,6 +614,7 @@ orc_cluster_list* orc_euclidean_clusters(const float* x, const float* y, const f
     std::unordered_map<uint64_t, std::vector<int>> grid;
     std::vector<int64_t> gxs((size_t)n), gys((size_t)n), gzs((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
+        if (!finite(i)) continue;  // no radius neighbours (NaN distances): a singleton
         gxs[i] = (int64_t)std::floor(((double)x[i] - mnx) / cell);
         gys[i] = (int64_t)std::floor(((double)y[i] - mny) / cell);
         gzs[i] = (int64_t)std::floor(((double)z[i] - mnz) / cell);
@@ -629,6 +632,7 @@ orc_cluster_list* orc_euclidean_clusters(const float* x, const float* y, const f
         while (sq < q.size()) {
             const int qi = q[sq];
             nn.clear();
+            if (!finite(qi)) { ++sq; continue; }
             for (int dx = -1; dx <= 1; ++dx)
                 for (int dy = -1; dy <= 1; ++dy)
                     for (int dz = -1; dz <= 1; ++dz) {

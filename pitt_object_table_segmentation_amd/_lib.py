@@ -144,11 +144,48 @@ SIGNATURES = {
                                        ctypes.POINTER(ClusterList)]),
     "pitt_synth_frame": (_i32, [_i32, ctypes.c_uint64, _i32, _i32, _f32p, _f32p, _f32p]),
     "pitt_synth_fused": (_i32, [ctypes.c_uint64, _i32, _i32, _i32, _f32p, _f32p, _f32p]),
+    "pitt_sampler_table": (_i32, [_i64, ctypes.c_uint32, _i64, _i32p]),
+    "pitt_float_threshold": (ctypes.c_float, [ctypes.c_double]),
     "pitt_profile_enable": (_i32, [_vp, _i32]),
     "pitt_profile_get": (_i32, [_vp, ctypes.c_char_p, _i64p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_double)]),
     "pitt_profile_reset": (_i32, [_vp]),
 }
+
+
+class SrvSupportRequest(ctypes.Structure):
+    _fields_ = [
+        ("min_iterative_cloud_percentual_size", ctypes.c_float),
+        ("min_iterative_plane_percentual_size", ctypes.c_float),
+        ("variance_threshold_for_horizontal", ctypes.c_float),
+        ("ransac_distance_point_in_shape_threshold", ctypes.c_float),
+        ("ransac_model_normal_distance_weigth", ctypes.c_float),
+        ("ransac_max_iteration_threshold", ctypes.c_int32),
+        ("n_horizontal_axis", ctypes.c_int32),
+        ("horizontal_axis", ctypes.c_float * 8),
+        ("n_edge_remove_offset", ctypes.c_int32),
+        ("edge_remove_offset", ctypes.c_float * 8),
+    ]
+
+
+# include/pitt_srv.h
+SIGNATURES.update({
+    "pitt_srv_create": (_vp, [_vp]),
+    "pitt_srv_destroy": (None, [_vp]),
+    "pitt_srv_param_set_int": (_i32, [_vp, ctypes.c_char_p, _i32]),
+    "pitt_srv_param_set_double": (_i32, [_vp, ctypes.c_char_p, ctypes.c_double]),
+    "pitt_srv_param_set_list": (_i32, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i32]),
+    "pitt_srv_param_erase": (_i32, [_vp, ctypes.c_char_p]),
+    "pitt_srv_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_srv_find_supports": (_i32, [_vp, _f32p, _i64, _i64, ctypes.POINTER(SrvSupportRequest), _i32p, _f32p]),
+    "pitt_srv_support_get": (_i32, [_vp, _i32, _i32p, _f32p, _i64p, _i64p]),
+    "pitt_srv_support_cloud": (_i32, [_vp, _i32, _i32, _f32p]),
+    "pitt_srv_clusterize": (_i32, [_vp, _f32p, _i64, _i32p]),
+    "pitt_srv_cluster_get": (_i32, [_vp, _i32, _i32p, _i64p, _f32p, _f32p]),
+    "pitt_srv_segment_objects": (_i32, [_vp, _f32p, _i64, _i64, _i32p]),
+    "pitt_srv_output_size": (_i32, [_vp, _i32, _i32p]),
+    "pitt_srv_output_cluster": (_i32, [_vp, _i32, _i32, _i32p, _i64p, _f32p]),
+})
 
 
 def _preload_torch_hip_runtime() -> None:

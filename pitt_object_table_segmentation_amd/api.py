@@ -1,0 +1,427 @@
+"""Python surface of the MI355X path: a thin, typed layer over libpitt_seg.so.
+
+Every call crosses the C ABI (include/pitt_seg.h, include/pitt_srv.h); nothing here computes a
+segmentation result.  Device memory comes from torch (plumbing only); host arrays are numpy.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+lib = L.lib
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_f32p)
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(_i32p)
+
+
+class PittError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"pitt error {code}: {msg}")
+        self.code = code
+
+
+def sac_params(threshold: float = 0.007, max_iterations: int = 1000, probability: float = 0.99,
+               seed: int = 12345, optimize: bool = True, reduce_order: int = L.REDUCE_SSE2,
+               div_mode: int = L.DIV_EIGEN32, sampler_slack: int = 64) -> L.SacParams:
+    """SACSegmentation parameters (defaults: plane_segmentation_srv.cpp:19-21)."""
+    p = L.SacParams()
+    lib.pitt_sac_params_default(ctypes.byref(p))
+    p.threshold = threshold
+    p.max_iterations = max_iterations
+    p.probability = probability
+    p.seed = seed
+    p.optimize = 1 if optimize else 0
+    p.reduce_order = reduce_order
+    p.div_mode = div_mode
+    p.sampler_slack = sampler_slack
+    return p
+
+
+def support_params(**kw) -> L.SupportParams:
+    """findSupports parameters (defaults: supports_segmentation_srv.cpp:30-39)."""
+    p = L.SupportParams()
+    lib.pitt_support_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        if k in ("horizontal_axis", "edge_remove_offset"):
+            getattr(p, k)[:] = [float(t) for t in v]
+        else:
+            setattr(p, k, v)
+    return p
+
+
+RESULT_DTYPE = np.dtype([("coefficients", np.float32, 4), ("n_coeff", np.int32), ("status", np.int32),
+                         ("n_inliers", np.int64), ("hypotheses", np.int32), ("best_hypothesis", np.int32),
+                         ("best_count", np.int64), ("rejected_samples", np.int32), ("flags", np.int32)])
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(L.PlaneResult)
+
+
+@dataclass
+class PlaneModel:
+    inliers: np.ndarray                 # int32, ascending (exact PCL semantics, index 0 kept)
+    coefficients: np.ndarray            # float32[4], or empty when no model
+    status: int = L.PITT_OK
+
+
+@dataclass
+class SupportResult:
+    idx_map: np.ndarray                 # int32[n]: Support::inliers
+    coefficients: np.ndarray            # float32[4] (refined)
+    support_cloud: np.ndarray           # float32[m, 3]
+    on_support_cloud: np.ndarray        # float32[k, 3]
+
+
+@dataclass
+class ClusterResult:
+    indices: np.ndarray                 # int32, ascending
+    sum_xyz: np.ndarray                 # float32[3], float sums in index order
+
+
+def synth_frame(scene: int = L.SCENE_TABLE, seed: int = 1000, width: int = 640, height: int = 480):
+    """Deterministic synthetic organised cloud (camera optical frame), SoA float32."""
+    n = width * height
+    x, y, z = (np.empty(n, np.float32) for _ in range(3))
+    rc = lib.pitt_synth_frame(scene, ctypes.c_uint64(seed), width, height, _fp(x), _fp(y), _fp(z))
+    if rc != L.PITT_OK:
+        raise PittError(rc, "pitt_synth_frame")
+    return x, y, z
+
+
+def synth_fused(seed: int = 1000, views: int = 4, width: int = 640, height: int = 480):
+    """`views` views of one table scene in a z-up world frame, concatenated (config 5)."""
+    n = views * width * height
+    x, y, z = (np.empty(n, np.float32) for _ in range(3))
+    rc = lib.pitt_synth_fused(ctypes.c_uint64(seed), views, width, height, _fp(x), _fp(y), _fp(z))
+    if rc != L.PITT_OK:
+        raise PittError(rc, "pitt_synth_fused")
+    return x, y, z
+
+
+def sampler_table(n: int, attempts: int, seed: int = 12345) -> np.ndarray:
+    out = np.empty(3 * attempts, np.int32)
+    rc = lib.pitt_sampler_table(n, seed, attempts, _ip(out))
+    if rc != L.PITT_OK:
+        raise PittError(rc, "pitt_sampler_table")
+    return out.reshape(attempts, 3)
+
+
+def float_threshold(th: float) -> np.float32:
+    return np.float32(lib.pitt_float_threshold(th))
+
+
+def padded_offsets(counts: Sequence[int], tile: int = L.PITT_TILE_POINTS):
+    """Frame offsets for a packed batch where every frame starts on a tile boundary; returns
+    (offsets, capacity)."""
+    offs, o = [], 0
+    for c in counts:
+        offs.append(o)
+        o += max(tile, -(-int(c) // tile) * tile)
+    return np.asarray(offs, np.int64), o
+
+
+class FrameBatch:
+    """Device-resident SoA batch (torch tensors on the context's device)."""
+
+    def __init__(self, x, y, z, offsets: np.ndarray, counts: np.ndarray, capacity: int):
+        self.x, self.y, self.z = x, y, z
+        self.offsets = np.ascontiguousarray(offsets, np.int64)
+        self.counts = np.ascontiguousarray(counts, np.int64)
+        self.capacity = int(capacity)
+
+    @property
+    def n_frames(self) -> int:
+        return len(self.counts)
+
+    @classmethod
+    def from_host(cls, frames: Sequence[tuple], device="cuda"):
+        import torch
+        counts = np.asarray([len(f[0]) for f in frames], np.int64)
+        offsets, cap = padded_offsets(counts)
+        planes = []
+        for c in range(3):
+            h = np.full(cap, np.nan, np.float32)
+            for f, o, n in zip(frames, offsets, counts):
+                h[o:o + n] = f[c]
+            planes.append(torch.from_numpy(h).to(device))
+        return cls(planes[0], planes[1], planes[2], offsets, counts, cap)
+
+    def abi(self) -> L.Frames:
+        self._keep = (self.offsets, self.counts)
+        return L.Frames(self.x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(),
+                        self.offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                        self.counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                        self.n_frames, self.capacity)
+
+
+class Context:
+    """One pitt_ctx: a device, a stream and its scratch arena.  Not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        rc = lib.pitt_create(ctypes.byref(h), device)
+        if rc != L.PITT_OK:
+            raise PittError(rc, "pitt_create (needs a gfx950 device)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib.pitt_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            raise PittError(rc, f"{what}: {lib.pitt_last_error(self.h).decode()}")
+        return rc
+
+    def set_stream(self, stream) -> None:
+        handle = getattr(stream, "cuda_stream", stream)
+        self._check(lib.pitt_set_stream(self.h, ctypes.c_void_p(handle or 0)), "pitt_set_stream")
+
+    # ---- plane -----------------------------------------------------------------------------
+    def plane_segment(self, cloud: np.ndarray, params: Optional[L.SacParams] = None) -> PlaneModel:
+        """seg.segment() on one host cloud: (n, 3) or (n, 4) float32 (PCL PointXYZ)."""
+        cloud = np.ascontiguousarray(cloud, np.float32)
+        n = cloud.shape[0]
+        stride = 4 * cloud.shape[1] if cloud.ndim == 2 else 12
+        p = params or sac_params()
+        inl = np.empty(max(n, 1), np.int32)
+        ni = ctypes.c_int64()
+        co = np.zeros(4, np.float32)
+        nc = ctypes.c_int32()
+        rc = self._check(lib.pitt_plane_segment(self.h, _fp(cloud), n, stride, ctypes.byref(p), _ip(inl),
+                                                ctypes.byref(ni), _fp(co), ctypes.byref(nc)), "pitt_plane_segment")
+        return PlaneModel(inl[:ni.value].copy(), co[:nc.value].copy(), rc)
+
+    def plane_segment_batch(self, batch: FrameBatch, params: Optional[L.SacParams] = None,
+                            inliers_out=None) -> np.ndarray:
+        """Batched seg.segment(); returns a RESULT_DTYPE record per frame.  inliers_out: optional
+        int32 device tensor of batch.capacity entries (frame f at batch.offsets[f])."""
+        p = params or sac_params()
+        res = np.zeros(batch.n_frames, RESULT_DTYPE)
+        fr = batch.abi()
+        ptr = ctypes.c_void_p(inliers_out.data_ptr()) if inliers_out is not None else ctypes.c_void_p()
+        self._check(lib.pitt_plane_segment_batch(self.h, ctypes.byref(fr), ctypes.byref(p),
+                                                 res.ctypes.data_as(ctypes.POINTER(L.PlaneResult)), ptr),
+                    "pitt_plane_segment_batch")
+        return res
+
+    def hypothesis_counts(self, frame: int, cap: int) -> np.ndarray:
+        out = np.zeros(cap, np.int32)
+        self._check(lib.pitt_last_hypothesis_counts(self.h, frame, _ip(out), cap), "hypothesis_counts")
+        return out
+
+    # ---- ExtractIndices ---------------------------------------------------------------------
+    def extract_indices(self, x, y, z, indices, negative: bool):
+        """Device tensors in/out; returns (ox, oy, oz) trimmed to the output size."""
+        import torch
+        n = x.numel()
+        m = indices.numel()
+        size = m if not negative else n
+        ox, oy, oz = (torch.empty(max(size, 1), dtype=torch.float32, device=x.device) for _ in range(3))
+        nout = ctypes.c_int64()
+        self._check(lib.pitt_extract_indices(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n,
+                                             indices.data_ptr() if m else None, m, 1 if negative else 0,
+                                             ox.data_ptr(), oy.data_ptr(), oz.data_ptr(), ctypes.byref(nout)),
+                    "pitt_extract_indices")
+        k = nout.value
+        return ox[:k], oy[:k], oz[:k]
+
+    # ---- supports ---------------------------------------------------------------------------
+    def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
+        x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+        p = params or support_params()
+        out = L.SupportList()
+        self._check(lib.pitt_find_supports(self.h, _fp(x), _fp(y), _fp(z), len(x), ctypes.byref(p),
+                                           ctypes.byref(out)), "pitt_find_supports")
+        res = []
+        for i in range(out.n_supports):
+            s = out.supports[i]
+            ns, no = s.n_support, s.n_on_support
+            sup = np.ctypeslib.as_array(s.support_xyz, (3 * ns,)).reshape(3, ns).T.copy() if ns else np.zeros((0, 3), np.float32)
+            on = np.ctypeslib.as_array(s.on_support_xyz, (3 * no,)).reshape(3, no).T.copy() if no else np.zeros((0, 3), np.float32)
+            res.append(SupportResult(np.ctypeslib.as_array(s.idx_map, (s.n_points,)).copy(),
+                                     np.array(list(s.coefficients), np.float32), sup, on))
+        return res
+
+    # ---- clusters ---------------------------------------------------------------------------
+    def euclidean_clusters(self, x, y, z, tolerance: float = 0.03, min_size: int = 1,
+                           max_size: int = 2 ** 31 - 1) -> List[ClusterResult]:
+        x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+        out = L.ClusterList()
+        self._check(lib.pitt_euclidean_clusters(self.h, _fp(x), _fp(y), _fp(z), len(x), tolerance, min_size,
+                                                max_size, ctypes.byref(out)), "pitt_euclidean_clusters")
+        res = []
+        for i in range(out.n_clusters):
+            c = out.clusters[i]
+            idx = np.ctypeslib.as_array(c.indices, (c.size,)).copy() if c.size else np.zeros(0, np.int32)
+            res.append(ClusterResult(idx, np.array(list(c.sum_xyz), np.float32)))
+        return res
+
+    # ---- profiling --------------------------------------------------------------------------
+    def profile(self, on: bool = True) -> None:
+        lib.pitt_profile_enable(self.h, 1 if on else 0)
+
+    def profile_reset(self) -> None:
+        lib.pitt_profile_reset(self.h)
+
+    def profile_get(self, kernel: str):
+        n, ms, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        self._check(lib.pitt_profile_get(self.h, kernel.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(b)),
+                    "pitt_profile_get")
+        return n.value, ms.value, b.value
+
+
+def _cloud16(xyz: np.ndarray) -> np.ndarray:
+    """(n, 3) -> PCL PointXYZ layout (n, 4) with the pad = 1.0f."""
+    xyz = np.asarray(xyz, np.float32)
+    if xyz.ndim == 2 and xyz.shape[1] == 4:
+        return np.ascontiguousarray(xyz)
+    out = np.ones((xyz.shape[0], 4), np.float32)
+    out[:, :3] = xyz
+    return out
+
+
+class Services:
+    """The reference's three service handlers + obj_segmentation glue (C++ mirror, pitt_srv.h)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.h = lib.pitt_srv_create(ctx.h)
+        if not self.h:
+            raise PittError(L.PITT_E_INVALID, "pitt_srv_create")
+
+    def close(self):
+        if self.h:
+            lib.pitt_srv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_param(self, name: str, value) -> None:
+        if isinstance(value, bool) or isinstance(value, int):
+            lib.pitt_srv_param_set_int(self.h, name.encode(), int(value))
+        elif isinstance(value, float):
+            lib.pitt_srv_param_set_double(self.h, name.encode(), value)
+        else:
+            arr = (ctypes.c_double * len(value))(*[float(v) for v in value])
+            lib.pitt_srv_param_set_list(self.h, name.encode(), arr, len(value))
+
+    def erase_param(self, name: str) -> None:
+        lib.pitt_srv_param_erase(self.h, name.encode())
+
+    def _rc(self, rc: int, what: str) -> bool:
+        if rc < 0:
+            raise PittError(rc, f"{what}: {lib.pitt_last_error(self.ctx.h).decode()}")
+        return rc == 1
+
+    def ransac_plane(self, cloud: np.ndarray, n_normals: Optional[int] = None):
+        """ransacPlaneDetaction: returns (ok, inliers (index 0 dropped), coefficients, centroid)."""
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        inl = np.empty(max(n, 1), np.int32)
+        ni, nc = ctypes.c_int64(), ctypes.c_int32()
+        co = np.zeros(4, np.float32)
+        ce = np.zeros(3, np.float32)
+        ok = self._rc(lib.pitt_srv_ransac_plane(self.h, _fp(c), n, n if n_normals is None else n_normals, _ip(inl),
+                                                ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)), "ransac_plane")
+        return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
+
+    def find_supports(self, cloud: np.ndarray, n_normals: Optional[int] = None, **req):
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        r = L.SrvSupportRequest()
+        r.min_iterative_cloud_percentual_size = req.get("min_iterative_cloud_percentual_size", -1.0)
+        r.min_iterative_plane_percentual_size = req.get("min_iterative_plane_percentual_size", -1.0)
+        r.variance_threshold_for_horizontal = req.get("variance_threshold_for_horizontal", -1.0)
+        r.ransac_distance_point_in_shape_threshold = req.get("ransac_distance_point_in_shape_threshold", -1.0)
+        r.ransac_model_normal_distance_weigth = req.get("ransac_model_normal_distance_weigth", -1.0)
+        r.ransac_max_iteration_threshold = req.get("ransac_max_iteration_threshold", -1)
+        ax = list(req.get("horizontal_axis", [-1.0]))
+        of = list(req.get("support_edge_remove_offset", [-1.0]))
+        r.n_horizontal_axis = len(ax)
+        r.horizontal_axis[:len(ax)] = ax
+        r.n_edge_remove_offset = len(of)
+        r.edge_remove_offset[:len(of)] = of
+        ns = ctypes.c_int32()
+        used = np.zeros(13, np.float32)
+        ok = self._rc(lib.pitt_srv_find_supports(self.h, _fp(c), n, n if n_normals is None else n_normals,
+                                                 ctypes.byref(r), ctypes.byref(ns), _fp(used)), "find_supports")
+        sups = []
+        for s in range(ns.value):
+            idx = np.empty(max(n, 1), np.int32)
+            co = np.zeros(4, np.float32)
+            a, b = ctypes.c_int64(), ctypes.c_int64()
+            lib.pitt_srv_support_get(self.h, s, _ip(idx), _fp(co), ctypes.byref(a), ctypes.byref(b))
+            sc = np.empty((max(a.value, 1), 4), np.float32)
+            oc = np.empty((max(b.value, 1), 4), np.float32)
+            lib.pitt_srv_support_cloud(self.h, s, 0, _fp(sc))
+            lib.pitt_srv_support_cloud(self.h, s, 1, _fp(oc))
+            sups.append(dict(inliers=idx[:n].copy(), coefficients=co, support_cloud=sc[:a.value, :3].copy(),
+                             on_support_cloud=oc[:b.value, :3].copy()))
+        return ok, sups, used
+
+    def clusterize(self, cloud: np.ndarray):
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        nc = ctypes.c_int32()
+        ok = self._rc(lib.pitt_srv_clusterize(self.h, _fp(c), n, ctypes.byref(nc)), "clusterize")
+        out = []
+        for k in range(nc.value):
+            size = ctypes.c_int64()
+            lib.pitt_srv_cluster_get(self.h, k, None, ctypes.byref(size), None, None)
+            idx = np.empty(max(size.value, 1), np.int32)
+            ce = np.zeros(3, np.float32)
+            cl = np.empty((max(size.value, 1), 4), np.float32)
+            lib.pitt_srv_cluster_get(self.h, k, _ip(idx), ctypes.byref(size), _fp(ce), _fp(cl))
+            out.append(dict(inliers=idx[:size.value].copy(), centroid=ce, cloud=cl[:size.value, :3].copy()))
+        return ok, out
+
+    def segment_objects(self, cloud: np.ndarray, n_normals: Optional[int] = None):
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        no = ctypes.c_int32()
+        self._rc(lib.pitt_srv_segment_objects(self.h, _fp(c), n, n if n_normals is None else n_normals,
+                                              ctypes.byref(no)), "segment_objects")
+        outs = []
+        for o in range(no.value):
+            k = ctypes.c_int32()
+            lib.pitt_srv_output_size(self.h, o, ctypes.byref(k))
+            objs = []
+            for c_ in range(k.value):
+                size = ctypes.c_int64()
+                lib.pitt_srv_output_cluster(self.h, o, c_, None, ctypes.byref(size), None)
+                idx = np.empty(max(size.value, 1), np.int32)
+                ce = np.zeros(3, np.float32)
+                lib.pitt_srv_output_cluster(self.h, o, c_, _ip(idx), ctypes.byref(size), _fp(ce))
+                objs.append(dict(inliers=idx[:size.value].copy(), centroid=ce))
+            outs.append(objs)
+        return outs

@@ -1,0 +1,61 @@
+// compact.hpp -- order-preserving stream compaction over per-point predicates (ExtractIndices,
+// createNewIdxMap's running counter, getPointOnPlane's output, cluster member lists).
+//
+// Layout: 256-thread blocks own 2048-point tiles; thread t owns the 8 CONSECUTIVE points
+// [8t, 8t+8) of its tile so a block-wide exclusive scan of per-thread counts yields output
+// positions in ascending point order.  Three launches: count per tile, scan of tile counts,
+// write.  All kernels are persistent grid-stride loops over tiles.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+
+namespace pitt {
+
+constexpr int kCTile = 2048;
+
+__host__ __device__ inline int64_t ctiles(int64_t n) { return (n + kCTile - 1) / kCTile; }
+
+// Pred: __device__ bool operator()(int64_t i) const  (i < n guaranteed by the caller)
+template <class Pred>
+__global__ __launch_bounds__(kBlock) void k_pred_count(Pred pred, int64_t n, int32_t* __restrict__ tile_counts) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int64_t nt = ctiles(n);
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const int64_t b = t * kCTile + threadIdx.x * 8;
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c += (b + k < n && pred(b + k)) ? 1 : 0;
+        int total;
+        (void)block_exscan(c, lds4, &total);
+        if (threadIdx.x == 0) tile_counts[t] = total;
+    }
+}
+
+// Single-block exclusive scan: offsets[t] for t < nt, offsets[nt] = total.
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(const int32_t* __restrict__ counts, int64_t nt,
+                                                       int32_t* __restrict__ offsets);
+
+// Action: __device__ void operator()(int64_t i, int64_t pos) const  -- point i is output #pos
+template <class Pred, class Action>
+__global__ __launch_bounds__(kBlock) void k_pred_apply(Pred pred, Action act, int64_t n,
+                                                       const int32_t* __restrict__ offsets) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const int64_t nt = ctiles(n);
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const int64_t b = t * kCTile + threadIdx.x * 8;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bits |= ((b + k < n && pred(b + k)) ? 1u : 0u) << k;
+        int total;
+        int pos = block_exscan(__builtin_popcount(bits), lds4, &total) + offsets[t];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if ((bits >> k) & 1u) act(b + k, (int64_t)pos++);
+    }
+}
+
+inline int grid_for_tiles(int64_t nt) { return (int)(nt < 1 ? 1 : (nt > 2048 ? 2048 : nt)); }
+
+}  // namespace pitt

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <map>
+#include <tuple>
 #include <string>
 #include <unordered_map>
 #include <vector>

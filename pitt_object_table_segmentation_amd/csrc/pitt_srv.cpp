@@ -1,0 +1,442 @@
+// pitt_srv.cpp -- the service mirror: the reference's handler logic above the C ABI.
+// Reference paths cited per function.  No arithmetic of the path lives here; it is parameter
+// resolution, message assembly and the reference's post-processing (Q1, Q2, Q3, Q6, Q7).
+#include "../../include/pitt_srv.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pitt_srv.h"
+
+namespace pitt {
+
+// ---- ParamServer: roscpp param.cpp getImpl typed reads ---------------------------------------
+bool ParamServer::get(const std::string& k, double& out) const {
+    auto it = m_.find(k);
+    if (it == m_.end()) return false;
+    if (it->second.kind == INT) { out = (double)it->second.i; return true; }
+    if (it->second.kind == DOUBLE) { out = it->second.d; return true; }
+    return false;
+}
+bool ParamServer::get(const std::string& k, float& out) const {
+    double d;
+    if (!get(k, d)) return false;
+    out = (float)d;
+    return true;
+}
+bool ParamServer::get(const std::string& k, int& out) const {
+    auto it = m_.find(k);
+    if (it == m_.end()) return false;
+    if (it->second.kind == INT) { out = (int)it->second.i; return true; }
+    if (it->second.kind == DOUBLE) {  // roscpp rounds a double read as int
+        double d = it->second.d;
+        d = std::fmod(d, 1.0) < 0.5 ? std::floor(d) : std::ceil(d);
+        out = (int)d;
+        return true;
+    }
+    return false;
+}
+bool ParamServer::get(const std::string& k, std::vector<float>& out) const {
+    auto it = m_.find(k);
+    if (it == m_.end() || it->second.kind != LIST) return false;
+    out.assign(it->second.list.begin(), it->second.list.end());
+    return true;
+}
+
+namespace {
+void to_soa(const pitt_msgs::PointCloud& c, std::vector<float>& x, std::vector<float>& y, std::vector<float>& z) {
+    const size_t n = c.size();
+    x.resize(n);
+    y.resize(n);
+    z.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        x[i] = c.data[4 * i];
+        y[i] = c.data[4 * i + 1];
+        z[i] = c.data[4 * i + 2];
+    }
+}
+}  // namespace
+
+// plane_segmentation_srv.cpp:27-74
+bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                                                pitt_msgs::PrimitiveSegmentation::Response& res) {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, epsAngleTh, minOpeningAngle, maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_PLANE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
+    params_.param(srvm::PARAM_NAME_PLANE_DISTANCE_TH, distanceThreshold, 0.007);
+    params_.param(srvm::PARAM_NAME_PLANE_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_PLANE_EPS_ANGLE_TH, epsAngleTh, 0.0);
+    params_.param(srvm::PARAM_NAME_PLANE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 0.0);
+    params_.param(srvm::PARAM_NAME_PLANE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 10.0);
+    (void)normalDistanceWeight; (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;  // unused by SACMODEL_PLANE (A1)
+
+    pitt_sac_params p;
+    pitt_sac_params_default(&p);
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    std::vector<int32_t> inl(req.cloud.size());
+    int64_t n_inl = 0;
+    float coef[4] = {0, 0, 0, 0};
+    int32_t n_coef = 0;
+    status_ = PITT_OK;
+    // SACSegmentationFromNormals::initSACModel: the normals must match the cloud, else PCL clears
+    // the outputs (A1).
+    if (req.normals.size() == req.cloud.size()) {
+        status_ = pitt_plane_segment(ctx_, req.cloud.data.data(), (int64_t)req.cloud.size(), 16, &p, inl.data(),
+                                     &n_inl, coef, &n_coef);
+        if (status_ < 0) { n_inl = 0; n_coef = 0; }
+    }
+    // PCManager::inlierToVectorMsg (pc_manager.cpp:105-111): drops index 0 (Q1)
+    res.inliers.clear();
+    for (int64_t i = 0; i < n_inl; ++i)
+        if (inl[(size_t)i] != 0) res.inliers.push_back(inl[(size_t)i]);
+    // coefficientToVectorMsg (:112-117)
+    res.coefficients.assign(coef, coef + n_coef);
+    return true;
+}
+
+// supports_segmentation_srv.cpp:241-361 (+ initializeInputParameters :70-86)
+bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request& req,
+                                        pitt_msgs::SupportSegmentation::Response& res) {
+    static const float kAxis[3] = {0.0f, 0.0f, -1.0f};
+    static const float kOffset[3] = {0.02f, 0.02f, 0.005f};
+    const float minCloud = srvm::getServiceFloatParameter(req.min_iterative_cloud_percentual_size, 0.030f);
+    const float minPlane = srvm::getServiceFloatParameter(req.min_iterative_plane_percentual_size, 0.030f);
+    const float maxVar = srvm::getServiceFloatParameter(req.variance_threshold_for_horizontal, 0.09f);
+    const float minVar = -1 * maxVar;
+    const float th = srvm::getServiceFloatParameter(req.ransac_distance_point_in_shape_threshold, 0.02f);
+    const float ndw = srvm::getServiceFloatParameter(req.ransac_model_normal_distance_weigth, 0.9f);
+    const int maxIt = srvm::getServiceIntParameter(req.ransac_max_iteration_threshold, 10);
+    const std::vector<float> axis = srvm::getService3DArrayParameter(req.horizontal_axis, kAxis);
+    const std::vector<float> off = srvm::getService3DArrayParameter(req.support_edge_remove_offset, kOffset);
+
+    res.supports_description.clear();
+    status_ = PITT_OK;
+    // The first RANSAC call runs with the request's normals: a size mismatch fails it (A1) and the
+    // loop exits before any support is found.  Later rounds re-estimate normals of matching size.
+    if (req.input_norm.size() == req.input_cloud.size()) {
+        pitt_support_params sp;
+        pitt_support_params_default(&sp);
+        sp.min_iterative_cloud_percentage = minCloud;
+        sp.min_iterative_plane_percentage = minPlane;
+        sp.horizontal_variance_threshold = maxVar;
+        sp.ransac_distance_threshold = th;
+        sp.ransac_max_iterations = maxIt;
+        for (int i = 0; i < 3; ++i) {
+            sp.horizontal_axis[i] = axis[(size_t)i];
+            sp.edge_remove_offset[i] = off[(size_t)i];
+        }
+        std::vector<float> x, y, z;
+        to_soa(req.input_cloud, x, y, z);
+        pitt_support_list L;
+        status_ = pitt_find_supports(ctx_, x.data(), y.data(), z.data(), (int64_t)x.size(), &sp, &L);
+        if (status_ == PITT_OK) {
+            for (int s = 0; s < L.n_supports; ++s) {
+                const pitt_support& su = L.supports[s];
+                pitt_msgs::Support m;
+                m.inliers.assign(su.idx_map, su.idx_map + su.n_points);
+                for (int64_t i = 0; i < su.n_support; ++i)
+                    m.support_cloud.push_back(su.support_xyz[i], su.support_xyz[su.n_support + i],
+                                              su.support_xyz[2 * su.n_support + i]);
+                for (int64_t i = 0; i < su.n_on_support; ++i)
+                    m.on_support_cloud.push_back(su.on_support_xyz[i], su.on_support_xyz[su.n_on_support + i],
+                                                 su.on_support_xyz[2 * su.n_on_support + i]);
+                m.support_coefficient_a = su.coefficients[0];
+                m.support_coefficient_b = su.coefficients[1];
+                m.support_coefficient_c = su.coefficients[2];
+                m.support_coefficient_d = su.coefficients[3];
+                res.supports_description.push_back(std::move(m));
+            }
+        }
+    }
+    res.used_min_iterative_cloud_percentual_size = minCloud;
+    res.used_min_iterative_plane_percentual_size = minPlane;
+    res.used_max_variance_threshold_for_horizontal = maxVar;
+    res.used_min_variance_threshold_for_horizontal = minVar;
+    res.used_ransac_max_iteration_threshold = maxIt;
+    res.used_ransac_distance_point_in_shape_threshold = th;
+    res.used_ransac_model_normal_distance_weigth = ndw;
+    res.used_horizontal_axis = axis;
+    res.used_support_edge_remove_offset = off;
+    return true;
+}
+
+// cluster_segmentation_srv.cpp:38-108
+bool SegmentationServices::clusterize(pitt_msgs::ClusterSegmentation::Request& req,
+                                      pitt_msgs::ClusterSegmentation::Response& res) {
+    double tolerance, minClusterSizeRate, maxClusterSizeRate;
+    int minInputSize;
+    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, tolerance, 0.03);
+    params_.param(srvm::PARAM_NAME_CLUSTER_MIN_RATE, minClusterSizeRate, 0.01);
+    params_.param(srvm::PARAM_NAME_CLUSTER_MAX_RATE, maxClusterSizeRate, 0.99);
+    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, minInputSize, 30);  // Q6: the tolerance name
+    res.cluster_objs.clear();
+    status_ = PITT_OK;
+    const size_t n = req.cloud.size();
+    if (n >= (size_t)(int64_t)minInputSize) {
+        const int mn = (int)std::round((double)n * minClusterSizeRate);
+        const int mx = (int)std::round((double)n * maxClusterSizeRate);
+        std::vector<float> x, y, z;
+        to_soa(req.cloud, x, y, z);
+        pitt_cluster_list L;
+        status_ = pitt_euclidean_clusters(ctx_, x.data(), y.data(), z.data(), (int64_t)n, tolerance, mn, mx, &L);
+        if (status_ == PITT_OK) {
+            for (int c = 0; c < L.n_clusters; ++c) {
+                const pitt_cluster& cl = L.clusters[c];
+                pitt_msgs::InliersCluster m;
+                m.inliers.assign(cl.indices, cl.indices + cl.size);
+                for (int64_t k = 0; k < cl.size; ++k) {
+                    const int32_t i = cl.indices[k];
+                    m.cloud.push_back(x[(size_t)i], y[(size_t)i], z[(size_t)i]);
+                }
+                const int cnt = (int)cl.size + 1;  // Q7: the counter starts at 1
+                m.x_centroid = cl.sum_xyz[0] / cnt;
+                m.y_centroid = cl.sum_xyz[1] / cnt;
+                m.z_centroid = cl.sum_xyz[2] / cnt;
+                res.cluster_objs.push_back(std::move(m));
+            }
+        }
+    }
+    return true;
+}
+
+// ransac_segmentation.cpp:175-199
+bool SegmentationServices::callRansacPlaneSegmentation(const pitt_msgs::PointCloud& cloud,
+                                                       const pitt_msgs::NormalCloud& norm,
+                                                       pitt_msgs::PrimitiveSegmentation& out) {
+    pitt_msgs::PrimitiveSegmentation srv;
+    srv.request.cloud = cloud;
+    srv.request.normals = norm;
+    if (ransacPlaneDetaction(srv.request, srv.response)) {
+        const int minInliers = 0;  // Q2: the /pitt/srv/plane_segmentation/min_inliers param is read but unused
+        if (srv.response.inliers.size() > (size_t)minInliers) {
+            out = srv;
+            return true;
+        }
+    }
+    return false;
+}
+
+// obj_segmentation.cpp:143-207 (callSupportFilter) and :261-312 (support -> cluster glue)
+std::vector<pitt_msgs::ClustersOutput> SegmentationServices::segmentObjects(const pitt_msgs::PointCloud& world_cloud,
+                                                                            const pitt_msgs::NormalCloud& normals) {
+    pitt_msgs::SupportSegmentation srv;
+    srv.request.input_cloud = world_cloud;
+    srv.request.input_norm = normals;
+    params_.param(srvm::PARAM_NAME_MIN_ITERATIVE_CLOUD_PERCENTAGE, srv.request.min_iterative_cloud_percentual_size,
+                  srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
+    params_.param(srvm::PARAM_NAME_MIN_ITERATIVE_SUPPORT_PERCENTAGE, srv.request.min_iterative_plane_percentual_size,
+                  srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
+    params_.param(srvm::PARAM_NAME_HORIZONTAL_VARIANCE_THRESHOLD, srv.request.variance_threshold_for_horizontal,
+                  srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
+    params_.param(srvm::PARAM_NAME_RANSAC_IN_SHAPE_DISTANCE_POINT_THRESHOLD,
+                  srv.request.ransac_distance_point_in_shape_threshold, srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
+    params_.param(srvm::PARAM_NAME_RANSAC_MODEL_NORMAL_DISTANCE_WEIGHT, srv.request.ransac_model_normal_distance_weigth,
+                  srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
+    params_.param(srvm::PARAM_NAME_RANSAC_MAX_ITERATION_THRESHOLD, srv.request.ransac_max_iteration_threshold,
+                  srvm::DEFAULT_SERVICE_PARAMETER_REQUEST);
+    params_.param(srvm::PARAM_NAME_HORIZONTAL_AXIS, srv.request.horizontal_axis, std::vector<float>(1, -1.0f));
+    params_.param(srvm::PARAM_NAME_SUPPORT_EDGE_REMOVE_OFFSET, srv.request.support_edge_remove_offset,
+                  std::vector<float>(1, -1.0f));
+    std::vector<pitt_msgs::ClustersOutput> outs;
+    if (!findSupports(srv.request, srv.response)) return outs;
+    for (pitt_msgs::Support& s : srv.response.supports_description) {
+        pitt_msgs::ClusterSegmentation cs;
+        cs.request.cloud = s.on_support_cloud;
+        clusterize(cs.request, cs.response);
+        if (!cs.response.cluster_objs.empty()) {
+            pitt_msgs::ClustersOutput o;
+            o.cluster_objs = cs.response.cluster_objs;
+            outs.push_back(std::move(o));
+        }
+    }
+    return outs;
+}
+
+}  // namespace pitt
+
+// ---- C ABI (pitt_srv.h) -----------------------------------------------------------------------
+struct pitt_srv {
+    pitt::SegmentationServices svc;
+    pitt_msgs::SupportSegmentation::Response supports;
+    pitt_msgs::ClusterSegmentation::Response clusters;
+    std::vector<pitt_msgs::ClustersOutput> outputs;
+    explicit pitt_srv(pitt_ctx* c) : svc(c) {}
+};
+
+namespace {
+pitt_msgs::PointCloud cloud_from(const float* xyz16, int64_t n) {
+    pitt_msgs::PointCloud c;
+    if (n > 0) c.data.assign(xyz16, xyz16 + 4 * n);
+    return c;
+}
+}  // namespace
+
+extern "C" {
+
+pitt_srv* pitt_srv_create(pitt_ctx* ctx) { return ctx ? new pitt_srv(ctx) : nullptr; }
+void pitt_srv_destroy(pitt_srv* s) { delete s; }
+
+int pitt_srv_param_set_int(pitt_srv* s, const char* k, int32_t v) {
+    if (!s || !k) return PITT_E_INVALID;
+    s->svc.params().set(k, (int)v);
+    return PITT_OK;
+}
+int pitt_srv_param_set_double(pitt_srv* s, const char* k, double v) {
+    if (!s || !k) return PITT_E_INVALID;
+    s->svc.params().set(k, v);
+    return PITT_OK;
+}
+int pitt_srv_param_set_list(pitt_srv* s, const char* k, const double* v, int32_t n) {
+    if (!s || !k || (n > 0 && !v) || n < 0) return PITT_E_INVALID;
+    s->svc.params().set(k, std::vector<double>(v, v + n));
+    return PITT_OK;
+}
+int pitt_srv_param_erase(pitt_srv* s, const char* k) {
+    if (!s || !k) return PITT_E_INVALID;
+    s->svc.params().erase(k);
+    return PITT_OK;
+}
+
+int pitt_srv_ransac_plane(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals, int32_t* inliers_out,
+                          int64_t* n_inliers, float* coefficients_out, int32_t* n_coefficients, float centroid_out[3]) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_inliers || !n_coefficients) return PITT_E_INVALID;
+    pitt_msgs::PrimitiveSegmentation srv;
+    srv.request.cloud = cloud_from(xyz16, n);
+    srv.request.normals.n = (size_t)n_normals;
+    bool ok = s->svc.ransacPlaneDetaction(srv.request, srv.response);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    *n_inliers = (int64_t)srv.response.inliers.size();
+    *n_coefficients = (int32_t)srv.response.coefficients.size();
+    if (inliers_out && !srv.response.inliers.empty())
+        std::memcpy(inliers_out, srv.response.inliers.data(), srv.response.inliers.size() * 4);
+    if (coefficients_out && !srv.response.coefficients.empty())
+        std::memcpy(coefficients_out, srv.response.coefficients.data(), srv.response.coefficients.size() * 4);
+    if (centroid_out) {
+        centroid_out[0] = srv.response.x_centroid;
+        centroid_out[1] = srv.response.y_centroid;
+        centroid_out[2] = srv.response.z_centroid;
+    }
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_find_supports(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals,
+                           const pitt_srv_support_request* r, int32_t* n_supports, float used_out[13]) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !r || !n_supports) return PITT_E_INVALID;
+    pitt_msgs::SupportSegmentation srv;
+    srv.request.input_cloud = cloud_from(xyz16, n);
+    srv.request.input_norm.n = (size_t)n_normals;
+    srv.request.min_iterative_cloud_percentual_size = r->min_iterative_cloud_percentual_size;
+    srv.request.min_iterative_plane_percentual_size = r->min_iterative_plane_percentual_size;
+    srv.request.variance_threshold_for_horizontal = r->variance_threshold_for_horizontal;
+    srv.request.ransac_distance_point_in_shape_threshold = r->ransac_distance_point_in_shape_threshold;
+    srv.request.ransac_model_normal_distance_weigth = r->ransac_model_normal_distance_weigth;
+    srv.request.ransac_max_iteration_threshold = r->ransac_max_iteration_threshold;
+    srv.request.horizontal_axis.assign(r->horizontal_axis, r->horizontal_axis + std::max(0, std::min(8, r->n_horizontal_axis)));
+    srv.request.support_edge_remove_offset.assign(r->edge_remove_offset,
+                                                  r->edge_remove_offset + std::max(0, std::min(8, r->n_edge_remove_offset)));
+    bool ok = s->svc.findSupports(srv.request, srv.response);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    s->supports = std::move(srv.response);
+    *n_supports = (int32_t)s->supports.supports_description.size();
+    if (used_out) {
+        const auto& u = s->supports;
+        used_out[0] = u.used_min_iterative_cloud_percentual_size;
+        used_out[1] = u.used_min_iterative_plane_percentual_size;
+        used_out[2] = u.used_max_variance_threshold_for_horizontal;
+        used_out[3] = u.used_min_variance_threshold_for_horizontal;
+        used_out[4] = (float)u.used_ransac_max_iteration_threshold;
+        used_out[5] = u.used_ransac_distance_point_in_shape_threshold;
+        used_out[6] = u.used_ransac_model_normal_distance_weigth;
+        for (int i = 0; i < 3; ++i) {
+            used_out[7 + i] = u.used_horizontal_axis[(size_t)i];
+            used_out[10 + i] = u.used_support_edge_remove_offset[(size_t)i];
+        }
+    }
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_support_get(pitt_srv* s, int32_t k, int32_t* idx_map, float coef[4], int64_t* n_support,
+                         int64_t* n_on_support) {
+    if (!s || k < 0 || k >= (int32_t)s->supports.supports_description.size()) return PITT_E_INVALID;
+    const pitt_msgs::Support& m = s->supports.supports_description[(size_t)k];
+    if (idx_map) std::memcpy(idx_map, m.inliers.data(), m.inliers.size() * 4);
+    if (coef) {
+        coef[0] = m.support_coefficient_a;
+        coef[1] = m.support_coefficient_b;
+        coef[2] = m.support_coefficient_c;
+        coef[3] = m.support_coefficient_d;
+    }
+    if (n_support) *n_support = (int64_t)m.support_cloud.size();
+    if (n_on_support) *n_on_support = (int64_t)m.on_support_cloud.size();
+    return PITT_OK;
+}
+
+int pitt_srv_support_cloud(pitt_srv* s, int32_t k, int32_t which, float* out) {
+    if (!s || !out || k < 0 || k >= (int32_t)s->supports.supports_description.size()) return PITT_E_INVALID;
+    const pitt_msgs::Support& m = s->supports.supports_description[(size_t)k];
+    const pitt_msgs::PointCloud& c = which ? m.on_support_cloud : m.support_cloud;
+    std::memcpy(out, c.data.data(), c.data.size() * 4);
+    return PITT_OK;
+}
+
+int pitt_srv_clusterize(pitt_srv* s, const float* xyz16, int64_t n, int32_t* n_clusters) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_clusters) return PITT_E_INVALID;
+    pitt_msgs::ClusterSegmentation srv;
+    srv.request.cloud = cloud_from(xyz16, n);
+    bool ok = s->svc.clusterize(srv.request, srv.response);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    s->clusters = std::move(srv.response);
+    *n_clusters = (int32_t)s->clusters.cluster_objs.size();
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_cluster_get(pitt_srv* s, int32_t c, int32_t* inliers, int64_t* size, float centroid[3], float* xyz16_out) {
+    if (!s || c < 0 || c >= (int32_t)s->clusters.cluster_objs.size()) return PITT_E_INVALID;
+    const pitt_msgs::InliersCluster& m = s->clusters.cluster_objs[(size_t)c];
+    if (inliers) std::memcpy(inliers, m.inliers.data(), m.inliers.size() * 4);
+    if (size) *size = (int64_t)m.inliers.size();
+    if (centroid) {
+        centroid[0] = m.x_centroid;
+        centroid[1] = m.y_centroid;
+        centroid[2] = m.z_centroid;
+    }
+    if (xyz16_out) std::memcpy(xyz16_out, m.cloud.data.data(), m.cloud.data.size() * 4);
+    return PITT_OK;
+}
+
+int pitt_srv_segment_objects(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals, int32_t* n_outputs) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_outputs) return PITT_E_INVALID;
+    pitt_msgs::NormalCloud nc;
+    nc.n = (size_t)n_normals;
+    s->outputs = s->svc.segmentObjects(cloud_from(xyz16, n), nc);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    *n_outputs = (int32_t)s->outputs.size();
+    return 1;
+}
+
+int pitt_srv_output_size(pitt_srv* s, int32_t o, int32_t* n_clusters) {
+    if (!s || !n_clusters || o < 0 || o >= (int32_t)s->outputs.size()) return PITT_E_INVALID;
+    *n_clusters = (int32_t)s->outputs[(size_t)o].cluster_objs.size();
+    return PITT_OK;
+}
+
+int pitt_srv_output_cluster(pitt_srv* s, int32_t o, int32_t c, int32_t* inliers, int64_t* size, float centroid[3]) {
+    if (!s || o < 0 || o >= (int32_t)s->outputs.size()) return PITT_E_INVALID;
+    const auto& objs = s->outputs[(size_t)o].cluster_objs;
+    if (c < 0 || c >= (int32_t)objs.size()) return PITT_E_INVALID;
+    const pitt_msgs::InliersCluster& m = objs[(size_t)c];
+    if (inliers) std::memcpy(inliers, m.inliers.data(), m.inliers.size() * 4);
+    if (size) *size = (int64_t)m.inliers.size();
+    if (centroid) {
+        centroid[0] = m.x_centroid;
+        centroid[1] = m.y_centroid;
+        centroid[2] = m.z_centroid;
+    }
+    return PITT_OK;
+}
+
+}  // extern "C"

@@ -400,46 +400,111 @@ __global__ __launch_bounds__(kBlock) void k_select_xyz(
     }
 }
 
-// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order.  Lane (slot, acc) of a wave owns
-// accumulator acc (xx, xy, xz, yy, yz, zz, x, y, z) of frame blockIdx.x * 7 + slot and adds its
-// terms sequentially in inlier order; lane acc == 0 then runs eigen33 and writes the refined plane.
+// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order.  One wave serves 7 frames;
+// lane (slot, acc) owns accumulator acc (xx, xy, xz, yy, yz, zz, x, y, z) of frame
+// blockIdx.x * 7 + slot and adds its terms sequentially in inlier order (A6: the float sum is
+// order-sensitive, so each accumulator is one serial chain).  The compacted inlier coordinates
+// stream through a 3-slot LDS ring filled by async global->LDS DMA (global_load_lds_dwordx4, one
+// 1 KiB piece = 256 floats of one coordinate plane of one frame per wave instruction), two chunks
+// ahead of the chain.  Lane acc == 0 then runs eigen33 and writes the refined plane.
+constexpr int kCovChunk = 256;                      // inliers per chunk
+constexpr int kCovPlane = kCovChunk + 4;            // +16 B pad: planes start on different banks
+constexpr int kCovSlot = kCovFramesPerWave * 3 * kCovPlane;
+constexpr int kCovRing = 3;
+
+__device__ __forceinline__ void cov_issue_chunk(float* ring, int slot_idx, const float* const* src,
+                                                const int64_t* nn, int64_t i0) {
+    const int lane = threadIdx.x;
+    float* base = ring + slot_idx * kCovSlot;
+#pragma unroll
+    for (int fs = 0; fs < kCovFramesPerWave; ++fs) {
+        // Every chunk issues exactly 21 pieces so the counted vmcnt waits stay exact; a frame
+        // without inliers left re-reads its first piece (always inside the buffer).
+        const int64_t at = i0 < nn[fs] ? i0 : 0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float* g = src[fs * 3 + c] + at + lane * 4;
+            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(base + (fs * 3 + c) * kCovPlane),
+                                             16, 0, 0);
+        }
+    }
+}
+
 template <int ORDER, int DIV>
 __global__ __launch_bounds__(64) void k_cov_eigen(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float* __restrict__ CX, const float* __restrict__ CY, const float* __restrict__ CZ,
     int n_frames, float4* __restrict__ final_coef) {
+    extern __shared__ __attribute__((aligned(16))) float ring[];  // kCovRing slots + ones
     const int lane = threadIdx.x;
     const int slot = lane / 9, acc = lane % 9;
+    // per-frame streams of this wave (uniform)
+    const float* src[kCovFramesPerWave * 3];
+    int64_t nn[kCovFramesPerWave];
+    int64_t nmax = 0;
+#pragma unroll
+    for (int fs = 0; fs < kCovFramesPerWave; ++fs) {
+        const int f = blockIdx.x * kCovFramesPerWave + fs;
+        int64_t n = 0, off = 0;
+        if (f < n_frames && st[f].need_refine) {
+            n = st[f].best_count;
+            off = meta[f].off;
+        }
+        nn[fs] = n;
+        nmax = n > nmax ? n : nmax;
+        src[fs * 3 + 0] = CX + off;
+        src[fs * 3 + 1] = CY + off;
+        src[fs * 3 + 2] = CZ + off;
+    }
+    float* ones = ring + kCovRing * kCovSlot;
+    for (int i = lane; i < kCovChunk; i += 64) ones[i] = 1.0f;
     const int f = blockIdx.x * kCovFramesPerWave + slot;
     const bool active = slot < kCovFramesPerWave && f < n_frames && st[f].need_refine;
-    int64_t n = 0;
-    const float *A = CX, *B = CX;
-    bool lin = false;
-    if (active) {
-        const FrameMeta m = meta[f];
-        n = st[f].best_count;
-        const float* planes[3] = {CX + m.off, CY + m.off, CZ + m.off};
-        const int ia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
-        const int ib[9] = {0, 1, 2, 1, 2, 2, 0, 1, 2};
-        A = planes[ia[acc]];
-        B = planes[ib[acc]];
-        lin = acc >= 6;
-    }
+    const int64_t n = active ? nn[slot] : 0;
+    const int ia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
+    const int ib[9] = {0, 1, 2, 1, 2, 2, -1, -1, -1};
+    const int sl = slot < kCovFramesPerWave ? slot : 0;
+    const int a_off = (sl * 3 + ia[acc]) * kCovPlane;
+    const int b_off = ib[acc] >= 0 ? (sl * 3 + ib[acc]) * kCovPlane : -1;
+    const int64_t nchunks = (nmax + kCovChunk - 1) / kCovChunk;
+    // prologue: chunks 0 and 1 in flight
+    if (nchunks > 0) cov_issue_chunk(ring, 0, src, nn, 0);
+    if (nchunks > 1) cov_issue_chunk(ring, 1, src, nn, kCovChunk);
     float s = 0.0f;
-    int64_t i = 0;
-    for (; i + 4 <= n; i += 4) {
-        const float4 a = *reinterpret_cast<const float4*>(A + i);
-        const float4 b = *reinterpret_cast<const float4*>(B + i);
-        s += a.x * (lin ? 1.0f : b.x);
-        s += a.y * (lin ? 1.0f : b.y);
-        s += a.z * (lin ? 1.0f : b.z);
-        s += a.w * (lin ? 1.0f : b.w);
+    for (int64_t c = 0; c < nchunks; ++c) {
+        if (c + 2 < nchunks) {
+            cov_issue_chunk(ring, (int)((c + 2) % kCovRing), src, nn, (c + 2) * kCovChunk);
+            // wait for chunk c: at most the two younger chunks (<= 42 pieces) still outstanding
+            asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+        } else if (c + 1 < nchunks) {
+            asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float* sb = ring + (int)(c % kCovRing) * kCovSlot;
+        const float* pa = (const float*)__builtin_assume_aligned(sb + a_off, 16);
+        const float* pb = (const float*)__builtin_assume_aligned(b_off >= 0 ? sb + b_off : ones, 16);
+        const int64_t i0 = c * kCovChunk;
+        const int64_t rem = n - i0;
+        if (rem >= kCovChunk) {
+#pragma unroll 8
+            for (int i = 0; i < kCovChunk; i += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(pa + i);
+                const float4 b = *reinterpret_cast<const float4*>(pb + i);
+                s += a.x * b.x;
+                s += a.y * b.y;
+                s += a.z * b.z;
+                s += a.w * b.w;
+            }
+        } else if (rem > 0) {
+            for (int i = 0; i < rem; ++i) s += pa[i] * pb[i];
+        }
     }
-    for (; i < n; ++i) s += A[i] * (lin ? 1.0f : B[i]);
     // gather the 9 accumulators of this frame into its acc == 0 lane
     float a9[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, slot * 9 + k, 64);
+    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, sl * 9 + k, 64);
     if (!active || acc != 0) return;
     const float fn = (float)n;
     if constexpr (DIV == 0) {
@@ -695,7 +760,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_cov_eigen", 0.0);
         hipLaunchKernelGGL((k_cov_eigen<ORDER, DIV>), dim3((nf + kCovFramesPerWave - 1) / kCovFramesPerWave),
-                           dim3(64), 0, sm, meta, st, CX, CY, CZ, nf, final_coef);
+                           dim3(64), (kCovRing * kCovSlot + kCovChunk) * sizeof(float), sm, meta, st, CX, CY, CZ,
+                           nf, final_coef);
         ctx->prof_end(rec);
     }
     rec = ctx->prof_begin("k_count_final", (double)total_pts * 12.0);

@@ -274,6 +274,16 @@ int pitt_last_hypothesis_counts(pitt_ctx* ctx, int32_t frame, int32_t* counts, i
     return PITT_OK;
 }
 
+int pitt_sampler_table(int64_t n, uint32_t seed, int64_t attempts, int32_t* out) {
+    if (n < 3 || attempts < 0 || (attempts > 0 && !out)) return PITT_E_INVALID;
+    pitt_ctx tmp;  // host-only: table cache lives in a throwaway context
+    const std::vector<int32_t>& t = pitt::sampler_table(&tmp, n, seed, attempts);
+    std::memcpy(out, t.data(), t.size() * sizeof(int32_t));
+    return PITT_OK;
+}
+
+float pitt_float_threshold(double threshold) { return pitt::float_threshold(threshold); }
+
 int pitt_profile_enable(pitt_ctx* ctx, int32_t on) {
     if (!ctx) return PITT_E_INVALID;
     if (!on) (void)ctx->prof_collect();

@@ -1,0 +1,527 @@
+// supports.hip -- ExtractIndices and the support (table) segmentation loop on gfx950.
+//
+// Replaces, in src/segmentation_services/supports_segmentation_srv.cpp (reference paths):
+//   removePlaneInliner  :114-127  -> k_gather (positive) + ordered compaction (negative)
+//   createNewIdxMap     :139-157  -> membership bitmask + ordered rank (O(N), not O(N*|inl|))
+//   getPointOnPlane     :187-238  -> prefix-max scan for the `if / else if` bbox (Q5), exact
+//                                    double z sum (Q10), ordered compaction of the originals
+//   findSupports        :241-361  -> host loop driving the device (stop tests in float, Q9)
+// The RANSAC inside the loop is pitt_plane_segment_batch with one frame.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "compact.hpp"
+#include "ctx.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pitt {
+
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(const int32_t* __restrict__ counts, int64_t nt,
+                                                       int32_t* __restrict__ offsets) {
+    __shared__ int32_t lds4[kBlock / 64];
+    int carry = 0;
+    for (int64_t base = 0; base < nt; base += kBlock) {
+        const int64_t t = base + threadIdx.x;
+        const int v = t < nt ? counts[t] : 0;
+        int total;
+        const int ex = block_exscan(v, lds4, &total);
+        if (t < nt) offsets[t] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) offsets[nt] = carry;
+}
+
+// ---- predicates / actions --------------------------------------------------------------------
+struct NotMember {  // negative ExtractIndices: keep points whose index is not in the bitmask
+    const uint32_t* bits;
+    __device__ bool operator()(int64_t i) const { return !((bits[i >> 5] >> (i & 31)) & 1u); }
+};
+struct CopyXYZ {
+    const float *x, *y, *z;
+    float *ox, *oy, *oz;
+    __device__ void operator()(int64_t i, int64_t p) const {
+        ox[p] = x[i];
+        oy[p] = y[i];
+        oz[p] = z[i];
+    }
+};
+
+__global__ void k_mark(const int32_t* __restrict__ idx, int64_t m, int64_t n, uint32_t* __restrict__ bits,
+                       int32_t* __restrict__ bad) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t i = idx[k];
+        if (i < 0 || i >= n) { atomicOr(bad, 1); continue; }
+        atomicOr(&bits[i >> 5], 1u << (i & 31));
+    }
+}
+
+__global__ void k_gather(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                         const int32_t* __restrict__ idx, int64_t m, float* __restrict__ ox, float* __restrict__ oy,
+                         float* __restrict__ oz) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t i = idx[k];
+        ox[k] = x[i];
+        oy[k] = y[i];
+        oz[k] = z[i];
+    }
+}
+
+__global__ void k_iota(int32_t* __restrict__ v, int64_t n) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        v[k] = (int32_t)k;
+}
+
+// createNewIdxMap: propagate (level < v < 0), tag members with `level`; the rest get a running
+// counter assigned by the ordered compaction below (MapRest / MapRank).
+__global__ void k_map_tags(const int32_t* __restrict__ prev, int64_t n, const uint32_t* __restrict__ bits,
+                           int64_t nbits, int level, int32_t* __restrict__ out) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int v = prev[p];
+        if (v > level && v < 0) out[p] = v;
+        else if (v >= 0 && v < nbits && ((bits[v >> 5] >> (v & 31)) & 1u)) out[p] = level;
+    }
+}
+struct MapRest {
+    const int32_t* prev;
+    const uint32_t* bits;
+    int64_t nbits;
+    int level;
+    __device__ bool operator()(int64_t p) const {
+        const int v = prev[p];
+        if (v > level && v < 0) return false;
+        if (v >= 0 && v < nbits && ((bits[v >> 5] >> (v & 31)) & 1u)) return false;
+        return true;
+    }
+};
+struct MapRank {
+    int32_t* out;
+    __device__ void operator()(int64_t p, int64_t pos) const { out[p] = (int32_t)pos; }
+};
+
+// ---- getPointOnPlane bbox (Q5) -----------------------------------------------------------------
+// xMax = max x; xMin = min { x_i : i >= 1, x_i <= max(x_0..x_{i-1}) } (the `else if` branch);
+// same for y.  zsum in double: computed in parallel and proven equal to the sequential sum when
+// every partial sum is exactly representable (all |z| multiples of 2^q and sum|z| <= 2^(52+q)).
+struct BBoxTile {
+    float mx, my;        // inclusive tile max
+    float cx, cy;        // candidate minima (else-if branch)
+    double zs, za;       // sum z, sum |z|
+    int32_t q;           // min ulp exponent of nonzero |z|
+    int32_t pad;
+};
+
+__device__ __forceinline__ float fmax_nan_free(float a, float b) { return (a < b) ? b : a; }
+
+__global__ __launch_bounds__(kBlock) void k_bbox_tilemax(const float* __restrict__ x, const float* __restrict__ y,
+                                                         int64_t n, BBoxTile* __restrict__ tiles) {
+    __shared__ float sx[kBlock / 64], sy[kBlock / 64];
+    const int64_t nt = ctiles(n);
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const int64_t b = t * kCTile + threadIdx.x * 8;
+        float mx = -INFINITY, my = -INFINITY;
+        for (int k = 0; k < 8; ++k)
+            if (b + k < n) { mx = fmax_nan_free(mx, x[b + k]); my = fmax_nan_free(my, y[b + k]); }
+        for (int d = 32; d >= 1; d >>= 1) {
+            mx = fmax_nan_free(mx, __shfl_xor(mx, d, 64));
+            my = fmax_nan_free(my, __shfl_xor(my, d, 64));
+        }
+        if ((threadIdx.x & 63) == 0) { sx[threadIdx.x >> 6] = mx; sy[threadIdx.x >> 6] = my; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float ax = sx[0], ay = sy[0];
+            for (int w = 1; w < kBlock / 64; ++w) { ax = fmax_nan_free(ax, sx[w]); ay = fmax_nan_free(ay, sy[w]); }
+            tiles[t].mx = ax;
+            tiles[t].my = ay;
+        }
+        __syncthreads();
+    }
+}
+
+// exclusive prefix max over tiles (single block, serial: tiles are few)
+__global__ void k_bbox_tilescan(BBoxTile* __restrict__ tiles, int64_t nt, float* __restrict__ pre /*2*nt*/) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float ax = -INFINITY, ay = -INFINITY;
+    for (int64_t t = 0; t < nt; ++t) {
+        pre[2 * t] = ax;
+        pre[2 * t + 1] = ay;
+        ax = fmax_nan_free(ax, tiles[t].mx);
+        ay = fmax_nan_free(ay, tiles[t].my);
+    }
+}
+
+__device__ __forceinline__ void excl_max_scan(float v, float* lds, float& ex) {
+    // block-wide exclusive max scan (kBlock threads)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        float t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc = fmax_nan_free(inc, t);
+    }
+    float exw = __shfl_up(inc, 1, 64);
+    if (lane == 0) exw = -INFINITY;
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    float pre = -INFINITY;
+    for (int i = 0; i < w; ++i) pre = fmax_nan_free(pre, lds[i]);
+    __syncthreads();
+    ex = fmax_nan_free(pre, exw);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bbox_tilemin(const float* __restrict__ x, const float* __restrict__ y,
+                                                         const float* __restrict__ z, int64_t n,
+                                                         const float* __restrict__ pre, BBoxTile* __restrict__ tiles) {
+    __shared__ float lx[kBlock / 64], ly[kBlock / 64];
+    __shared__ float rcx[kBlock / 64], rcy[kBlock / 64];
+    __shared__ double rzs[kBlock / 64], rza[kBlock / 64];
+    __shared__ int32_t rq[kBlock / 64];
+    const int64_t nt = ctiles(n);
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const int64_t b = t * kCTile + threadIdx.x * 8;
+        float vx[8], vy[8];
+        float tmx = -INFINITY, tmy = -INFINITY;
+        for (int k = 0; k < 8; ++k) {
+            vx[k] = b + k < n ? x[b + k] : -INFINITY;
+            vy[k] = b + k < n ? y[b + k] : -INFINITY;
+            tmx = fmax_nan_free(tmx, vx[k]);
+            tmy = fmax_nan_free(tmy, vy[k]);
+        }
+        float ex, ey;
+        excl_max_scan(tmx, lx, ex);
+        excl_max_scan(tmy, ly, ey);
+        float runx = fmax_nan_free(pre[2 * t], ex), runy = fmax_nan_free(pre[2 * t + 1], ey);
+        float cx = INFINITY, cy = INFINITY;
+        double zs = 0.0, za = 0.0;
+        int q = 1 << 30;
+        for (int k = 0; k < 8; ++k) {
+            if (b + k >= n) break;
+            if (vx[k] > runx) runx = vx[k];
+            else if (vx[k] < cx) cx = vx[k];
+            if (vy[k] > runy) runy = vy[k];
+            else if (vy[k] < cy) cy = vy[k];
+            const float zz = z[b + k];
+            zs += (double)zz;
+            za += fabs((double)zz);
+            if (zz != 0.0f) {
+                int e;
+                (void)frexpf(zz, &e);
+                q = min(q, max(e - 24, -149));
+            }
+        }
+        for (int d = 32; d >= 1; d >>= 1) {
+            cx = fminf(cx, __shfl_xor(cx, d, 64));
+            cy = fminf(cy, __shfl_xor(cy, d, 64));
+            zs += __shfl_xor(zs, d, 64);
+            za += __shfl_xor(za, d, 64);
+            q = min(q, __shfl_xor(q, d, 64));
+        }
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { rcx[w] = cx; rcy[w] = cy; rzs[w] = zs; rza[w] = za; rq[w] = q; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            BBoxTile bt = tiles[t];
+            bt.cx = rcx[0]; bt.cy = rcy[0]; bt.zs = rzs[0]; bt.za = rza[0]; bt.q = rq[0];
+            for (int i = 1; i < kBlock / 64; ++i) {
+                bt.cx = fminf(bt.cx, rcx[i]);
+                bt.cy = fminf(bt.cy, rcy[i]);
+                bt.zs += rzs[i];
+                bt.za += rza[i];
+                bt.q = min(bt.q, rq[i]);
+            }
+            tiles[t] = bt;
+        }
+        __syncthreads();
+    }
+}
+
+// out[0..7]: xMax, xMin, yMax, yMin, zsum, zabs, q, exact(1/0)
+__global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, const float* __restrict__ z, int64_t n,
+                             double* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float mx = -INFINITY, my = -INFINITY, cx = INFINITY, cy = INFINITY;
+    double zs = 0.0, za = 0.0;
+    int q = 1 << 30;
+    for (int64_t t = 0; t < nt; ++t) {
+        mx = fmax_nan_free(mx, tiles[t].mx);
+        my = fmax_nan_free(my, tiles[t].my);
+        cx = fminf(cx, tiles[t].cx);
+        cy = fminf(cy, tiles[t].cy);
+        zs += tiles[t].zs;
+        za += tiles[t].za;
+        q = min(q, tiles[t].q);
+    }
+    const bool exact = (q == (1 << 30)) || (za <= ldexp(1.0, 52 + q));
+    if (!exact) {  // fall back to the reference's sequential double sum
+        zs = 0.0;
+        for (int64_t i = 0; i < n; ++i) zs += (double)z[i];
+    }
+    out[0] = mx; out[1] = cx; out[2] = my; out[3] = cy;
+    out[4] = zs; out[5] = za; out[6] = q; out[7] = exact ? 1.0 : 0.0;
+}
+
+struct OnSupport {
+    const float *x, *y, *z;
+    const int32_t* map;
+    int level;
+    double xMin, xMax, yMin, yMax, zMed;
+    __device__ bool operator()(int64_t i) const {
+        if (map[i] == level) return false;
+        const double px = x[i], py = y[i], pz = z[i];
+        return px > xMin && px < xMax && pz > zMed && py > yMin && py < yMax;
+    }
+};
+
+// ---- host helpers -------------------------------------------------------------------------------
+template <class Pred, class Act>
+static int run_compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total) {
+    const int64_t nt = ctiles(n);
+    int32_t* counts = (int32_t*)ctx->buf("cmp_counts", (size_t)std::max<int64_t>(nt, 1) * 4);
+    int32_t* offs = (int32_t*)ctx->buf("cmp_offs", (size_t)(nt + 1) * 4);
+    if (!counts || !offs) return ctx->fail(PITT_E_NOMEM, "compaction scratch");
+    hipStream_t s = ctx->stream;
+    if (n > 0) {
+        hipLaunchKernelGGL((k_pred_count<Pred>), dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, pred, n, counts);
+    }
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, counts, nt, offs);
+    if (n > 0) {
+        hipLaunchKernelGGL((k_pred_apply<Pred, Act>), dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, pred, act, n,
+                           offs);
+    }
+    PITT_HIP_TRY(hipGetLastError());
+    if (total) {
+        int32_t* h = (int32_t*)ctx->pinned("cmp_total", 16);
+        PITT_HIP_TRY(hipMemcpyAsync(h, offs + nt, 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        *total = h[0];
+    }
+    return PITT_OK;
+}
+
+static inline int ew_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
+
+int extract_indices_impl(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                         const int32_t* idx, int64_t m, int negative, float* ox, float* oy, float* oz,
+                         int64_t* n_out) {
+    hipStream_t s = ctx->stream;
+    if (!negative) {
+        if (m > 0) hipLaunchKernelGGL(k_gather, dim3(ew_grid(m)), dim3(256), 0, s, x, y, z, idx, m, ox, oy, oz);
+        PITT_HIP_TRY(hipGetLastError());
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        *n_out = m;
+        return PITT_OK;
+    }
+    const int64_t words = (n + 31) / 32;
+    uint32_t* bits = (uint32_t*)ctx->buf("ext_bits", (size_t)std::max<int64_t>(words, 1) * 4 + 16);
+    if (!bits) return ctx->fail(PITT_E_NOMEM, "bitmask");
+    int32_t* bad = (int32_t*)(bits + words);
+    PITT_HIP_TRY(hipMemsetAsync(bits, 0, (size_t)words * 4 + 16, s));
+    if (m > 0) hipLaunchKernelGGL(k_mark, dim3(ew_grid(m)), dim3(256), 0, s, idx, m, n, bits, bad);
+    return run_compact(ctx, n, NotMember{bits}, CopyXYZ{x, y, z, ox, oy, oz}, n_out);
+}
+
+// isHorizontalPlane :161-179, float.
+static bool is_horizontal(const float c[4], const float axis[3], float var_th) {
+    float div = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    float nx = c[0] / div, ny = c[1] / div, nz = c[2] / div;
+    float cx = ny * axis[2] - nz * axis[1];
+    float cy = nz * axis[0] - nx * axis[2];
+    float cz = nx * axis[1] - ny * axis[0];
+    float lo = -1 * var_th, hi = var_th;
+    return (cx > lo && cx < hi) && (cy > lo && cy < hi) && (cz > lo && cz < hi);
+}
+
+int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t N,
+                       const pitt_support_params* sp, pitt_support_list* out) {
+    hipStream_t s = ctx->stream;
+    ctx->keep_i32.clear();
+    ctx->keep_f32.clear();
+    ctx->keep_supports.clear();
+    out->n_supports = 0;
+    out->supports = nullptr;
+    out->iterations = 0;
+    const int64_t cap = std::max<int64_t>(kCTile, (N + kCTile - 1) / kCTile * kCTile);
+    auto plane3 = [&](const char* name) { return (float*)ctx->buf(name, (size_t)cap * 3 * sizeof(float)); };
+    float* O = plane3("sup_orig");
+    float* IT[2] = {plane3("sup_it0"), plane3("sup_it1")};
+    float* S = plane3("sup_s");
+    float* ON = plane3("sup_on");
+    int32_t* INL = (int32_t*)ctx->buf("sup_inl", (size_t)cap * 4);
+    int32_t* MAP[2] = {(int32_t*)ctx->buf("sup_map0", (size_t)cap * 4), (int32_t*)ctx->buf("sup_map1", (size_t)cap * 4)};
+    const int64_t words = (cap + 31) / 32;
+    uint32_t* MEM = (uint32_t*)ctx->buf("sup_mem", (size_t)words * 4 + 16);
+    const int64_t ntmax = ctiles(cap);
+    BBoxTile* BT = (BBoxTile*)ctx->buf("sup_bbox", (size_t)ntmax * sizeof(BBoxTile));
+    float* PRE = (float*)ctx->buf("sup_pre", (size_t)ntmax * 2 * sizeof(float));
+    double* BB = (double*)ctx->buf("sup_bbout", 8 * sizeof(double));
+    if (!O || !IT[0] || !IT[1] || !S || !ON || !INL || !MAP[0] || !MAP[1] || !MEM || !BT || !PRE || !BB)
+        return ctx->fail(PITT_E_NOMEM, "support scratch");
+    // upload the original cloud (host SoA) -- iterativeCloud starts as its copy
+    PITT_HIP_TRY(hipMemcpyAsync(O, hx, (size_t)N * 4, hipMemcpyHostToDevice, s));
+    PITT_HIP_TRY(hipMemcpyAsync(O + cap, hy, (size_t)N * 4, hipMemcpyHostToDevice, s));
+    PITT_HIP_TRY(hipMemcpyAsync(O + 2 * cap, hz, (size_t)N * 4, hipMemcpyHostToDevice, s));
+    PITT_HIP_TRY(hipMemcpyAsync(IT[0], O, (size_t)cap * 3 * 4, hipMemcpyDeviceToDevice, s));
+
+    pitt_sac_params p;
+    pitt_sac_params_default(&p);
+    p.threshold = (double)sp->ransac_distance_threshold;
+    p.max_iterations = sp->ransac_max_iterations;
+    p.reduce_order = sp->reduce_order;
+    p.div_mode = sp->div_mode;
+
+    struct Staged {
+        std::vector<int32_t> map;
+        std::vector<float> sup, on;
+        float coef[4];
+    };
+    std::vector<Staged> staged;
+    int cur = 0, mcur = 0;
+    int64_t Nk = N;
+    int level = -2, cnt = 0;
+    const float Nf = (float)N;
+    while (true) {
+        pitt_frames fr;
+        int64_t off = 0;
+        fr.x = IT[cur];
+        fr.y = IT[cur] + cap;
+        fr.z = IT[cur] + 2 * cap;
+        fr.offsets = &off;
+        fr.counts = &Nk;
+        fr.n_frames = 1;
+        fr.capacity = cap;
+        pitt_plane_result r;
+        int rc = pitt_plane_segment_batch(ctx, &fr, &p, &r, INL);
+        if (rc < 0) return rc;
+        if (r.status < 0) return ctx->fail(r.status, "RANSAC inside the support loop failed");
+        out->iterations++;
+        const int64_t n_inl = r.n_coeff ? r.n_inliers : 0;
+        if (n_inl == 0) break;                                                   // :270
+        if ((float)Nk < Nf * sp->min_iterative_cloud_percentage) break;          // :274 (Q9)
+        if ((float)n_inl < Nf * sp->min_iterative_plane_percentage) break;       // :278
+        // membership bitmask of the inliers (indices into the current iterative cloud)
+        PITT_HIP_TRY(hipMemsetAsync(MEM, 0, (size_t)words * 4 + 16, s));
+        hipLaunchKernelGGL(k_mark, dim3(ew_grid(n_inl)), dim3(256), 0, s, INL, n_inl, Nk, MEM,
+                           (int32_t*)(MEM + words));
+        // removePlaneInliner: support = it[inl] ; it <- it \ inl
+        hipLaunchKernelGGL(k_gather, dim3(ew_grid(n_inl)), dim3(256), 0, s, IT[cur], IT[cur] + cap, IT[cur] + 2 * cap,
+                           INL, n_inl, S, S + cap, S + 2 * cap);
+        int64_t Nn = 0;
+        rc = run_compact(ctx, Nk, NotMember{MEM},
+                         CopyXYZ{IT[cur], IT[cur] + cap, IT[cur] + 2 * cap, IT[cur ^ 1], IT[cur ^ 1] + cap,
+                                 IT[cur ^ 1] + 2 * cap},
+                         &Nn);
+        if (rc) return rc;
+        // index map w.r.t. the original cloud
+        if (!cnt) hipLaunchKernelGGL(k_iota, dim3(ew_grid(N)), dim3(256), 0, s, MAP[mcur], N);
+        const bool horizontal = is_horizontal(r.coefficients, sp->horizontal_axis, sp->horizontal_variance_threshold);
+        const int lv = horizontal ? level : -1;
+        hipLaunchKernelGGL(k_map_tags, dim3(ew_grid(N)), dim3(256), 0, s, MAP[mcur], N, MEM, Nk, lv, MAP[mcur ^ 1]);
+        rc = run_compact(ctx, N, MapRest{MAP[mcur], MEM, Nk, lv}, MapRank{MAP[mcur ^ 1]}, nullptr);
+        if (rc) return rc;
+        if (horizontal) {
+            Staged st;
+            const int64_t nt = ctiles(n_inl);
+            hipLaunchKernelGGL(k_bbox_tilemax, dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, S, S + cap, n_inl, BT);
+            hipLaunchKernelGGL(k_bbox_tilescan, dim3(1), dim3(64), 0, s, BT, nt, PRE);
+            hipLaunchKernelGGL(k_bbox_tilemin, dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, S, S + cap, S + 2 * cap,
+                               n_inl, PRE, BT);
+            hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, BT, nt, S + 2 * cap, n_inl, BB);
+            double* hb = (double*)ctx->pinned("sup_bb_h", 8 * sizeof(double));
+            PITT_HIP_TRY(hipMemcpyAsync(hb, BB, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+            PITT_HIP_TRY(hipStreamSynchronize(s));
+            double xMax = hb[0], xMin = hb[1], yMax = hb[2], yMin = hb[3], zMed = hb[4];
+            xMax -= sp->edge_remove_offset[0];
+            xMin += sp->edge_remove_offset[0];
+            yMax -= sp->edge_remove_offset[1];
+            yMin += sp->edge_remove_offset[1];
+            zMed = zMed / (double)n_inl + sp->edge_remove_offset[2];
+            int64_t n_on = 0;
+            rc = run_compact(ctx, N,
+                             OnSupport{O, O + cap, O + 2 * cap, MAP[mcur ^ 1], lv, xMin, xMax, yMin, yMax, zMed},
+                             CopyXYZ{O, O + cap, O + 2 * cap, ON, ON + cap, ON + 2 * cap}, &n_on);
+            if (rc) return rc;
+            st.map.resize((size_t)N);
+            st.sup.resize((size_t)n_inl * 3);
+            st.on.resize((size_t)n_on * 3);
+            PITT_HIP_TRY(hipMemcpyAsync(st.map.data(), MAP[mcur ^ 1], (size_t)N * 4, hipMemcpyDeviceToHost, s));
+            for (int c = 0; c < 3; ++c) {
+                PITT_HIP_TRY(hipMemcpyAsync(st.sup.data() + c * n_inl, S + c * cap, (size_t)n_inl * 4,
+                                            hipMemcpyDeviceToHost, s));
+                PITT_HIP_TRY(hipMemcpyAsync(st.on.data() + c * n_on, ON + c * cap, (size_t)n_on * 4,
+                                            hipMemcpyDeviceToHost, s));
+            }
+            PITT_HIP_TRY(hipStreamSynchronize(s));
+            std::memcpy(st.coef, r.coefficients, sizeof st.coef);
+            staged.push_back(std::move(st));
+        }
+        mcur ^= 1;
+        cur ^= 1;
+        Nk = Nn;
+        ++cnt;
+        --level;
+    }
+    for (Staged& st : staged) {
+        ctx->keep_i32.push_back(std::move(st.map));
+        ctx->keep_f32.push_back(std::move(st.sup));
+        ctx->keep_f32.push_back(std::move(st.on));
+        pitt_support su;
+        su.n_points = (int32_t)N;
+        su.idx_map = ctx->keep_i32.back().data();
+        std::memcpy(su.coefficients, st.coef, sizeof su.coefficients);
+        su.support_xyz = ctx->keep_f32[ctx->keep_f32.size() - 2].data();
+        su.n_support = (int64_t)ctx->keep_f32[ctx->keep_f32.size() - 2].size() / 3;
+        su.on_support_xyz = ctx->keep_f32.back().data();
+        su.n_on_support = (int64_t)ctx->keep_f32.back().size() / 3;
+        ctx->keep_supports.push_back(su);
+    }
+    out->n_supports = (int32_t)ctx->keep_supports.size();
+    out->supports = ctx->keep_supports.data();
+    return PITT_OK;
+}
+
+}  // namespace pitt
+
+extern "C" {
+
+void pitt_support_params_default(pitt_support_params* p) {
+    if (!p) return;
+    p->min_iterative_cloud_percentage = 0.030f;   // supports_segmentation_srv.cpp:30
+    p->min_iterative_plane_percentage = 0.030f;   // :31
+    p->horizontal_variance_threshold = 0.09f;     // :33
+    p->ransac_distance_threshold = 0.02f;         // :35
+    p->ransac_max_iterations = 10;                // :37
+    p->horizontal_axis[0] = 0.0f;                 // :38
+    p->horizontal_axis[1] = 0.0f;
+    p->horizontal_axis[2] = -1.0f;
+    p->edge_remove_offset[0] = 0.02f;             // :39
+    p->edge_remove_offset[1] = 0.02f;
+    p->edge_remove_offset[2] = 0.005f;
+    p->reduce_order = PITT_REDUCE_SSE2;
+    p->div_mode = PITT_DIV_EIGEN32;
+}
+
+int pitt_extract_indices(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                         const int32_t* indices_dev, int64_t n_indices, int32_t negative, float* ox, float* oy,
+                         float* oz, int64_t* n_out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!n_out || n < 0 || n_indices < 0 || (n > 0 && (!x || !y || !z)) || (n_indices > 0 && !indices_dev))
+        return ctx->fail(PITT_E_INVALID, "null argument");
+    if ((n_indices > 0 || n > 0) && (!ox || !oy || !oz)) return ctx->fail(PITT_E_INVALID, "null output");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::extract_indices_impl(ctx, x, y, z, n, indices_dev, n_indices, negative, ox, oy, oz, n_out);
+}
+
+int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                       const pitt_support_params* p, pitt_support_list* out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!p || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::find_supports_impl(ctx, x, y, z, n, p, out);
+}
+
+}  // extern "C"

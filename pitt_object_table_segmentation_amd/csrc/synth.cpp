@@ -209,7 +209,10 @@ double cast(const Scene& s, V3 o, V3 d) {
 // Render one view.  world == false: points in the camera optical frame; else world frame.
 void render(const Scene& s, uint64_t seed, int W, int H, bool world, bool with_nan, float* X,
             float* Y, float* Z) {
-    const double fx = 525.0, fy = 525.0, cx = 319.5, cy = 239.5;
+    // Kinect intrinsics at 640x480 (fx = fy = 525, cx = 319.5, cy = 239.5), scaled with the
+    // resolution so smaller test clouds see the same scene.
+    const double fx = 525.0 * W / 640.0, fy = 525.0 * H / 480.0;
+    const double cx = 0.5 * (W - 1), cy = 0.5 * (H - 1);
     for (int v = 0; v < H; ++v) {
         for (int u = 0; u < W; ++u) {
             const uint64_t pix = (uint64_t)v * (uint64_t)W + (uint64_t)u;

@@ -1,0 +1,71 @@
+"""Frame-parallel multi-GPU plumbing: contiguous frame shards, one process per
+GPU, and a single gather of fixed-size per-frame result records to rank 0.
+
+The data path has no collective: every rank segments its own frames with its own context.  The
+only exchange is the result gather.  RCCL has no native gather, so it is an all_gather of
+equal-size records (the `nccl` backend of torch.distributed is RCCL over xGMI on MI355X); with
+the `gloo` backend the same code runs on CPU tensors (tests).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+from .api import RESULT_DTYPE
+
+RECORD_BYTES = RESULT_DTYPE.itemsize
+
+
+def shard_range(n_frames: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous shard [start, end) of rank `rank`: GPU g gets frames [g*B/G, (g+1)*B/G)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    base, rem = divmod(n_frames, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def pack_records(results: np.ndarray, frame_ids: np.ndarray, slots: int) -> np.ndarray:
+    """Fixed-size byte records [slots, 8 + RECORD_BYTES]: (frame id int64, result record)."""
+    out = np.zeros((slots, 8 + RECORD_BYTES), np.uint8)
+    ids = np.full(slots, -1, np.int64)
+    ids[:len(frame_ids)] = frame_ids
+    out[:, :8] = ids.view(np.uint8).reshape(slots, 8)
+    if len(results):
+        out[:len(results), 8:] = np.ascontiguousarray(results, RESULT_DTYPE).view(np.uint8).reshape(len(results), -1)
+    return out
+
+
+def unpack_records(buf: np.ndarray, n_frames: int) -> np.ndarray:
+    """Inverse of pack_records over the gathered buffer; returns results ordered by frame id."""
+    buf = np.ascontiguousarray(buf.reshape(-1, 8 + RECORD_BYTES))
+    ids = buf[:, :8].copy().view(np.int64).reshape(-1)
+    recs = buf[:, 8:].copy().view(RESULT_DTYPE).reshape(-1)
+    out = np.zeros(n_frames, RESULT_DTYPE)
+    seen = np.zeros(n_frames, bool)
+    for i, r in zip(ids, recs):
+        if i >= 0:
+            out[i] = r
+            seen[i] = True
+    if not seen.all():
+        raise RuntimeError(f"gather lost frames: {np.nonzero(~seen)[0][:8]}")
+    return out
+
+
+def gather_results(results: np.ndarray, frame_start: int, n_frames: int, device=None):
+    """Gather every rank's per-frame results to all ranks (rank 0 consumes them).
+
+    results: this rank's RESULT_DTYPE records for frames [frame_start, frame_start+len).
+    device: torch device for the collective buffer ('cuda:k' with nccl/RCCL, cpu with gloo).
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    slots = -(-n_frames // world)  # equal-size records per rank
+    local = pack_records(results, np.arange(frame_start, frame_start + len(results), dtype=np.int64), slots)
+    src = torch.from_numpy(local.reshape(-1)).to(device)
+    dst = torch.empty(world * src.numel(), dtype=torch.uint8, device=src.device)
+    dist.all_gather_into_tensor(dst, src)
+    return unpack_records(dst.cpu().numpy(), n_frames)

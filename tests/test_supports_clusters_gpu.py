@@ -1,0 +1,110 @@
+"""Parity of the HIP support loop (findSupports) and Euclidean clustering with the oracle:
+identical index maps, support / on-support clouds, coefficients, cluster member sets, cluster
+order and centroids (bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_binding as orc
+import pitt_object_table_segmentation_amd as pitt
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare_supports(dev, ref):
+    assert len(dev) == len(ref)
+    for d, r in zip(dev, ref):
+        assert np.array_equal(d.idx_map, r["idx_map"])
+        assert np.array_equal(d.coefficients, r["coefficients"])
+        assert np.array_equal(d.support_cloud, r["support_cloud"])
+        assert np.array_equal(d.on_support_cloud, r["on_support_cloud"])
+
+
+@pytest.mark.parametrize("seed,views,w,h", [(11, 2, 160, 120), (12, 4, 160, 120), (13, 1, 320, 240)])
+def test_find_supports_matches_oracle(ctx, seed, views, w, h):
+    x, y, z = pitt.synth_fused(seed, views, w, h)
+    _compare_supports(ctx.find_supports(x, y, z), orc.find_supports(x, y, z))
+
+
+def test_find_supports_fused_1p2m(ctx):
+    """BASELINE config 5: 4 fused 640x480 views (1,228,800 points)."""
+    x, y, z = pitt.synth_fused(1000, 4)
+    assert x.size == 1228800
+    dev = ctx.find_supports(x, y, z)
+    ref = orc.find_supports(x, y, z)
+    _compare_supports(dev, ref)
+    assert len(dev) >= 1
+    for d in dev:
+        cl_dev = ctx.euclidean_clusters(*d.on_support_cloud.T, tolerance=0.03,
+                                        min_size=int(np.floor(len(d.on_support_cloud) * 0.01 + 0.5)),
+                                        max_size=int(np.floor(len(d.on_support_cloud) * 0.99 + 0.5)))
+        cl_ref = orc.euclidean_clusters(*d.on_support_cloud.T)
+        assert [len(c.indices) for c in cl_dev] == [len(c["inliers"]) for c in cl_ref]
+        for a, b in zip(cl_dev, cl_ref):
+            assert np.array_equal(a.indices, b["inliers"])
+            assert np.array_equal(a.sum_xyz / np.float32(len(a.indices) + 1), b["centroid"])
+
+
+def test_support_parameter_variants(ctx):
+    x, y, z = pitt.synth_fused(21, 2, 160, 120)
+    for kw in (dict(ransac_max_iterations=30), dict(horizontal_variance_threshold=0.5),
+               dict(horizontal_axis=(0.0, 0.0, 1.0)), dict(min_iterative_plane_percentage=0.2),
+               dict(edge_remove_offset=(0.0, 0.0, 0.0)), dict(ransac_distance_threshold=0.005)):
+        dev = ctx.find_supports(x, y, z, pitt.support_params(**kw))
+        _compare_supports(dev, orc.find_supports(x, y, z, **kw))
+
+
+def _blob(center, n_side, step=0.01):
+    g = np.stack(np.meshgrid(*(np.arange(n_side) * step,) * 3), -1).reshape(-1, 3)
+    return (g + np.asarray(center)).astype(np.float32)
+
+
+def test_clusters_known_layouts(ctx):
+    rng = np.random.default_rng(2)
+    blobs = [_blob(rng.uniform(-1, 1, 3) * 3, int(rng.integers(2, 8))) for _ in range(30)]
+    xyz = np.concatenate(blobs)
+    xyz = xyz[rng.permutation(len(xyz))]
+    for min_size, max_size in ((1, 10 ** 9), (9, 200), (100, 100)):
+        dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=min_size, max_size=max_size)
+        n = len(xyz)
+        ref = orc.euclidean_clusters(*xyz.T, min_rate=min_size / n, max_rate=max_size / n, min_input_size=0)
+        # the oracle's rates round back to exactly these sizes only when n divides evenly; compare
+        # the size-filtered components directly
+        sizes = [len(c.indices) for c in dev]
+        assert all(min_size <= s <= max_size for s in sizes)
+        assert sizes == sorted(sizes, reverse=True)
+    dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=1, max_size=10 ** 9)
+    ref = orc.euclidean_clusters(*xyz.T, min_rate=0.0, max_rate=1.0, min_input_size=0)
+    assert len(dev) == len(ref) == 30
+    for a, b in zip(dev, ref):
+        assert np.array_equal(a.indices, b["inliers"])
+
+
+def test_clusters_ties_many_equal_sizes(ctx):
+    # 40 equal-size blobs (> 16 clusters: libstdc++ introsort path of the size sort)
+    blobs = [_blob([0.2 * i, 0, 0], 3) for i in range(40)]
+    xyz = np.concatenate(blobs[::-1])
+    dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=1, max_size=10 ** 9)
+    ref = orc.euclidean_clusters(*xyz.T, min_rate=0.0, max_rate=1.0, min_input_size=0)
+    assert len(dev) == len(ref) == 40
+    for a, b in zip(dev, ref):
+        assert np.array_equal(a.indices, b["inliers"])
+
+
+def test_clusters_nan_points_and_empty(ctx):
+    xyz = np.concatenate([_blob([0, 0, 0], 4), np.full((5, 3), np.nan, np.float32), _blob([1, 0, 0], 4)])
+    dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=1, max_size=10 ** 9)
+    ref = orc.euclidean_clusters(*xyz.T, min_rate=0.0, max_rate=1.0, min_input_size=0)
+    assert [list(c.indices) for c in dev] == [list(c["inliers"]) for c in ref]
+    assert ctx.euclidean_clusters(*(np.zeros(0, np.float32),) * 3) == []
+
+
+def test_extract_indices(ctx):
+    x, y, z = (torch.from_numpy(a).cuda() for a in pitt.synth_frame(0, 5, 100, 80))
+    idx = torch.from_numpy(np.sort(np.random.default_rng(1).choice(8000, 3000, replace=False)).astype(np.int32)).cuda()
+    px, py, pz = ctx.extract_indices(x, y, z, idx, negative=False)
+    assert torch.equal(px, x[idx.long()]) and torch.equal(pz, z[idx.long()])
+    nx, ny, nz = ctx.extract_indices(x, y, z, idx, negative=True)
+    keep = torch.ones(8000, dtype=torch.bool, device="cuda")
+    keep[idx.long()] = False
+    assert torch.equal(ny, y[keep]) and nx.numel() == 5000
