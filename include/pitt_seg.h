@@ -120,6 +120,13 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
 int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev);
 
+/* Asynchronous form: enqueues the whole batch on the context's stream and returns; `results` is
+ * filled by pitt_wait (or by the next call on the context).  One batch in flight per context --
+ * overlap consecutive batches with two contexts on two streams. */
+int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
+                                   pitt_plane_result* results, int32_t* inliers_dev);
+int pitt_wait(pitt_ctx* ctx);
+
 /* Debug / parity hooks: per-hypothesis inlier counts of the last batch (host [n_frames*cap]),
  * hypotheses beyond a frame's T are unspecified. */
 int pitt_last_hypothesis_counts(pitt_ctx* ctx, int32_t frame, int32_t* counts, int32_t cap);

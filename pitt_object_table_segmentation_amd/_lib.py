@@ -135,6 +135,9 @@ SIGNATURES = {
                                   _f32p, _i32p]),
     "pitt_plane_segment_batch": (_i32, [_vp, ctypes.POINTER(Frames), ctypes.POINTER(SacParams),
                                         ctypes.POINTER(PlaneResult), _vp]),
+    "pitt_plane_segment_batch_async": (_i32, [_vp, ctypes.POINTER(Frames), ctypes.POINTER(SacParams),
+                                              ctypes.POINTER(PlaneResult), _vp]),
+    "pitt_wait": (_i32, [_vp]),
     "pitt_last_hypothesis_counts": (_i32, [_vp, _i32, _i32p, _i32]),
     "pitt_extract_indices": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _i64p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),

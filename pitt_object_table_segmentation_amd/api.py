@@ -230,6 +230,24 @@ class Context:
                     "pitt_plane_segment_batch")
         return res
 
+    def plane_segment_batch_async(self, batch: FrameBatch, params: Optional[L.SacParams] = None,
+                                  inliers_out=None) -> np.ndarray:
+        """Enqueue a batch on this context's stream and return immediately; the returned record
+        array is filled by wait().  One batch in flight per context."""
+        p = params or sac_params()
+        res = np.zeros(batch.n_frames, RESULT_DTYPE)
+        fr = batch.abi()
+        self._inflight = (res, fr, p, batch)  # keep the buffers alive until wait()
+        ptr = ctypes.c_void_p(inliers_out.data_ptr()) if inliers_out is not None else ctypes.c_void_p()
+        self._check(lib.pitt_plane_segment_batch_async(self.h, ctypes.byref(fr), ctypes.byref(p),
+                                                       res.ctypes.data_as(ctypes.POINTER(L.PlaneResult)), ptr),
+                    "pitt_plane_segment_batch_async")
+        return res
+
+    def wait(self) -> None:
+        self._check(lib.pitt_wait(self.h), "pitt_wait")
+        self._inflight = None
+
     def hypothesis_counts(self, frame: int, cap: int) -> np.ndarray:
         out = np.zeros(cap, np.int32)
         self._check(lib.pitt_last_hypothesis_counts(self.h, frame, _ip(out), cap), "hypothesis_counts")

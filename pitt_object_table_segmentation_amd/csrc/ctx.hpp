@@ -62,6 +62,16 @@ struct pitt_ctx {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, pitt::ProfTotal> totals;
 
+    // batch in flight (pitt_plane_segment_batch_async until pitt_wait)
+    bool inflight = false;
+    pitt_plane_result* inflight_results = nullptr;
+    int inflight_frames = 0;
+    void* inflight_hres = nullptr;
+    void* inflight_hstat = nullptr;
+    std::vector<std::pair<int64_t, int64_t>> inflight_stat;
+    std::vector<int> inflight_score_recs;
+    std::vector<int> inflight_chunks;
+
     // last batch (debug / parity hooks)
     int32_t last_hcap = 0;
     int32_t last_frames = 0;

@@ -29,7 +29,6 @@ namespace pitt {
 
 constexpr int kMaxAttempts = 8192;
 constexpr int kMaxAttemptWords = kMaxAttempts / 32;
-constexpr int kCovFramesPerWave = 7;  // 7 frames x 9 accumulators = 63 lanes
 
 struct FrameMeta {
     int64_t off;    // first point (multiple of 4)
@@ -162,24 +161,46 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
 
 // ------------------------------------------------------------------------------------------
 // k_score: persistent grid over (active frame, tile).  Each thread keeps 8 points (2 x float4 of
-// each coordinate plane) in registers and scores all H hypotheses of the chunk against them:
-// 3 mul + 3 add + 1 cmp per point-hypothesis on the VALU, the count on the scalar unit
-// (ballot -> s_bcnt1), one LDS add per wave and hypothesis.
+// each coordinate plane) in VGPRs and scores every hypothesis of the chunk against them: 3 mul +
+// 3 add + 1 cmp per point-hypothesis on the VALU (no FMA: PCL's rounding), the count on the scalar
+// unit (ballot -> s_bcnt1).  Coefficients arrive 8 hypotheses at a time as one scalar batch.
+// Per-wave counts go to LDS with plain stores; one coalesced 4*H-byte row per (frame, tile).
+constexpr int kHypBlock = 8;
+
+template <int ORDER, int NH>
+__device__ __forceinline__ void score_block(const float4* __restrict__ hc, const float (&px)[8],
+                                            const float (&py)[8], const float (&pz)[8], float thf,
+                                            int32_t* __restrict__ wcnt) {
+    float4 c[NH];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) c[k] = hc[k];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+        int wc = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const float d = plane_dot<ORDER>(c[k], px[p], py[p], pz[p]);
+            wc += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fabsf(d) < thf));
+        }
+        if ((threadIdx.x & 63) == 0) wcnt[k] = wc;
+    }
+}
+
 template <int ORDER>
 __global__ __launch_bounds__(kBlock) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap,
     const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0,
     int H, float thf, int32_t* __restrict__ tile_counts) {
-    __shared__ int32_t lds_cnt[kMaxChunk];
-    const int lane = threadIdx.x & 63;
-    const int64_t items = (int64_t)(*cnt) * tiles_max;
-    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = __builtin_amdgcn_readfirstlane(list[item / tiles_max]);
-        const int t = (int)(item % tiles_max);
+    __shared__ int32_t wcnt[kBlock / 64][kMaxChunk];
+    const int w = threadIdx.x >> 6;
+    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        const int li = item / tiles_max;
+        const int t = item - li * tiles_max;
+        const int f = __builtin_amdgcn_readfirstlane(list[li]);
         const FrameMeta m = meta[f];
         if (t >= m.tiles) continue;
-        for (int i = threadIdx.x; i < H; i += kBlock) lds_cnt[i] = 0;
         const int64_t tb = (int64_t)t * kTile;
         const float* x = X + m.off + tb;
         const float* y = Y + m.off + tb;
@@ -187,10 +208,10 @@ __global__ __launch_bounds__(kBlock) void k_score(
         float px[8], py[8], pz[8];
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-            const int li = g * 1024 + threadIdx.x * 4;
-            const float4 vx = *reinterpret_cast<const float4*>(x + li);
-            const float4 vy = *reinterpret_cast<const float4*>(y + li);
-            const float4 vz = *reinterpret_cast<const float4*>(z + li);
+            const int li4 = g * 1024 + threadIdx.x * 4;
+            const float4 vx = *reinterpret_cast<const float4*>(x + li4);
+            const float4 vy = *reinterpret_cast<const float4*>(y + li4);
+            const float4 vz = *reinterpret_cast<const float4*>(z + li4);
             px[4 * g + 0] = vx.x; px[4 * g + 1] = vx.y; px[4 * g + 2] = vx.z; px[4 * g + 3] = vx.w;
             py[4 * g + 0] = vy.x; py[4 * g + 1] = vy.y; py[4 * g + 2] = vy.z; py[4 * g + 3] = vy.w;
             pz[4 * g + 0] = vz.x; pz[4 * g + 1] = vz.y; pz[4 * g + 2] = vz.z; pz[4 * g + 3] = vz.w;
@@ -203,21 +224,14 @@ __global__ __launch_bounds__(kBlock) void k_score(
                 for (int s = 0; s < 4; ++s)
                     if (g * 1024 + threadIdx.x * 4 + s >= rem) px[4 * g + s] = __builtin_nanf("");
         }
-        __syncthreads();
         const float4* hc = hyp_coef + (int64_t)f * hcap + h0;
-        for (int h = 0; h < H; ++h) {
-            const float4 c = hc[h];
-            int wc = 0;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const float d = plane_dot<ORDER>(c, px[p], py[p], pz[p]);
-                wc += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fabsf(d) < thf));
-            }
-            if (lane == 0) atomicAdd(&lds_cnt[h], wc);
-        }
+        int h = 0;
+        for (; h + kHypBlock <= H; h += kHypBlock)
+            score_block<ORDER, kHypBlock>(hc + h, px, py, pz, thf, &wcnt[w][h]);
+        for (; h < H; ++h) score_block<ORDER, 1>(hc + h, px, py, pz, thf, &wcnt[w][h]);
         __syncthreads();
-        int32_t* out = tile_counts + ((int64_t)f * hcap + h0) * tiles_max + t;
-        for (int i = threadIdx.x; i < H; i += kBlock) out[(int64_t)i * tiles_max] = lds_cnt[i];
+        int32_t* out = tile_counts + ((int64_t)f * tiles_max + t) * hcap + h0;
+        for (int i = threadIdx.x; i < H; i += kBlock) out[i] = wcnt[0][i] + wcnt[1][i] + wcnt[2][i] + wcnt[3][i];
         __syncthreads();
     }
 }
@@ -235,9 +249,9 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int h = w; h < H; h += kBlock / 64) {
-        const int32_t* row = tile_counts + ((int64_t)f * hcap + h0 + h) * tiles_max;
+        const int32_t* col = tile_counts + (int64_t)f * tiles_max * hcap + h0 + h;
         int s = 0;
-        for (int t = lane; t < m.tiles; t += 64) s += row[t];
+        for (int t = lane; t < m.tiles; t += 64) s += col[(int64_t)t * hcap];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
         if (lane == 0) tot[h] = s;
@@ -317,13 +331,15 @@ __global__ __launch_bounds__(kBlock) void k_tile_offsets(
     if (!s.has_model) return;
     if (mode == 0 && !s.need_refine) return;
     const int tiles = meta[f].tiles;
-    const int32_t* row = mode == 0 ? tile_counts + ((int64_t)f * hcap + s.best_h) * tiles_max
+    // mode 0: tile_counts is [frame][tile][hcap]; mode 1: [frame][tile]
+    const int64_t stride = mode == 0 ? hcap : 1;
+    const int32_t* row = mode == 0 ? tile_counts + (int64_t)f * tiles_max * hcap + s.best_h
                                    : tile_counts + (int64_t)f * tiles_max;
     int32_t* out = offsets + (int64_t)f * (tiles_max + 1);
     int carry = 0;
     for (int base = 0; base < tiles; base += kBlock) {
         const int t = base + threadIdx.x;
-        const int v = t < tiles ? row[t] : 0;
+        const int v = t < tiles ? row[(int64_t)t * stride] : 0;
         int total;
         const int ex = block_exscan(v, lds4, &total);
         if (t < tiles) out[t] = carry + ex;
@@ -361,7 +377,9 @@ __device__ __forceinline__ uint32_t tile_predicates(const float* x, const float*
     return bits;
 }
 
-// k_select_xyz: compact (x, y, z) of the winning model's inliers, ascending point order.
+// k_select_xyz: compact (x, y, z) of the winning model's inliers, ascending point order.  The
+// tile's inliers are placed in LDS at their block-scan positions, then written out as contiguous,
+// coalesced runs.
 template <int ORDER>
 __global__ __launch_bounds__(kBlock) void k_select_xyz(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
@@ -370,9 +388,10 @@ __global__ __launch_bounds__(kBlock) void k_select_xyz(
     int tiles_max, float thf, float* __restrict__ CX, float* __restrict__ CY,
     float* __restrict__ CZ) {
     __shared__ int32_t lds4[kBlock / 64];
-    const int64_t items = (int64_t)n_frames * tiles_max;
-    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+    __shared__ float sx[kTile], sy[kTile], sz[kTile];
+    const int items = n_frames * tiles_max;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = item / tiles_max, t = item - f * tiles_max;
         const FrameMeta m = meta[f];
         if (t >= m.tiles || !st[f].need_refine) continue;
         const int64_t tb = (int64_t)t * kTile;
@@ -382,52 +401,67 @@ __global__ __launch_bounds__(kBlock) void k_select_xyz(
         const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
         int total;
         const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
-        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
         int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < 2; ++g)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int k = 4 * g + s;
                 if ((bits >> k) & 1u) {
-                    const int64_t o = ob + pos[g]++;
-                    CX[o] = P.x[k];
-                    CY[o] = P.y[k];
-                    CZ[o] = P.z[k];
+                    const int o = pos[g]++;
+                    sx[o] = P.x[k];
+                    sy[o] = P.y[k];
+                    sz[o] = P.z[k];
                 }
             }
+        __syncthreads();
+        const int cnt = (total & 0xFFFF) + (total >> 16);
+        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
+        for (int i = threadIdx.x; i < cnt; i += kBlock) {
+            CX[ob + i] = sx[i];
+            CY[ob + i] = sy[i];
+            CZ[ob + i] = sz[i];
         }
+        __syncthreads();
     }
 }
 
-// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order.  One wave serves 7 frames;
-// lane (slot, acc) owns accumulator acc (xx, xy, xz, yy, yz, zz, x, y, z) of frame
-// blockIdx.x * 7 + slot and adds its terms sequentially in inlier order (A6: the float sum is
-// order-sensitive, so each accumulator is one serial chain).  The compacted inlier coordinates
-// stream through a 3-slot LDS ring filled by async global->LDS DMA (global_load_lds_dwordx4, one
-// 1 KiB piece = 256 floats of one coordinate plane of one frame per wave instruction), two chunks
-// ahead of the chain.  Lane acc == 0 then runs eigen33 and writes the refined plane.
-constexpr int kCovChunk = 256;                      // inliers per chunk
-constexpr int kCovPlane = kCovChunk + 4;            // +16 B pad: planes start on different banks
-constexpr int kCovSlot = kCovFramesPerWave * 3 * kCovPlane;
+// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order (A6: nine float accumulators,
+// each a serial chain in ascending inlier order -- the rounding sequence must not change).
+// One wave per frame.  Per 256-inlier chunk the whole wave (a) DMAs x, y, z two chunks ahead into
+// an LDS ring (global_load_lds_dwordx4: one 1 KiB piece per coordinate), (b) forms the six product
+// streams (xx, xy, xz, yy, yz, zz; separately rounded, no FMA) into an LDS double buffer, and
+// (c) lanes 0..8 run the nine chains over the chunk with 16 reads in flight.  Lane 0 then divides
+// (Eigen 3.2 `accu /= n`), runs eigen33 and writes the refined plane.
+constexpr int kCovChunk = 256;
 constexpr int kCovRing = 3;
+constexpr int kCovRawFloats = kCovRing * 3 * kCovChunk;  // raw x, y, z ring
+constexpr int kCovProdFloats = 2 * 6 * kCovChunk;        // product double buffer
 
-__device__ __forceinline__ void cov_issue_chunk(float* ring, int slot_idx, const float* const* src,
-                                                const int64_t* nn, int64_t i0) {
+__device__ __forceinline__ void cov_issue(float* raw, int slot, const float* xs, const float* ys,
+                                          const float* zs, int64_t i0) {
     const int lane = threadIdx.x;
-    float* base = ring + slot_idx * kCovSlot;
-#pragma unroll
-    for (int fs = 0; fs < kCovFramesPerWave; ++fs) {
-        // Every chunk issues exactly 21 pieces so the counted vmcnt waits stay exact; a frame
-        // without inliers left re-reads its first piece (always inside the buffer).
-        const int64_t at = i0 < nn[fs] ? i0 : 0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float* g = src[fs * 3 + c] + at + lane * 4;
-            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(base + (fs * 3 + c) * kCovPlane),
-                                             16, 0, 0);
-        }
-    }
+    float* b = raw + slot * 3 * kCovChunk;
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    __builtin_amdgcn_global_load_lds(xs + i0 + lane * 4, (lds_ptr)(b), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(ys + i0 + lane * 4, (lds_ptr)(b + kCovChunk), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(zs + i0 + lane * 4, (lds_ptr)(b + 2 * kCovChunk), 16, 0, 0);
+}
+
+__device__ __forceinline__ void cov_produce(const float* raw, int slot, float* prod, int buf) {
+    const int lane = threadIdx.x;
+    const float* b = raw + slot * 3 * kCovChunk;
+    const float4 x = *reinterpret_cast<const float4*>(b + lane * 4);
+    const float4 y = *reinterpret_cast<const float4*>(b + kCovChunk + lane * 4);
+    const float4 z = *reinterpret_cast<const float4*>(b + 2 * kCovChunk + lane * 4);
+    float4* o = reinterpret_cast<float4*>(prod + buf * 6 * kCovChunk) + lane;
+    constexpr int S = kCovChunk / 4;
+    o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
+    o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+    o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
+    o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
+    o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
+    o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
 }
 
 template <int ORDER, int DIV>
@@ -435,79 +469,63 @@ __global__ __launch_bounds__(64) void k_cov_eigen(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float* __restrict__ CX, const float* __restrict__ CY, const float* __restrict__ CZ,
     int n_frames, float4* __restrict__ final_coef) {
-    extern __shared__ __attribute__((aligned(16))) float ring[];  // kCovRing slots + ones
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* raw = lds;
+    float* prod = lds + kCovRawFloats;
+    const int f = blockIdx.x;
+    if (f >= n_frames || !st[f].need_refine) return;
     const int lane = threadIdx.x;
-    const int slot = lane / 9, acc = lane % 9;
-    // per-frame streams of this wave (uniform)
-    const float* src[kCovFramesPerWave * 3];
-    int64_t nn[kCovFramesPerWave];
-    int64_t nmax = 0;
-#pragma unroll
-    for (int fs = 0; fs < kCovFramesPerWave; ++fs) {
-        const int f = blockIdx.x * kCovFramesPerWave + fs;
-        int64_t n = 0, off = 0;
-        if (f < n_frames && st[f].need_refine) {
-            n = st[f].best_count;
-            off = meta[f].off;
-        }
-        nn[fs] = n;
-        nmax = n > nmax ? n : nmax;
-        src[fs * 3 + 0] = CX + off;
-        src[fs * 3 + 1] = CY + off;
-        src[fs * 3 + 2] = CZ + off;
-    }
-    float* ones = ring + kCovRing * kCovSlot;
-    for (int i = lane; i < kCovChunk; i += 64) ones[i] = 1.0f;
-    const int f = blockIdx.x * kCovFramesPerWave + slot;
-    const bool active = slot < kCovFramesPerWave && f < n_frames && st[f].need_refine;
-    const int64_t n = active ? nn[slot] : 0;
-    const int ia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
-    const int ib[9] = {0, 1, 2, 1, 2, 2, -1, -1, -1};
-    const int sl = slot < kCovFramesPerWave ? slot : 0;
-    const int a_off = (sl * 3 + ia[acc]) * kCovPlane;
-    const int b_off = ib[acc] >= 0 ? (sl * 3 + ib[acc]) * kCovPlane : -1;
-    const int64_t nchunks = (nmax + kCovChunk - 1) / kCovChunk;
-    // prologue: chunks 0 and 1 in flight
-    if (nchunks > 0) cov_issue_chunk(ring, 0, src, nn, 0);
-    if (nchunks > 1) cov_issue_chunk(ring, 1, src, nn, kCovChunk);
+    const int64_t n = st[f].best_count;
+    const int64_t off = meta[f].off;
+    const float* xs = CX + off;
+    const float* ys = CY + off;
+    const float* zs = CZ + off;
+    const int nch = (int)((n + kCovChunk - 1) / kCovChunk);
+    cov_issue(raw, 0, xs, ys, zs, 0);
+    if (nch > 1) cov_issue(raw, 1, xs, ys, zs, kCovChunk);
+    if (nch > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cov_produce(raw, 0, prod, 0);
     float s = 0.0f;
-    for (int64_t c = 0; c < nchunks; ++c) {
-        if (c + 2 < nchunks) {
-            cov_issue_chunk(ring, (int)((c + 2) % kCovRing), src, nn, (c + 2) * kCovChunk);
-            // wait for chunk c: at most the two younger chunks (<= 42 pieces) still outstanding
-            asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
-        } else if (c + 1 < nchunks) {
-            asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+    for (int c = 0; c < nch; ++c) {
+        if (c + 2 < nch) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring slot (c+2)%3 no longer read
+            cov_issue(raw, (c + 2) % kCovRing, xs, ys, zs, (int64_t)(c + 2) * kCovChunk);
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");     // chunk c+1 landed
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_sched_barrier(0);
-        const float* sb = ring + (int)(c % kCovRing) * kCovSlot;
-        const float* pa = (const float*)__builtin_assume_aligned(sb + a_off, 16);
-        const float* pb = (const float*)__builtin_assume_aligned(b_off >= 0 ? sb + b_off : ones, 16);
-        const int64_t i0 = c * kCovChunk;
-        const int64_t rem = n - i0;
-        if (rem >= kCovChunk) {
-#pragma unroll 8
-            for (int i = 0; i < kCovChunk; i += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(pa + i);
-                const float4 b = *reinterpret_cast<const float4*>(pb + i);
-                s += a.x * b.x;
-                s += a.y * b.y;
-                s += a.z * b.z;
-                s += a.w * b.w;
+        if (c + 1 < nch) cov_produce(raw, (c + 1) % kCovRing, prod, (c + 1) & 1);
+        if (lane < 9) {
+            const float* p = lane < 6 ? prod + ((c & 1) * 6 + lane) * kCovChunk
+                                      : raw + ((c % kCovRing) * 3 + (lane - 6)) * kCovChunk;
+            const int64_t rem = n - (int64_t)c * kCovChunk;
+            if (rem >= kCovChunk) {
+#pragma unroll
+                for (int i = 0; i < kCovChunk; i += 64) {
+                    float4 v[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) v[k] = *reinterpret_cast<const float4*>(p + i + 4 * k);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        s += v[k].x;
+                        s += v[k].y;
+                        s += v[k].z;
+                        s += v[k].w;
+                    }
+                }
+            } else {
+                for (int i = 0; i < (int)rem; ++i) s += p[i];
             }
-        } else if (rem > 0) {
-            for (int i = 0; i < rem; ++i) s += pa[i] * pb[i];
         }
     }
-    // gather the 9 accumulators of this frame into its acc == 0 lane
     float a9[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, sl * 9 + k, 64);
-    if (!active || acc != 0) return;
+    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, k, 64);
+    if (lane != 0) return;
     const float fn = (float)n;
-    if constexpr (DIV == 0) {
+    if constexpr (DIV == 0) {  // Eigen 3.2: accu /= n  ==>  accu * (1/n)
         const float r = 1.0f / fn;
 #pragma unroll
         for (int k = 0; k < 9; ++k) a9[k] = a9[k] * r;
@@ -539,9 +557,9 @@ __global__ __launch_bounds__(kBlock) void k_count_final(
     const float4* __restrict__ final_coef, int n_frames, int tiles_max, float thf,
     int32_t* __restrict__ tile_counts2) {
     __shared__ int32_t lds4[kBlock / 64];
-    const int64_t items = (int64_t)n_frames * tiles_max;
-    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+    const int items = n_frames * tiles_max;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = item / tiles_max, t = item - f * tiles_max;
         const FrameMeta m = meta[f];
         if (t >= m.tiles || !st[f].has_model) continue;
         const int64_t tb = (int64_t)t * kTile;
@@ -554,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_count_final(
     }
 }
 
-// Write the final inlier indices (relative to the frame), ascending.
+// Write the final inlier indices (relative to the frame), ascending, via LDS staging.
 template <int ORDER>
 __global__ __launch_bounds__(kBlock) void k_write_final(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
@@ -562,9 +580,10 @@ __global__ __launch_bounds__(kBlock) void k_write_final(
     const float4* __restrict__ final_coef, const int32_t* __restrict__ offsets, int n_frames,
     int tiles_max, float thf, int32_t* __restrict__ out) {
     __shared__ int32_t lds4[kBlock / 64];
-    const int64_t items = (int64_t)n_frames * tiles_max;
-    for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = (int)(item / tiles_max), t = (int)(item % tiles_max);
+    __shared__ int32_t si[kTile];
+    const int items = n_frames * tiles_max;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        const int f = item / tiles_max, t = item - f * tiles_max;
         const FrameMeta m = meta[f];
         if (t >= m.tiles || !st[f].has_model) continue;
         const int64_t tb = (int64_t)t * kTile;
@@ -574,15 +593,19 @@ __global__ __launch_bounds__(kBlock) void k_write_final(
         const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
         int total;
         const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
-        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
         int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             const int li = (int)tb + g * 1024 + threadIdx.x * 4;
 #pragma unroll
             for (int s = 0; s < 4; ++s)
-                if ((bits >> (4 * g + s)) & 1u) out[ob + pos[g]++] = li + s;
+                if ((bits >> (4 * g + s)) & 1u) si[pos[g]++] = li + s;
         }
+        __syncthreads();
+        const int cnt = (total & 0xFFFF) + (total >> 16);
+        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
+        for (int i = threadIdx.x; i < cnt; i += kBlock) out[ob + i] = si[i];
+        __syncthreads();
     }
 }
 
@@ -628,8 +651,10 @@ __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __r
 template <typename T>
 static T* as(void* p) { return static_cast<T*>(p); }
 
+// Persistent grids of 6 blocks x 4 waves per CU (24 of 32 wave slots): enough loads in flight to
+// saturate HBM, and free slots for the latency-bound k_cov_eigen of a batch on another stream.
 static int grid_items(int64_t items) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(items, 256 * 8));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(items, 256 * 6));
 }
 
 template <int ORDER, int DIV>
@@ -650,6 +675,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     const int A = hcap + std::max(0, p->sampler_slack);
     if (A > kMaxAttempts) return ctx->fail(PITT_E_INVALID, "max_iterations + sampler_slack exceeds 8191");
     const float thf = float_threshold(p->threshold);
+    if ((int64_t)nf * tiles_max >= ((int64_t)1 << 31) || (int64_t)nf * hcap * tiles_max >= ((int64_t)1 << 40))
+        return ctx->fail(PITT_E_INVALID, "batch too large (frames x tiles must stay below 2^31)");
 
     // --- sampler tables: one per distinct point count ---
     std::vector<int64_t> distinct;
@@ -759,9 +786,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            fr->x, fr->y, fr->z, meta, st, best_coef, offs1, nf, tiles_max, thf, CX, CY, CZ);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_cov_eigen", 0.0);
-        hipLaunchKernelGGL((k_cov_eigen<ORDER, DIV>), dim3((nf + kCovFramesPerWave - 1) / kCovFramesPerWave),
-                           dim3(64), (kCovRing * kCovSlot + kCovChunk) * sizeof(float), sm, meta, st, CX, CY, CZ,
-                           nf, final_coef);
+        hipLaunchKernelGGL((k_cov_eigen<ORDER, DIV>), dim3(nf), dim3(64),
+                           (kCovRawFloats + kCovProdFloats) * sizeof(float), sm, meta, st, CX, CY, CZ, nf,
+                           final_coef);
         ctx->prof_end(rec);
     }
     rec = ctx->prof_begin("k_count_final", (double)total_pts * 12.0);
@@ -783,20 +810,39 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
-    PITT_HIP_TRY(hipStreamSynchronize(sm));
-    std::memcpy(results, hres, (size_t)nf * sizeof(pitt_plane_result));
-    // algorithmic bytes of each score launch: 12 B per point of every active frame's tiles
-    // (the full tiles are read) + the per-tile count words written.
-    for (int c = 0; c < nchunks; ++c)
-        ctx->prof_set_bytes(score_recs[(size_t)c], (double)hstat[c].tiles * kTile * 12.0 +
-                                                       (double)hstat[c].tiles * chunks[(size_t)c] * 4.0);
+    // completion (pitt_wait): copy results out, price the score launches
+    ctx->inflight = true;
+    ctx->inflight_results = results;
+    ctx->inflight_frames = nf;
+    ctx->inflight_hres = hres;
+    ctx->inflight_stat.assign((size_t)(nchunks + 1), {0, 0});
+    ctx->inflight_score_recs = score_recs;
+    ctx->inflight_chunks = chunks;
+    ctx->inflight_hstat = hstat;
     ctx->last_hcap = hcap;
     ctx->last_frames = nf;
     return PITT_OK;
 }
 
+// Completes the batch enqueued on ctx (if any): waits for the stream, copies the per-frame results
+// to the caller's array and fills in the algorithmic bytes of each k_score launch (12 B per point
+// of every active frame's tiles + the per-tile count words written).
+int finish_batch(pitt_ctx* ctx) {
+    if (!ctx->inflight) return PITT_OK;
+    ctx->inflight = false;
+    PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::memcpy(ctx->inflight_results, ctx->inflight_hres, (size_t)ctx->inflight_frames * sizeof(pitt_plane_result));
+    const ChunkStat* hstat = (const ChunkStat*)ctx->inflight_hstat;
+    for (size_t c = 0; c < ctx->inflight_score_recs.size(); ++c)
+        ctx->prof_set_bytes(ctx->inflight_score_recs[c],
+                            (double)hstat[c].tiles * kTile * 12.0 + (double)hstat[c].tiles * ctx->inflight_chunks[c] * 4.0);
+    return PITT_OK;
+}
+
 int plane_segment_batch_impl(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev) {
+    int rc = finish_batch(ctx);  // one batch in flight per context
+    if (rc) return rc;
     const int key = p->reduce_order * 2 + (p->div_mode ? 1 : 0);
     switch (key) {
     case 0: return run_plane_batch<0, 0>(ctx, fr, p, results, inliers_dev);

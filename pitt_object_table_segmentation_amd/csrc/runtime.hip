@@ -15,6 +15,7 @@
 namespace pitt {
 int plane_segment_batch_impl(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev);
+int finish_batch(pitt_ctx* ctx);
 
 // A2: drawIndexSample's index triples for a cloud of n points.  The shuffled index vector of
 // SampleConsensusModel is the identity except at the positions the swaps touched, so it is kept
@@ -167,6 +168,7 @@ int pitt_create(pitt_ctx** out, int hip_device) {
 
 void pitt_destroy(pitt_ctx* ctx) {
     if (!ctx) return;
+    (void)pitt::finish_batch(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->bufs)
@@ -194,6 +196,18 @@ const char* pitt_last_error(pitt_ctx* ctx) { return ctx ? ctx->err.c_str() : "nu
 
 int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev) {
+    int rc = pitt_plane_segment_batch_async(ctx, fr, p, results, inliers_dev);
+    if (rc < 0) return rc;
+    return pitt_wait(ctx);
+}
+
+int pitt_wait(pitt_ctx* ctx) {
+    if (!ctx) return PITT_E_INVALID;
+    return pitt::finish_batch(ctx);
+}
+
+int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
+                                   pitt_plane_result* results, int32_t* inliers_dev) {
     if (!ctx) return PITT_E_INVALID;
     if (!fr || !p || !results) return ctx->fail(PITT_E_INVALID, "null argument");
     if (fr->n_frames < 0) return ctx->fail(PITT_E_INVALID, "n_frames < 0");
@@ -264,6 +278,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
 
 int pitt_last_hypothesis_counts(pitt_ctx* ctx, int32_t frame, int32_t* counts, int32_t cap) {
     if (!ctx || !counts) return PITT_E_INVALID;
+    if (int rc = pitt::finish_batch(ctx)) return rc;
     if (frame < 0 || frame >= ctx->last_frames) return ctx->fail(PITT_E_INVALID, "frame out of range");
     auto it = ctx->bufs.find("hyp_total");
     if (it == ctx->bufs.end()) return ctx->fail(PITT_E_INVALID, "no batch run yet");
@@ -294,6 +309,7 @@ int pitt_profile_enable(pitt_ctx* ctx, int32_t on) {
 int pitt_profile_get(pitt_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms,
                      double* algorithmic_bytes) {
     if (!ctx || !kernel) return PITT_E_INVALID;
+    if (int rc = pitt::finish_batch(ctx)) return rc;
     int rc = ctx->prof_collect();
     if (rc) return rc;
     auto it = ctx->totals.find(kernel);
