@@ -160,86 +160,236 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
 }
 
 // ------------------------------------------------------------------------------------------
-// k_score: persistent grid over (active frame, tile).  Each thread keeps 8 points (2 x float4 of
-// each coordinate plane) in VGPRs and scores every hypothesis of the chunk against them: 3 mul +
-// 3 add + 1 cmp per point-hypothesis on the VALU (no FMA: PCL's rounding), the count on the scalar
-// unit (ballot -> s_bcnt1).  Coefficients arrive 8 hypotheses at a time as one scalar batch.
-// Per-wave counts go to LDS with plain stores; one coalesced 4*H-byte row per (frame, tile).
-constexpr int kHypBlock = 8;
+// k_score: persistent grid whose workers are WAVES.  A wave owns whole (active frame, 2048-point
+// tile) items and walks each in 4 sub-steps of 512 points (8 per lane: 2 x float4 of each
+// coordinate plane), with the next sub-step -- or the next item's first -- already loading into a
+// second register set while the current one is scored.
+//
+// Per point-hypothesis: 3 mul + 3 add + 1 cmp on the VALU (no FMA: PCL's rounding), the count on
+// the scalar unit (ballot -> s_bcnt1).  Every VALU operand is a VGPR: on gfx950 a wave64 VALU op
+// that reads an SGPR issues at half rate (tools/microbench/valu_asm.hip: v_mul_f32 s,v 1.71 ns vs
+// v,v 0.93 ns per SIMD), so the item's coefficients are staged once into the wave's LDS row and
+// read back per hypothesis with broadcast ds_read_b128, and the threshold lives in a VGPR.
+// Counts accumulate in the wave's LDS row (no block barriers); one coalesced row per item.
+#ifndef PITT_SCORE_EXP
+#define PITT_SCORE_EXP 0  // timing experiments only: 3 = synthetic points (no point loads)
+#endif
+#ifndef PITT_SCORE_PTS
+#define PITT_SCORE_PTS 4
+#endif
+#ifndef PITT_SCORE_NH
+#define PITT_SCORE_NH 4
+#endif
+constexpr int kHypBlock = PITT_SCORE_NH;   // hypotheses per LDS coefficient batch
+constexpr int kPts = PITT_SCORE_PTS;       // points per lane per sub-step (4 or 8)
+constexpr int kSub = 64 * kPts;            // points per wave sub-step
+constexpr int kSubs = kTile / kSub;        // sub-steps per item
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 
-template <int ORDER, int NH>
-__device__ __forceinline__ void score_block(const float4* __restrict__ hc, const float (&px)[8],
-                                            const float (&py)[8], const float (&pz)[8], float thf,
-                                            int32_t* __restrict__ wcnt) {
-    float4 c[NH];
+struct SubPts {
+    float x[kPts], y[kPts], z[kPts];
+};
+
+struct ScoreItem {
+    int64_t base;  // first point of the tile (global)
+    int32_t rem;   // points of the frame from the tile start, clamped to kTile
+    int32_t f, t;
+};
+
+__device__ __forceinline__ void load_sub(const float* __restrict__ X, const float* __restrict__ Y,
+                                         const float* __restrict__ Z, int64_t p0, int lane, SubPts& P) {
 #pragma unroll
-    for (int k = 0; k < NH; ++k) c[k] = hc[k];
-#pragma unroll
-    for (int k = 0; k < NH; ++k) {
-        int wc = 0;
-#pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            const float d = plane_dot<ORDER>(c[k], px[p], py[p], pz[p]);
-            wc += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fabsf(d) < thf));
-        }
-        if ((threadIdx.x & 63) == 0) wcnt[k] = wc;
+    for (int g = 0; g < kPts / 4; ++g) {
+        const int64_t i = p0 + g * 256 + lane * 4;
+#if PITT_SCORE_EXP == 3
+        const float fi = (float)(int)i * 1e-7f;
+        const float4 vx = make_float4(fi, fi + 1e-3f, fi + 2e-3f, fi + 3e-3f);
+        const float4 vy = make_float4(fi * 0.5f, fi * 0.25f, fi * 0.125f, fi * 0.0625f);
+        const float4 vz = make_float4(fi + 1.0f, fi + 1.5f, fi + 2.0f, fi + 2.5f);
+#else
+        const float4 vx = *reinterpret_cast<const float4*>(X + i);
+        const float4 vy = *reinterpret_cast<const float4*>(Y + i);
+        const float4 vz = *reinterpret_cast<const float4*>(Z + i);
+#endif
+        P.x[4 * g + 0] = vx.x; P.x[4 * g + 1] = vx.y; P.x[4 * g + 2] = vx.z; P.x[4 * g + 3] = vx.w;
+        P.y[4 * g + 0] = vy.x; P.y[4 * g + 1] = vy.y; P.y[4 * g + 2] = vy.z; P.y[4 * g + 3] = vy.w;
+        P.z[4 * g + 0] = vz.x; P.z[4 * g + 1] = vz.y; P.z[4 * g + 2] = vz.z; P.z[4 * g + 3] = vz.w;
     }
 }
 
-template <int ORDER>
-__global__ __launch_bounds__(kBlock) void k_score(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0,
-    int H, float thf, int32_t* __restrict__ tile_counts) {
-    __shared__ int32_t wcnt[kBlock / 64][kMaxChunk];
-    const int w = threadIdx.x >> 6;
-    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int li = item / tiles_max;
-        const int t = item - li * tiles_max;
+// The item's coefficients, lane i <- hypothesis h0 + i + 64 j (clamped: rows past H are never read).
+template <int NST>
+struct CoefRegs {
+    float4 c[NST];
+};
+
+template <int NST>
+__device__ __forceinline__ void load_coefs(const float4* __restrict__ hc, int H, int lane, CoefRegs<NST>& C) {
+#pragma unroll
+    for (int j = 0; j < NST; ++j) C.c[j] = hc[min(lane + 64 * j, H - 1)];
+}
+
+// First valid item at or after `it` in this wave's stride (frames shorter than tiles_max skip).
+__device__ __forceinline__ int next_item(int it, int stride, int items, int tiles_max,
+                                         const int32_t* __restrict__ list,
+                                         const FrameMeta* __restrict__ meta, ScoreItem& r) {
+    for (; it < items; it += stride) {
+        const int li = it / tiles_max;
+        const int t = it - li * tiles_max;
         const int f = __builtin_amdgcn_readfirstlane(list[li]);
         const FrameMeta m = meta[f];
-        if (t >= m.tiles) continue;
-        const int64_t tb = (int64_t)t * kTile;
-        const float* x = X + m.off + tb;
-        const float* y = Y + m.off + tb;
-        const float* z = Z + m.off + tb;
-        float px[8], py[8], pz[8];
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int li4 = g * 1024 + threadIdx.x * 4;
-            const float4 vx = *reinterpret_cast<const float4*>(x + li4);
-            const float4 vy = *reinterpret_cast<const float4*>(y + li4);
-            const float4 vz = *reinterpret_cast<const float4*>(z + li4);
-            px[4 * g + 0] = vx.x; px[4 * g + 1] = vx.y; px[4 * g + 2] = vx.z; px[4 * g + 3] = vx.w;
-            py[4 * g + 0] = vy.x; py[4 * g + 1] = vy.y; py[4 * g + 2] = vy.z; py[4 * g + 3] = vy.w;
-            pz[4 * g + 0] = vz.x; pz[4 * g + 1] = vz.y; pz[4 * g + 2] = vz.z; pz[4 * g + 3] = vz.w;
+        if (t < m.tiles) {
+            r.base = m.off + (int64_t)t * kTile;
+            r.rem = (int32_t)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
+            r.f = f;
+            r.t = t;
+            return it;
         }
-        const int64_t rem = m.n - tb;
-        if (rem < kTile) {  // tail tile: points past the frame never count (NaN fails every test)
+    }
+    return items;
+}
+
+template <int ORDER, int NH, bool FIRST>
+__device__ __forceinline__ void score_block(const float4* cl, const SubPts& P, float tv, int lane,
+                                            int32_t* __restrict__ wc) {
+    float4 c[NH];
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
+    for (int k = 0; k < NH; ++k) c[k] = cl[k];  // LDS broadcast -> VGPRs
+    int v = 0;  // lane k <- count of hypothesis k (v_writelane), then one LDS op per lane
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    if (g * 1024 + threadIdx.x * 4 + s >= rem) px[4 * g + s] = __builtin_nanf("");
+    for (int k = 0; k < NH; ++k) {
+        // the 8 compare masks land in distinct SGPR pairs before any is counted (one shared mask
+        // register would make every v_cmp wait for the previous s_bcnt1); the products and sums
+        // are formed 4 points at a time so independent chains sit side by side
+        uint64_t m[kPts];
+#pragma unroll
+        for (int q = 0; q < kPts; q += 4) {
+            float a0[4], a1[4], a2[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) a0[p] = c[k].x * P.x[q + p];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) a2[p] = c[k].z * P.z[q + p];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) a1[p] = c[k].y * P.y[q + p];
+            if constexpr (ORDER == 0) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) a0[p] = a0[p] + a2[p];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) a1[p] = a1[p] + c[k].w;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) a0[p] = a0[p] + a1[p];
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) a0[p] = red4<ORDER>(a0[p], a1[p], a2[p], c[k].w);
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) m[q + p] = __builtin_amdgcn_ballot_w64(fabsf(a0[p]) < tv);
         }
-        const float4* hc = hyp_coef + (int64_t)f * hcap + h0;
-        int h = 0;
-        for (; h + kHypBlock <= H; h += kHypBlock)
-            score_block<ORDER, kHypBlock>(hc + h, px, py, pz, thf, &wcnt[w][h]);
-        for (; h < H; ++h) score_block<ORDER, 1>(hc + h, px, py, pz, thf, &wcnt[w][h]);
-        __syncthreads();
-        int32_t* out = tile_counts + ((int64_t)f * tiles_max + t) * hcap + h0;
-        for (int i = threadIdx.x; i < H; i += kBlock) out[i] = wcnt[0][i] + wcnt[1][i] + wcnt[2][i] + wcnt[3][i];
-        __syncthreads();
+        int n = 0;
+#pragma unroll
+        for (int p = 0; p < kPts; ++p) n += __builtin_popcountll(m[p]);
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(n), "i"(k));
+    }
+    if (lane < NH) {
+        if constexpr (FIRST) wc[lane] = v;
+        else __hip_atomic_fetch_add(&wc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+}
+
+template <int ORDER, bool FIRST>
+__device__ __forceinline__ void score_sub(const float4* cl, int H, SubPts& P, int rem, float tv, int lane,
+                                          int32_t* __restrict__ wc) {
+    if (rem < kSub) {  // frame tail: points past the frame never count (NaN fails every test)
+#pragma unroll
+        for (int g = 0; g < kPts / 4; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (g * 256 + lane * 4 + q >= rem) P.x[4 * g + q] = __builtin_nanf("");
+    }
+    int h = 0;
+    for (; h + kHypBlock <= H; h += kHypBlock) score_block<ORDER, kHypBlock, FIRST>(cl + h, P, tv, lane, wc + h);
+    for (; h < H; ++h) score_block<ORDER, 1, FIRST>(cl + h, P, tv, lane, wc + h);
+}
+
+// NST = ceil(H / 64) stores per lane, unpredicated (rows are padded by 64 counts).
+template <int NST>
+__device__ __forceinline__ void store_counts(int32_t* __restrict__ out, const int32_t* row, int lane) {
+    asm volatile("" ::: "memory");  // compiler barrier only: the wave's LDS ops complete in order
+#pragma unroll
+    for (int j = 0; j < NST; ++j) out[lane + 64 * j] = row[lane + 64 * j];
+    asm volatile("" ::: "memory");
+}
+
+template <int NST>
+__device__ __forceinline__ void put_coefs(float4* cl, const CoefRegs<NST>& C, int lane) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NST; ++j) cl[lane + 64 * j] = C.c[j];
+    asm volatile("" ::: "memory");
+}
+
+// The loop issues a fixed sequence of vector-memory ops -- per item: 6 point loads per sub-step,
+// NST coefficient loads with the next item's first sub-step, NST count stores -- with nothing
+// conditional (the prologue stores NST dummy rows into the padding), so every s_waitcnt the
+// compiler places is an exact vmcnt(N) that leaves the prefetched sub-step in flight.
+template <int ORDER, int NST>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 ? 4 : 6, NST >= 4 ? 4 : 8))) void k_score(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap, int hstride,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0,
+    int H, float thf, int32_t* __restrict__ tile_counts) {
+    __shared__ float4 wcoef[kWaves][NST * 64];
+    __shared__ int32_t wcnt[kWaves][NST * 64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    float4* cl = wcoef[w];
+    int32_t* wc = wcnt[w];
+    float tv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
+    const int stride = gridDim.x * kWaves;
+    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
+    ScoreItem cur, nxt;
+    int it = next_item(blockIdx.x * kWaves + w, stride, items, tiles_max, list, meta, cur);
+    if (it >= items) return;
+    SubPts A, B;
+    CoefRegs<NST> C;
+    load_sub(X, Y, Z, cur.base, lane, A);
+    load_coefs<NST>(hyp_coef + (int64_t)cur.f * hcap + h0, H, lane, C);
+    {   // dummy stores into the row padding keep the per-iteration vmcnt sequence uniform
+        int32_t* pad = tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + hcap;
+#pragma unroll
+        for (int j = 0; j < NST; ++j) pad[lane] = 0;
+    }
+    while (true) {
+        load_sub(X, Y, Z, cur.base + kSub, lane, B);
+        put_coefs<NST>(cl, C, lane);
+        score_sub<ORDER, true>(cl, H, A, cur.rem, tv, lane, wc);
+#pragma unroll
+        for (int s = 1; s + 2 < kSubs; s += 2) {
+            load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, A);
+            score_sub<ORDER, false>(cl, H, B, cur.rem - s * kSub, tv, lane, wc);
+            load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, B);
+            score_sub<ORDER, false>(cl, H, A, cur.rem - (s + 1) * kSub, tv, lane, wc);
+        }
+        const int it2 = next_item(it + stride, stride, items, tiles_max, list, meta, nxt);
+        // unconditional (re-reads this item when the wave is done): a conditional load here
+        // makes the compiler wait for every outstanding load at the loop head
+        const ScoreItem& nx = it2 < items ? nxt : cur;
+        load_sub(X, Y, Z, nx.base, lane, A);
+        load_coefs<NST>(hyp_coef + (int64_t)nx.f * hcap + h0, H, lane, C);
+        score_sub<ORDER, false>(cl, H, B, cur.rem - (kSubs - 1) * kSub, tv, lane, wc);
+        store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
+        if (it2 >= items) break;
+        it = it2;
+        cur = nxt;
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // k_replay: RandomSampleConsensus::computeModel's serial control over the chunk's counts.
 __global__ __launch_bounds__(kBlock) void k_replay(
-    const int32_t* __restrict__ tile_counts, int hcap, int tiles_max, int h0, int H, int max_iter,
+    const int32_t* __restrict__ tile_counts, int hcap, int hstride, int tiles_max, int h0, int H, int max_iter,
     double log_probability, const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
     int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
     ChunkStat* __restrict__ next_stat) {
@@ -249,9 +399,9 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int h = w; h < H; h += kBlock / 64) {
-        const int32_t* col = tile_counts + (int64_t)f * tiles_max * hcap + h0 + h;
+        const int32_t* col = tile_counts + (int64_t)f * tiles_max * hstride + h0 + h;
         int s = 0;
-        for (int t = lane; t < m.tiles; t += 64) s += col[(int64_t)t * hcap];
+        for (int t = lane; t < m.tiles; t += 64) s += col[(int64_t)t * hstride];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
         if (lane == 0) tot[h] = s;
@@ -323,7 +473,7 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
 // Exclusive scan of a frame's per-tile counts.  mode 0: winning hypothesis row; mode 1: final.
 __global__ __launch_bounds__(kBlock) void k_tile_offsets(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const int32_t* __restrict__ tile_counts, int hcap, int tiles_max, int mode,
+    const int32_t* __restrict__ tile_counts, int hstride, int tiles_max, int mode,
     int32_t* __restrict__ offsets /* [f][tiles_max + 1] */) {
     __shared__ int32_t lds4[kBlock / 64];
     const int f = blockIdx.x;
@@ -332,8 +482,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_offsets(
     if (mode == 0 && !s.need_refine) return;
     const int tiles = meta[f].tiles;
     // mode 0: tile_counts is [frame][tile][hcap]; mode 1: [frame][tile]
-    const int64_t stride = mode == 0 ? hcap : 1;
-    const int32_t* row = mode == 0 ? tile_counts + (int64_t)f * tiles_max * hcap + s.best_h
+    const int64_t stride = mode == 0 ? hstride : 1;
+    const int32_t* row = mode == 0 ? tile_counts + (int64_t)f * tiles_max * hstride + s.best_h
                                    : tile_counts + (int64_t)f * tiles_max;
     int32_t* out = offsets + (int64_t)f * (tiles_max + 1);
     int carry = 0;
@@ -657,6 +807,24 @@ static int grid_items(int64_t items) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(items, 256 * 6));
 }
 
+// k_score's persistent grid: as many waves as the kernel's registers let stay resident (at most 6
+// blocks per CU), each wave a worker -- a block that cannot be resident would run its items after
+// everyone else.
+template <typename K>
+static int score_grid(K kern, int64_t items) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kBlock, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 4;
+    per_cu = std::min(per_cu, 6);
+    return (int)std::max<int64_t>(1, std::min<int64_t>((items + kWaves - 1) / kWaves, (int64_t)cus * per_cu));
+}
+
 template <int ORDER, int DIV>
 static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                            pitt_plane_result* results, int32_t* inliers_dev) {
@@ -718,7 +886,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     // --- chunk schedule (geometric after the first few HBM-bound 16-hypothesis passes) ---
     std::vector<int> chunks;
     for (int h0 = 0, i = 0; h0 < hcap; ++i) {
-        int H = i < 4 ? 16 : std::min(kMaxChunk, 16 << (i - 3));
+        int H = i < 4 ? 16 : std::min(kMaxScoreChunk, 16 << (i - 3));
         H = std::min(H, hcap - h0);
         chunks.push_back(H);
         h0 += H;
@@ -729,7 +897,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* hyp_coef = as<float4>(ctx->buf("hyp_coef", (size_t)nf * hcap * sizeof(float4)));
     int32_t* hyp_attempt = as<int32_t>(ctx->buf("hyp_attempt", (size_t)nf * hcap * 4));
     int32_t* hyp_total = as<int32_t>(ctx->buf("hyp_total", (size_t)nf * hcap * 4));
-    int32_t* tile_counts = as<int32_t>(ctx->buf("tile_counts", (size_t)nf * hcap * tiles_max * 4));
+    // rows padded by 64 counts: k_score's stores cover ceil(H / 64) * 64 entries unpredicated
+    const int hstride = hcap + 64;
+    int32_t* tile_counts = as<int32_t>(ctx->buf("tile_counts", (size_t)nf * hstride * tiles_max * 4));
     FrameState* st = as<FrameState>(ctx->buf("state", (size_t)nf * sizeof(FrameState)));
     int32_t* lists = as<int32_t>(ctx->buf("lists", (size_t)(nchunks + 1) * nf * 4));
     // counters + chunk stats in one zeroed block
@@ -764,12 +934,14 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int H = chunks[(size_t)c];
         rec = ctx->prof_begin("k_score", 0.0);
         score_recs.push_back(rec);
-        hipLaunchKernelGGL((k_score<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
-                           fr->x, fr->y, fr->z, meta, hyp_coef, hcap, lists + (size_t)c * nf, counters + c,
-                           tiles_max, h0, H, thf, tile_counts);
+        auto kern = H <= 64 ? k_score<ORDER, 1> : H <= 128 ? k_score<ORDER, 2> : k_score<ORDER, 4>;
+        hipLaunchKernelGGL(kern, dim3(score_grid(kern, (int64_t)nf * tiles_max)), dim3(kBlock), 0, sm, fr->x, fr->y,
+                           fr->z, meta, hyp_coef, hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H,
+                           thf, tile_counts);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
-        hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, tiles_max, h0, H, max_iter,
+        hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride, tiles_max, h0, H,
+                           max_iter,
                            log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf, counters + c + 1,
                            cstat + c + 1);
         ctx->prof_end(rec);
@@ -778,7 +950,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                        p->optimize ? 1 : 0, best_coef, final_coef);
     if (p->optimize) {
         rec = ctx->prof_begin("k_tile_offsets", 0.0);
-        hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, tile_counts, hcap, tiles_max,
+        hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, tile_counts, hstride, tiles_max,
                            0, offs1);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_select_xyz", (double)total_pts * 12.0);
