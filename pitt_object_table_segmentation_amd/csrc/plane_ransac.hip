@@ -7,10 +7,10 @@
 //                   VGPRs and reused across the H hypotheses, wave ballot + s_bcnt1 counting
 //   k_replay x C    PCL's serial best / adaptive-k logic over the chunk's counts (A5); builds
 //                   the next chunk's active-frame list on the device (no host round trip)
-//   k_tile_offsets  exclusive scan of the winning hypothesis' per-tile counts
-//   k_select_xyz    ordered compaction of the winning model's inliers (x, y, z)
-//   k_cov_eigen     9 float accumulators in exact PCL order (one lane each) + eigen33 (A6, A7)
-//   k_count_final / k_tile_offsets / k_write_final   refined-model inlier list (ascending)
+//   k_decide        model / refinement decision per frame
+//   k_refine        per frame: winning model's inliers streamed in order into the nine exact-order
+//                   float accumulators + eigen33 (A6, A7), then the refined model's ascending
+//                   inlier list (one 2-wave block per frame)
 //   k_finalize      per-frame pitt_plane_result
 #include <hip/hip_runtime.h>
 
@@ -160,10 +160,13 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
 }
 
 // ------------------------------------------------------------------------------------------
-// k_score: persistent grid whose workers are WAVES.  A wave owns whole (active frame, 2048-point
-// tile) items and walks each in 4 sub-steps of 512 points (8 per lane: 2 x float4 of each
-// coordinate plane), with the next sub-step -- or the next item's first -- already loading into a
-// second register set while the current one is scored.
+// k_score: one wave per (active frame, 2048-point tile) item, 4 waves per block, one block per 4
+// items (the grid covers every frame's tiles; waves past the active items exit at once).  A wave
+// walks its item in kSubs sub-steps of 64 * kPts points (kPts per lane: float4s of each coordinate
+// plane), the next sub-step already loading into a second register set while the current one is
+// scored.  (A persistent grid of wave workers was tried: with other streams' kernels holding part
+// of the CUs, blocks that become resident late carry their whole share after everyone else, and a
+// global atomic work counter serialises at ~5 ns per grab.)
 //
 // Per point-hypothesis: 3 mul + 3 add + 1 cmp on the VALU (no FMA: PCL's rounding), the count on
 // the scalar unit (ballot -> s_bcnt1).  Every VALU operand is a VGPR: on gfx950 a wave64 VALU op
@@ -230,24 +233,21 @@ __device__ __forceinline__ void load_coefs(const float4* __restrict__ hc, int H,
     for (int j = 0; j < NST; ++j) C.c[j] = hc[min(lane + 64 * j, H - 1)];
 }
 
-// First valid item at or after `it` in this wave's stride (frames shorter than tiles_max skip).
-__device__ __forceinline__ int next_item(int it, int stride, int items, int tiles_max,
-                                         const int32_t* __restrict__ list,
-                                         const FrameMeta* __restrict__ meta, ScoreItem& r) {
-    for (; it < items; it += stride) {
-        const int li = it / tiles_max;
-        const int t = it - li * tiles_max;
-        const int f = __builtin_amdgcn_readfirstlane(list[li]);
-        const FrameMeta m = meta[f];
-        if (t < m.tiles) {
-            r.base = m.off + (int64_t)t * kTile;
-            r.rem = (int32_t)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
-            r.f = f;
-            r.t = t;
-            return it;
-        }
-    }
-    return items;
+// Item it -> (frame, tile).  Tiles past a shorter frame's end (ragged batches) become empty
+// items on the frame's first tile: every item then issues the same memory operations.
+__device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const int32_t* __restrict__ list,
+                                                  const FrameMeta* __restrict__ meta) {
+    ScoreItem r;
+    const int li = it / tiles_max;
+    const int t = it - li * tiles_max;
+    const int f = __builtin_amdgcn_readfirstlane(list[li]);
+    const FrameMeta m = meta[f];
+    const bool ok = t < m.tiles;
+    r.base = m.off + (ok ? (int64_t)t * kTile : 0);
+    r.rem = ok ? (int32_t)min(m.n - (int64_t)t * kTile, (int64_t)kTile) : 0;
+    r.f = f;
+    r.t = t;
+    return r;
 }
 
 template <int ORDER, int NH, bool FIRST>
@@ -337,53 +337,36 @@ template <int ORDER, int NST>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 ? 4 : 6, NST >= 4 ? 4 : 8))) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap, int hstride,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0,
-    int H, float thf, int32_t* __restrict__ tile_counts) {
+    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0, int H,
+    float thf, int32_t* __restrict__ tile_counts) {
     __shared__ float4 wcoef[kWaves][NST * 64];
     __shared__ int32_t wcnt[kWaves][NST * 64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
+    const int it = blockIdx.x * kWaves + w;
+    if (it >= items) return;
     float4* cl = wcoef[w];
     int32_t* wc = wcnt[w];
     float tv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
-    const int stride = gridDim.x * kWaves;
-    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
-    ScoreItem cur, nxt;
-    int it = next_item(blockIdx.x * kWaves + w, stride, items, tiles_max, list, meta, cur);
-    if (it >= items) return;
+    const ScoreItem cur = resolve_item(it, tiles_max, list, meta);
     SubPts A, B;
     CoefRegs<NST> C;
     load_sub(X, Y, Z, cur.base, lane, A);
     load_coefs<NST>(hyp_coef + (int64_t)cur.f * hcap + h0, H, lane, C);
-    {   // dummy stores into the row padding keep the per-iteration vmcnt sequence uniform
-        int32_t* pad = tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + hcap;
+    load_sub(X, Y, Z, cur.base + kSub, lane, B);
+    put_coefs<NST>(cl, C, lane);
+    score_sub<ORDER, true>(cl, H, A, cur.rem, tv, lane, wc);
 #pragma unroll
-        for (int j = 0; j < NST; ++j) pad[lane] = 0;
+    for (int s = 1; s + 2 < kSubs; s += 2) {
+        load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, A);
+        score_sub<ORDER, false>(cl, H, B, cur.rem - s * kSub, tv, lane, wc);
+        load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, B);
+        score_sub<ORDER, false>(cl, H, A, cur.rem - (s + 1) * kSub, tv, lane, wc);
     }
-    while (true) {
-        load_sub(X, Y, Z, cur.base + kSub, lane, B);
-        put_coefs<NST>(cl, C, lane);
-        score_sub<ORDER, true>(cl, H, A, cur.rem, tv, lane, wc);
-#pragma unroll
-        for (int s = 1; s + 2 < kSubs; s += 2) {
-            load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, A);
-            score_sub<ORDER, false>(cl, H, B, cur.rem - s * kSub, tv, lane, wc);
-            load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, B);
-            score_sub<ORDER, false>(cl, H, A, cur.rem - (s + 1) * kSub, tv, lane, wc);
-        }
-        const int it2 = next_item(it + stride, stride, items, tiles_max, list, meta, nxt);
-        // unconditional (re-reads this item when the wave is done): a conditional load here
-        // makes the compiler wait for every outstanding load at the loop head
-        const ScoreItem& nx = it2 < items ? nxt : cur;
-        load_sub(X, Y, Z, nx.base, lane, A);
-        load_coefs<NST>(hyp_coef + (int64_t)nx.f * hcap + h0, H, lane, C);
-        score_sub<ORDER, false>(cl, H, B, cur.rem - (kSubs - 1) * kSub, tv, lane, wc);
-        store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
-        if (it2 >= items) break;
-        it = it2;
-        cur = nxt;
-    }
+    score_sub<ORDER, false>(cl, H, B, cur.rem - (kSubs - 1) * kSub, tv, lane, wc);
+    store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -464,216 +447,234 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
     if (s.has_model) {
         const float4 c = hyp_coef[(int64_t)f * hcap + s.best_h];
         best_coef[f] = c;
-        final_coef[f] = c;  // overwritten by k_cov_eigen when refined
+        final_coef[f] = c;  // overwritten by k_refine
     }
     st[f] = s;
     (void)meta;
 }
 
-// Exclusive scan of a frame's per-tile counts.  mode 0: winning hypothesis row; mode 1: final.
-__global__ __launch_bounds__(kBlock) void k_tile_offsets(
-    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const int32_t* __restrict__ tile_counts, int hstride, int tiles_max, int mode,
-    int32_t* __restrict__ offsets /* [f][tiles_max + 1] */) {
-    __shared__ int32_t lds4[kBlock / 64];
-    const int f = blockIdx.x;
-    const FrameState s = st[f];
-    if (!s.has_model) return;
-    if (mode == 0 && !s.need_refine) return;
-    const int tiles = meta[f].tiles;
-    // mode 0: tile_counts is [frame][tile][hcap]; mode 1: [frame][tile]
-    const int64_t stride = mode == 0 ? hstride : 1;
-    const int32_t* row = mode == 0 ? tile_counts + (int64_t)f * tiles_max * hstride + s.best_h
-                                   : tile_counts + (int64_t)f * tiles_max;
-    int32_t* out = offsets + (int64_t)f * (tiles_max + 1);
-    int carry = 0;
-    for (int base = 0; base < tiles; base += kBlock) {
-        const int t = base + threadIdx.x;
-        const int v = t < tiles ? row[(int64_t)t * stride] : 0;
-        int total;
-        const int ex = block_exscan(v, lds4, &total);
-        if (t < tiles) out[t] = carry + ex;
-        carry += total;
-    }
-    if (threadIdx.x == 0) out[tiles] = carry;
-}
+// ------------------------------------------------------------------------------------------
+// k_refine: everything after RANSAC for one frame, one 2-wave block per frame.
+//
+//   pass 1 (optimizeModelCoefficients, A6/A7): the producer wave streams the frame (4 points per
+//     lane per 256-point step, global_load_lds ring kRDepth1 steps deep), selects the winning
+//     model's inliers and appends them -- ascending -- to an LDS ring; the consumer wave's lanes
+//     0..8 run the nine float accumulators of computeMeanAndCovarianceMatrix over that ring in
+//     exact PCL order (product formed per element, separately rounded; 32 elements per batched
+//     read).  Consumer lane 0 then divides (Eigen 3.2 `accu /= n`), runs eigen33 and forms the
+//     refined plane.
+//   pass 2 (selectWithinDistance on the refined model): the producer wave streams the frame again
+//     and writes the ascending inlier indices straight to the caller's buffer.
+//
+// The two waves hand over ring space through LDS counters (W: produced, R: consumed) with
+// release/acquire ordering at workgroup scope.  Frames without refinement run pass 2 only.
+#ifndef PITT_REFINE_EXP
+#define PITT_REFINE_EXP 0  // timing experiments only: 1 = skip pass 2, 2 = skip pass 1,
+#endif                     // 3 = consumer skips the chain, 4 = producer skips the ring writes
+constexpr int kRChunk = 256;   // points per producer step (4 per lane)
+constexpr int kRSlot = 3 * kRChunk;          // floats per raw ring slot (x, y, z)
+constexpr int kRDepth1 = 6;    // pass 1: raw steps in flight (the rest of the pool is the inlier ring)
+constexpr int kRRing = 1024;   // compacted-inlier ring (points): 3 * kRRing floats = 4 slots
+constexpr int kRDepth2 = kRDepth1 + 3 * kRRing / kRSlot;  // pass 2: the whole pool is raw ring
+constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
 
-// Shared tile loader for the compaction kernels: the thread's 8 points (groups of 4 consecutive
-// points at tile offsets 4*tid and 1024 + 4*tid) and their inlier bits.
-struct TilePts {
-    float x[8], y[8], z[8];
+struct RefineLds {
+    float pool[kRDepth2 * kRSlot];  // pass 1: raw[kRDepth1] | cx | cy | cz;  pass 2: raw[kRDepth2]
+    float prod[6][kRBlk];           // xx, xy, xz, yy, yz, zz of the current chain block
+    int W, R, done, total;
+    float4 coef;
 };
 
-template <int ORDER>
-__device__ __forceinline__ uint32_t tile_predicates(const float* x, const float* y, const float* z,
-                                                    int64_t rem, float4 c, float thf, TilePts& P) {
-    uint32_t bits = 0;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        const int li = g * 1024 + threadIdx.x * 4;
-        const float4 vx = *reinterpret_cast<const float4*>(x + li);
-        const float4 vy = *reinterpret_cast<const float4*>(y + li);
-        const float4 vz = *reinterpret_cast<const float4*>(z + li);
-        P.x[4 * g + 0] = vx.x; P.x[4 * g + 1] = vx.y; P.x[4 * g + 2] = vx.z; P.x[4 * g + 3] = vx.w;
-        P.y[4 * g + 0] = vy.x; P.y[4 * g + 1] = vy.y; P.y[4 * g + 2] = vy.z; P.y[4 * g + 3] = vy.w;
-        P.z[4 * g + 0] = vz.x; P.z[4 * g + 1] = vz.y; P.z[4 * g + 2] = vz.z; P.z[4 * g + 3] = vz.w;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int k = 4 * g + s;
-            const bool in = (li + s < rem) && (fabsf(plane_dot<ORDER>(c, P.x[k], P.y[k], P.z[k])) < thf);
-            bits |= (in ? 1u : 0u) << k;
-        }
-    }
-    return bits;
+__device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth1 * kRSlot; }
+
+typedef __attribute__((address_space(3))) volatile int lds_vint;  // ds_read/ds_write, not flat
+
+// Hand-over counters.  LDS executes each wave's operations in issue order, so a counter written
+// after the data it covers is seen only after that data, and a counter read before a write is
+// performed before it; compiler barriers keep the source order.  (Workgroup-scope acquire/release
+// atomics would also wait for the ring's in-flight global loads: vmcnt(0).)
+__device__ __forceinline__ int lds_acquire(int* p) {
+    asm volatile("" ::: "memory");
+    const int v = *(lds_vint*)(p);
+    asm volatile("" ::: "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+    asm volatile("" ::: "memory");
+    *(lds_vint*)(p) = v;
+    asm volatile("" ::: "memory");
 }
 
-// k_select_xyz: compact (x, y, z) of the winning model's inliers, ascending point order.  The
-// tile's inliers are placed in LDS at their block-scan positions, then written out as contiguous,
-// coalesced runs.
-template <int ORDER>
-__global__ __launch_bounds__(kBlock) void k_select_xyz(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const float4* __restrict__ best_coef, const int32_t* __restrict__ offsets, int n_frames,
-    int tiles_max, float thf, float* __restrict__ CX, float* __restrict__ CY,
-    float* __restrict__ CZ) {
-    __shared__ int32_t lds4[kBlock / 64];
-    __shared__ float sx[kTile], sy[kTile], sz[kTile];
-    const int items = n_frames * tiles_max;
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = item / tiles_max, t = item - f * tiles_max;
-        const FrameMeta m = meta[f];
-        if (t >= m.tiles || !st[f].need_refine) continue;
-        const int64_t tb = (int64_t)t * kTile;
-        TilePts P;
-        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
-                                                     m.n - tb, best_coef[f], thf, P);
-        const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
-        int total;
-        const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
-        int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int k = 4 * g + s;
-                if ((bits >> k) & 1u) {
-                    const int o = pos[g]++;
-                    sx[o] = P.x[k];
-                    sy[o] = P.y[k];
-                    sz[o] = P.z[k];
-                }
-            }
-        __syncthreads();
-        const int cnt = (total & 0xFFFF) + (total >> 16);
-        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
-        for (int i = threadIdx.x; i < cnt; i += kBlock) {
-            CX[ob + i] = sx[i];
-            CY[ob + i] = sy[i];
-            CZ[ob + i] = sz[i];
-        }
-        __syncthreads();
-    }
-}
-
-// k_cov_eigen: computeMeanAndCovarianceMatrix in exact PCL order (A6: nine float accumulators,
-// each a serial chain in ascending inlier order -- the rounding sequence must not change).
-// One wave per frame.  Per 256-inlier chunk the whole wave (a) DMAs x, y, z two chunks ahead into
-// an LDS ring (global_load_lds_dwordx4: one 1 KiB piece per coordinate), (b) forms the six product
-// streams (xx, xy, xz, yy, yz, zz; separately rounded, no FMA) into an LDS double buffer, and
-// (c) lanes 0..8 run the nine chains over the chunk with 16 reads in flight.  Lane 0 then divides
-// (Eigen 3.2 `accu /= n`), runs eigen33 and writes the refined plane.
-constexpr int kCovChunk = 256;
-constexpr int kCovRing = 3;
-constexpr int kCovRawFloats = kCovRing * 3 * kCovChunk;  // raw x, y, z ring
-constexpr int kCovProdFloats = 2 * 6 * kCovChunk;        // product double buffer
-
-__device__ __forceinline__ void cov_issue(float* raw, int slot, const float* xs, const float* ys,
-                                          const float* zs, int64_t i0) {
-    const int lane = threadIdx.x;
-    float* b = raw + slot * 3 * kCovChunk;
+// Step c of the frame into ring slot c % DEPTH; steps past the end re-read the last step so that
+// every iteration issues the same three loads (the waits below are fixed vmcnt counts).
+template <int DEPTH>
+__device__ __forceinline__ void refine_issue(float* raw, const float* xs, const float* ys, const float* zs,
+                                             int c, int nch, int lane) {
     typedef __attribute__((address_space(3))) void* lds_ptr;
-    __builtin_amdgcn_global_load_lds(xs + i0 + lane * 4, (lds_ptr)(b), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(ys + i0 + lane * 4, (lds_ptr)(b + kCovChunk), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(zs + i0 + lane * 4, (lds_ptr)(b + 2 * kCovChunk), 16, 0, 0);
+    const int cc = min(c, nch - 1);
+    float* b = raw + (c % DEPTH) * kRSlot;
+    const int64_t o = (int64_t)cc * kRChunk + lane * 4;
+    __builtin_amdgcn_global_load_lds(xs + o, (lds_ptr)(b), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(ys + o, (lds_ptr)(b + kRChunk), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(zs + o, (lds_ptr)(b + 2 * kRChunk), 16, 0, 0);
 }
 
-__device__ __forceinline__ void cov_produce(const float* raw, int slot, float* prod, int buf) {
-    const int lane = threadIdx.x;
-    const float* b = raw + slot * 3 * kCovChunk;
-    const float4 x = *reinterpret_cast<const float4*>(b + lane * 4);
-    const float4 y = *reinterpret_cast<const float4*>(b + kCovChunk + lane * 4);
-    const float4 z = *reinterpret_cast<const float4*>(b + 2 * kCovChunk + lane * 4);
-    float4* o = reinterpret_cast<float4*>(prod + buf * 6 * kCovChunk) + lane;
-    constexpr int S = kCovChunk / 4;
-    o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
-    o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
-    o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
-    o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
-    o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
-    o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
-}
-
-template <int ORDER, int DIV>
-__global__ __launch_bounds__(64) void k_cov_eigen(
-    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const float* __restrict__ CX, const float* __restrict__ CY, const float* __restrict__ CZ,
-    int n_frames, float4* __restrict__ final_coef) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* raw = lds;
-    float* prod = lds + kCovRawFloats;
-    const int f = blockIdx.x;
-    if (f >= n_frames || !st[f].need_refine) return;
-    const int lane = threadIdx.x;
-    const int64_t n = st[f].best_count;
-    const int64_t off = meta[f].off;
-    const float* xs = CX + off;
-    const float* ys = CY + off;
-    const float* zs = CZ + off;
-    const int nch = (int)((n + kCovChunk - 1) / kCovChunk);
-    cov_issue(raw, 0, xs, ys, zs, 0);
-    if (nch > 1) cov_issue(raw, 1, xs, ys, zs, kCovChunk);
-    if (nch > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    cov_produce(raw, 0, prod, 0);
-    float s = 0.0f;
-    for (int c = 0; c < nch; ++c) {
-        if (c + 2 < nch) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring slot (c+2)%3 no longer read
-            cov_issue(raw, (c + 2) % kCovRing, xs, ys, zs, (int64_t)(c + 2) * kCovChunk);
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");     // chunk c+1 landed
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+// Producer: one pass over the frame with plane c.  PASS 1 appends the inliers' coordinates to the
+// LDS ring for the consumer; PASS 2 writes their indices to out (when given).  Returns the count.
+template <int ORDER, int PASS>
+__device__ __forceinline__ int refine_stream(RefineLds& L, const float* xs, const float* ys, const float* zs, int64_t n,
+                             float4 c, float thf, int lane, int32_t* __restrict__ out) {
+    constexpr int DEPTH = PASS == 1 ? kRDepth1 : kRDepth2;
+    const int nch = (int)((n + kRChunk - 1) / kRChunk);
+    float* raw = L.pool;
+    float* rx = ring_x(L);
+    asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));  // plane in registers before the ring starts
+#pragma unroll
+    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(raw, xs, ys, zs, k, nch, lane);
+    int wpos = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot refilled next are done
+        refine_issue<DEPTH>(raw, xs, ys, zs, ch + DEPTH - 1, nch, lane);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");  // step ch landed
         __builtin_amdgcn_sched_barrier(0);
-        if (c + 1 < nch) cov_produce(raw, (c + 1) % kCovRing, prod, (c + 1) & 1);
-        if (lane < 9) {
-            const float* p = lane < 6 ? prod + ((c & 1) * 6 + lane) * kCovChunk
-                                      : raw + ((c % kCovRing) * 3 + (lane - 6)) * kCovChunk;
-            const int64_t rem = n - (int64_t)c * kCovChunk;
-            if (rem >= kCovChunk) {
+        // the slot's reads in asm: the compiler treats any LDS read as aliasing the ring's
+        // in-flight global_load_lds writes and would wait for all of them (vmcnt(0))
+        const uint32_t b = (uint32_t)(uintptr_t)(raw + (ch % DEPTH) * kRSlot + lane * 4);
+        float4 x4, y4, z4;
+        asm volatile(
+            "ds_read_b128 %0, %3\n"
+            "ds_read_b128 %1, %3 offset:1024\n"
+            "ds_read_b128 %2, %3 offset:2048\n"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x4), "=&v"(y4), "=&v"(z4)
+            : "v"(b)
+            : "memory");
+        const float px[4] = {x4.x, x4.y, x4.z, x4.w};
+        const float py[4] = {y4.x, y4.y, y4.z, y4.w};
+        const float pz[4] = {z4.x, z4.y, z4.z, z4.w};
+        const int64_t p0 = (int64_t)ch * kRChunk + lane * 4;
+        uint32_t bits = 0;
 #pragma unroll
-                for (int i = 0; i < kCovChunk; i += 64) {
-                    float4 v[16];
+        for (int q = 0; q < 4; ++q) {
+            const bool in = (p0 + q < n) && (fabsf(plane_dot<ORDER>(c, px[q], py[q], pz[q])) < thf);
+            bits |= (in ? 1u : 0u) << q;
+        }
+        // ascending positions: exclusive prefix of the per-lane counts (0..4) from their bit slices
+        const int cnt = __builtin_popcount(bits);
+        const uint64_t b0 = __builtin_amdgcn_ballot_w64((cnt & 1) != 0);
+        const uint64_t b1 = __builtin_amdgcn_ballot_w64((cnt & 2) != 0);
+        const uint64_t b2 = __builtin_amdgcn_ballot_w64((cnt & 4) != 0);
+        const uint32_t lo = 0xFFFFFFFFu;
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b0 & lo), 0u)) +
+                        2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b1 & lo), 0u)) +
+                        4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b2 & lo), 0u));
+        const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+        if constexpr (PASS == 1) {
+            while (wpos + tot - lds_acquire(&L.R) > kRRing) __builtin_amdgcn_s_sleep(1);
+            int k = wpos + pre;
+#if PITT_REFINE_EXP != 4
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) v[k] = *reinterpret_cast<const float4*>(p + i + 4 * k);
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        s += v[k].x;
-                        s += v[k].y;
-                        s += v[k].z;
-                        s += v[k].w;
-                    }
+            for (int q = 0; q < 4; ++q)
+                if ((bits >> q) & 1u) {
+                    const int r = k & (kRRing - 1);
+                    rx[r] = px[q];
+                    rx[kRRing + r] = py[q];
+                    rx[2 * kRRing + r] = pz[q];
+                    ++k;
                 }
-            } else {
-                for (int i = 0; i < (int)rem; ++i) s += p[i];
+#endif
+            (void)k;
+            if (lane == 0) lds_release(&L.W, wpos + tot);
+        } else {
+            if (out) {
+                int k = wpos + pre;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if ((bits >> q) & 1u) out[k++] = (int32_t)(p0 + q);
             }
         }
+        wpos += tot;
     }
-    float a9[9];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read steps land before the pool is reused
+    return wpos;
+}
+
+// 16 dependent adds, back to back, in order.
+__device__ __forceinline__ void chain16(float& s, const float4& a, const float4& b, const float4& c, const float4& d) {
+    asm volatile(
+        "v_add_f32 %0, %0, %1\n v_add_f32 %0, %0, %2\n v_add_f32 %0, %0, %3\n v_add_f32 %0, %0, %4\n"
+        "v_add_f32 %0, %0, %5\n v_add_f32 %0, %0, %6\n v_add_f32 %0, %0, %7\n v_add_f32 %0, %0, %8\n"
+        "v_add_f32 %0, %0, %9\n v_add_f32 %0, %0, %10\n v_add_f32 %0, %0, %11\n v_add_f32 %0, %0, %12\n"
+        "v_add_f32 %0, %0, %13\n v_add_f32 %0, %0, %14\n v_add_f32 %0, %0, %15\n v_add_f32 %0, %0, %16"
+        : "+v"(s)
+        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x), "v"(c.y),
+          "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
+}
+
+// Consumer: lane k < 9 accumulates stream k of computeMeanAndCovarianceMatrix (xx, xy, xz, yy, yz,
+// zz, x, y, z) over the ring in ascending inlier order.  Per 256-element block all 64 lanes first
+// form the six product streams (separately rounded, as PCL) into LDS; lanes 0..8 then run their
+// chain as pure dependent adds, 64 elements per batched read.  Lanes >= 9 repeat lane 0's stream
+// (uniform control flow; results unused).  The last partial block goes element by element.
+__device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
+    const int k = lane < 9 ? lane : 0;
+    float* rx = ring_x(L);
+    float s = 0.0f;
+    int r = 0;
+    while (true) {
+        const int w = lds_acquire(&L.W);
+        if (w - r >= kRBlk) {
+#if PITT_REFINE_EXP == 3
+            r += kRBlk;
+            if (lane == 0) lds_release(&L.R, r);
+            continue;
+#endif
+            const int q = r & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
+            {
+                const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
+                const float4 y = *reinterpret_cast<const float4*>(rx + kRRing + q + 4 * lane);
+                const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRRing + q + 4 * lane);
+                float4* o = reinterpret_cast<float4*>(&L.prod[0][0]) + lane;
+                constexpr int S = kRBlk / 4;
+                o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
+                o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+                o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
+                o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
+                o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
+                o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
+            }
+            asm volatile("" ::: "memory");  // this wave's LDS writes precede its reads (in order)
+            const float* p = k < 6 ? &L.prod[k][0] : rx + (k - 6) * kRRing + q;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a9[k] = __shfl(s, k, 64);
-    if (lane != 0) return;
+            for (int i = 0; i < kRBlk; i += 32) {
+                float4 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const float4*>(p + i + 4 * t);
+                chain16(s, v[0], v[1], v[2], v[3]);
+                chain16(s, v[4], v[5], v[6], v[7]);
+            }
+            r += kRBlk;
+            if (lane == 0) lds_release(&L.R, r);
+            continue;
+        }
+        if (lds_acquire(&L.done)) {
+            const int wf = lds_acquire(&L.W);
+            const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRRing : rx + 2 * kRRing;
+            const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRRing : rx + 2 * kRRing;
+            for (; r < wf; ++r) {
+                const int q = r & (kRRing - 1);
+                s += k >= 6 ? U[q] : U[q] * V[q];
+            }
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return s;
+}
+
+// The refined plane from the nine accumulators (Eigen 3.2 `accu /= n`, then eigen33, A6/A7/A9).
+template <int ORDER, int DIV>
+__device__ float4 refine_plane(float a9[9], int n) {
     const float fn = (float)n;
     if constexpr (DIV == 0) {  // Eigen 3.2: accu /= n  ==>  accu * (1/n)
         const float r = 1.0f / fn;
@@ -696,74 +697,60 @@ __global__ __launch_bounds__(64) void k_cov_eigen(
     float e[3];
     eigen33(cov, e);
     const float d = -1.0f * red4<ORDER>(e[0] * a9[6], e[1] * a9[7], e[2] * a9[8], 0.0f * 1.0f);
-    final_coef[f] = make_float4(e[0], e[1], e[2], d);
+    return make_float4(e[0], e[1], e[2], d);
 }
 
-// Count the final model's inliers per tile.
-template <int ORDER>
-__global__ __launch_bounds__(kBlock) void k_count_final(
+template <int ORDER, int DIV>
+__global__ __launch_bounds__(128) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const float4* __restrict__ final_coef, int n_frames, int tiles_max, float thf,
-    int32_t* __restrict__ tile_counts2) {
-    __shared__ int32_t lds4[kBlock / 64];
-    const int items = n_frames * tiles_max;
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = item / tiles_max, t = item - f * tiles_max;
-        const FrameMeta m = meta[f];
-        if (t >= m.tiles || !st[f].has_model) continue;
-        const int64_t tb = (int64_t)t * kTile;
-        TilePts P;
-        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
-                                                     m.n - tb, final_coef[f], thf, P);
-        int total;
-        (void)block_exscan(__builtin_popcount(bits), lds4, &total);
-        if (threadIdx.x == 0) tile_counts2[(int64_t)f * tiles_max + t] = total;
+    const float4* __restrict__ best_coef, float thf, int32_t* __restrict__ inliers,
+    float4* __restrict__ final_coef, int32_t* __restrict__ n_final) {
+    __shared__ RefineLds L;
+    const int f = blockIdx.x;
+    const FrameState s = st[f];
+    if (!s.has_model) return;
+    const FrameMeta m = meta[f];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const float* xs = X + m.off;
+    const float* ys = Y + m.off;
+    const float* zs = Z + m.off;
+    if (threadIdx.x == 0) {
+        L.W = 0;
+        L.R = 0;
+        L.done = 0;
+        L.coef = best_coef[f];
     }
-}
-
-// Write the final inlier indices (relative to the frame), ascending, via LDS staging.
-template <int ORDER>
-__global__ __launch_bounds__(kBlock) void k_write_final(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const float4* __restrict__ final_coef, const int32_t* __restrict__ offsets, int n_frames,
-    int tiles_max, float thf, int32_t* __restrict__ out) {
-    __shared__ int32_t lds4[kBlock / 64];
-    __shared__ int32_t si[kTile];
-    const int items = n_frames * tiles_max;
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int f = item / tiles_max, t = item - f * tiles_max;
-        const FrameMeta m = meta[f];
-        if (t >= m.tiles || !st[f].has_model) continue;
-        const int64_t tb = (int64_t)t * kTile;
-        TilePts P;
-        const uint32_t bits = tile_predicates<ORDER>(X + m.off + tb, Y + m.off + tb, Z + m.off + tb,
-                                                     m.n - tb, final_coef[f], thf, P);
-        const int c0 = __builtin_popcount(bits & 0xFu), c1 = __builtin_popcount(bits >> 4);
-        int total;
-        const int ex = block_exscan(c0 | (c1 << 16), lds4, &total);
-        int pos[2] = {ex & 0xFFFF, (total & 0xFFFF) + (ex >> 16)};
+    __syncthreads();
+    if (s.need_refine && PITT_REFINE_EXP != 2) {
+        if (wave == 0) {
+            const int total = refine_stream<ORDER, 1>(L, xs, ys, zs, m.n, L.coef, thf, lane, nullptr);
+            if (lane == 0) {
+                L.total = total;
+                lds_release(&L.done, 1);
+            }
+        } else {
+            const float acc = refine_chain(L, lane);
+            float a9[9];
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int li = (int)tb + g * 1024 + threadIdx.x * 4;
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                if ((bits >> (4 * g + s)) & 1u) si[pos[g]++] = li + s;
+            for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
+            if (lane == 0) L.coef = refine_plane<ORDER, DIV>(a9, lds_acquire(&L.W));
         }
         __syncthreads();
-        const int cnt = (total & 0xFFFF) + (total >> 16);
-        const int64_t ob = m.off + offsets[(int64_t)f * (tiles_max + 1) + t];
-        for (int i = threadIdx.x; i < cnt; i += kBlock) out[ob + i] = si[i];
-        __syncthreads();
+    }
+    if (wave != 0 || PITT_REFINE_EXP == 1) return;
+    const float4 c = L.coef;
+    const int nf = refine_stream<ORDER, 2>(L, xs, ys, zs, m.n, c, thf, lane, inliers ? inliers + m.off : nullptr);
+    if (lane == 0) {
+        final_coef[f] = c;
+        n_final[f] = nf;
     }
 }
 
 __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __restrict__ hyp_attempt,
-                           const float4* __restrict__ best_coef, const float4* __restrict__ final_coef,
-                           const int32_t* __restrict__ offsets2, int hcap, int tiles_max,
-                           const FrameMeta* __restrict__ meta, int n_frames,
-                           pitt_plane_result* __restrict__ res) {
+                           const float4* __restrict__ final_coef, const int32_t* __restrict__ n_final,
+                           int hcap, int n_frames, pitt_plane_result* __restrict__ res) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_frames) return;
     const FrameState s = st[f];
@@ -785,13 +772,12 @@ __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __r
         r.coefficients[2] = c.z;
         r.coefficients[3] = c.w;
         r.n_coeff = 4;
-        r.n_inliers = offsets2[(int64_t)f * (tiles_max + 1) + meta[f].tiles];
+        r.n_inliers = n_final[f];
     } else {
         r.coefficients[0] = r.coefficients[1] = r.coefficients[2] = r.coefficients[3] = 0.0f;
         r.n_coeff = 0;
         r.n_inliers = 0;
     }
-    (void)best_coef;
     res[f] = r;
 }
 
@@ -800,30 +786,6 @@ __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __r
 
 template <typename T>
 static T* as(void* p) { return static_cast<T*>(p); }
-
-// Persistent grids of 6 blocks x 4 waves per CU (24 of 32 wave slots): enough loads in flight to
-// saturate HBM, and free slots for the latency-bound k_cov_eigen of a batch on another stream.
-static int grid_items(int64_t items) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(items, 256 * 6));
-}
-
-// k_score's persistent grid: as many waves as the kernel's registers let stay resident (at most 6
-// blocks per CU), each wave a worker -- a block that cannot be resident would run its items after
-// everyone else.
-template <typename K>
-static int score_grid(K kern, int64_t items) {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kBlock, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 4;
-    per_cu = std::min(per_cu, 6);
-    return (int)std::max<int64_t>(1, std::min<int64_t>((items + kWaves - 1) / kWaves, (int64_t)cus * per_cu));
-}
 
 template <int ORDER, int DIV>
 static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
@@ -911,15 +873,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ChunkStat* cstat = as<ChunkStat>(zblock + stat_off);
     float4* best_coef = as<float4>(ctx->buf("best_coef", (size_t)nf * sizeof(float4)));
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
-    int32_t* offs1 = as<int32_t>(ctx->buf("offs1", (size_t)nf * (tiles_max + 1) * 4));
-    int32_t* offs2 = as<int32_t>(ctx->buf("offs2", (size_t)nf * (tiles_max + 1) * 4));
-    int32_t* counts2 = as<int32_t>(ctx->buf("counts2", (size_t)nf * tiles_max * 4));
-    const size_t cap = (size_t)fr->capacity;
-    float* CX = as<float>(ctx->buf("compact", cap * 3 * sizeof(float)));
-    float* CY = CX + cap;
-    float* CZ = CY + cap;
+    int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !CX || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!hyp_coef || !tile_counts || !n_final || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
 
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
@@ -935,9 +891,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         rec = ctx->prof_begin("k_score", 0.0);
         score_recs.push_back(rec);
         auto kern = H <= 64 ? k_score<ORDER, 1> : H <= 128 ? k_score<ORDER, 2> : k_score<ORDER, 4>;
-        hipLaunchKernelGGL(kern, dim3(score_grid(kern, (int64_t)nf * tiles_max)), dim3(kBlock), 0, sm, fr->x, fr->y,
-                           fr->z, meta, hyp_coef, hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H,
-                           thf, tile_counts);
+        const int score_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
+        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, hyp_coef, hcap,
+                           hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
         hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride, tiles_max, h0, H,
@@ -948,35 +904,13 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        p->optimize ? 1 : 0, best_coef, final_coef);
-    if (p->optimize) {
-        rec = ctx->prof_begin("k_tile_offsets", 0.0);
-        hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, tile_counts, hstride, tiles_max,
-                           0, offs1);
-        ctx->prof_end(rec);
-        rec = ctx->prof_begin("k_select_xyz", (double)total_pts * 12.0);
-        hipLaunchKernelGGL((k_select_xyz<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
-                           fr->x, fr->y, fr->z, meta, st, best_coef, offs1, nf, tiles_max, thf, CX, CY, CZ);
-        ctx->prof_end(rec);
-        rec = ctx->prof_begin("k_cov_eigen", 0.0);
-        hipLaunchKernelGGL((k_cov_eigen<ORDER, DIV>), dim3(nf), dim3(64),
-                           (kCovRawFloats + kCovProdFloats) * sizeof(float), sm, meta, st, CX, CY, CZ, nf,
-                           final_coef);
-        ctx->prof_end(rec);
-    }
-    rec = ctx->prof_begin("k_count_final", (double)total_pts * 12.0);
-    hipLaunchKernelGGL((k_count_final<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
-                       fr->x, fr->y, fr->z, meta, st, final_coef, nf, tiles_max, thf, counts2);
+    // refinement (two passes over refined frames, one over the rest) + the final inlier list
+    rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0 * 2.0);
+    hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(128), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+                       thf, inliers_dev, final_coef, n_final);
     ctx->prof_end(rec);
-    hipLaunchKernelGGL(k_tile_offsets, dim3(nf), dim3(kBlock), 0, sm, meta, st, counts2, hcap, tiles_max, 1,
-                       offs2);
-    if (inliers_dev) {
-        rec = ctx->prof_begin("k_write_final", (double)total_pts * 12.0);
-        hipLaunchKernelGGL((k_write_final<ORDER>), dim3(grid_items((int64_t)nf * tiles_max)), dim3(kBlock), 0, sm,
-                           fr->x, fr->y, fr->z, meta, st, final_coef, offs2, nf, tiles_max, thf, inliers_dev);
-        ctx->prof_end(rec);
-    }
-    hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, best_coef,
-                       final_coef, offs2, hcap, tiles_max, meta, nf, dres);
+    hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
+                       hcap, nf, dres);
     PITT_HIP_TRY(hipGetLastError());
     pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
     ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
