@@ -187,6 +187,10 @@ constexpr int kHypBlock = PITT_SCORE_NH;   // hypotheses per LDS coefficient bat
 constexpr int kPts = PITT_SCORE_PTS;       // points per lane per sub-step (4 or 8)
 constexpr int kSub = 64 * kPts;            // points per wave sub-step
 constexpr int kSubs = kTile / kSub;        // sub-steps per item
+#ifndef PITT_SCORE_PF
+#define PITT_SCORE_PF 2
+#endif
+constexpr int kPF = PITT_SCORE_PF;         // sub-steps in flight ahead of the scored one
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 
@@ -198,6 +202,7 @@ struct ScoreItem {
     int64_t base;  // first point of the tile (global)
     int32_t rem;   // points of the frame from the tile start, clamped to kTile
     int32_t f, t;
+    int32_t h;     // hypotheses of this chunk the frame can still need
 };
 
 __device__ __forceinline__ void load_sub(const float* __restrict__ X, const float* __restrict__ Y,
@@ -235,8 +240,14 @@ __device__ __forceinline__ void load_coefs(const float4* __restrict__ hc, int H,
 
 // Item it -> (frame, tile).  Tiles past a shorter frame's end (ragged batches) become empty
 // items on the frame's first tile: every item then issues the same memory operations.
+//
+// Hypotheses per frame: RandomSampleConsensus evaluates hypothesis it only while it < k, and k
+// never grows once a hypothesis has been scored (a larger best count means a smaller k), so past
+// the first chunk the frame needs at most ceil(k) - h0 of this chunk's hypotheses (and no more
+// than it has samples for).  The first chunk is scored whole: k is still the initial 1.0 there.
 __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const int32_t* __restrict__ list,
-                                                  const FrameMeta* __restrict__ meta) {
+                                                  const FrameMeta* __restrict__ meta,
+                                                  const FrameState* __restrict__ st, int h0, int H) {
     ScoreItem r;
     const int li = it / tiles_max;
     const int t = it - li * tiles_max;
@@ -247,6 +258,13 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
     r.rem = ok ? (int32_t)min(m.n - (int64_t)t * kTile, (int64_t)kTile) : 0;
     r.f = f;
     r.t = t;
+    int h = H;
+    if (h0 > 0) {
+        const double k = st[f].k;
+        const int need = k < (double)(h0 + H) ? (int)ceil(k) - h0 : H;  // hypotheses hh < k
+        h = max(0, min(h, min(need, st[f].n_avail - h0)));
+    }
+    r.h = __builtin_amdgcn_readfirstlane(h);
     return r;
 }
 
@@ -334,11 +352,11 @@ __device__ __forceinline__ void put_coefs(float4* cl, const CoefRegs<NST>& C, in
 // conditional (the prologue stores NST dummy rows into the padding), so every s_waitcnt the
 // compiler places is an exact vmcnt(N) that leaves the prefetched sub-step in flight.
 template <int ORDER, int NST>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 ? 4 : 6, NST >= 4 ? 4 : 8))) void k_score(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 || kPts > 4 ? 4 : 6, NST >= 4 || kPts > 4 ? 5 : 8))) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const FrameMeta* __restrict__ meta, const float4* __restrict__ hyp_coef, int hcap, int hstride,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max, int h0, int H,
-    float thf, int32_t* __restrict__ tile_counts) {
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
+    int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
+    int h0, int H, float thf, int32_t* __restrict__ tile_counts) {
     __shared__ float4 wcoef[kWaves][NST * 64];
     __shared__ int32_t wcnt[kWaves][NST * 64];
     const int lane = threadIdx.x & 63;
@@ -350,22 +368,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4
     int32_t* wc = wcnt[w];
     float tv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
-    const ScoreItem cur = resolve_item(it, tiles_max, list, meta);
-    SubPts A, B;
+    const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H);
+    const int Hf = cur.h;
+    // kPF sub-steps in flight ahead of the one being scored (rotating register sets): k_score is
+    // VALU-bound alone, but beside other streams' k_refine the memory latency grows and a single
+    // sub-step of look-ahead leaves the VALU waiting
+    SubPts P[kPF + 1];
     CoefRegs<NST> C;
-    load_sub(X, Y, Z, cur.base, lane, A);
+    load_sub(X, Y, Z, cur.base, lane, P[0]);
     load_coefs<NST>(hyp_coef + (int64_t)cur.f * hcap + h0, H, lane, C);
-    load_sub(X, Y, Z, cur.base + kSub, lane, B);
-    put_coefs<NST>(cl, C, lane);
-    score_sub<ORDER, true>(cl, H, A, cur.rem, tv, lane, wc);
 #pragma unroll
-    for (int s = 1; s + 2 < kSubs; s += 2) {
-        load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, A);
-        score_sub<ORDER, false>(cl, H, B, cur.rem - s * kSub, tv, lane, wc);
-        load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, B);
-        score_sub<ORDER, false>(cl, H, A, cur.rem - (s + 1) * kSub, tv, lane, wc);
+    for (int s = 1; s <= kPF; ++s) load_sub(X, Y, Z, cur.base + s * kSub, lane, P[s]);
+    put_coefs<NST>(cl, C, lane);
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s) {
+        if (s > 0 && s + kPF < kSubs) load_sub(X, Y, Z, cur.base + (s + kPF) * kSub, lane, P[(s + kPF) % (kPF + 1)]);
+        if (s == 0) score_sub<ORDER, true>(cl, Hf, P[0], cur.rem, tv, lane, wc);
+        else score_sub<ORDER, false>(cl, Hf, P[s % (kPF + 1)], cur.rem - s * kSub, tv, lane, wc);
     }
-    score_sub<ORDER, false>(cl, H, B, cur.rem - (kSubs - 1) * kSub, tv, lane, wc);
     store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
 }
 
@@ -847,8 +867,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
 
     // --- chunk schedule (geometric after the first few HBM-bound 16-hypothesis passes) ---
     std::vector<int> chunks;
+#ifndef PITT_FIRST_CHUNK
+#define PITT_FIRST_CHUNK 16
+#endif
     for (int h0 = 0, i = 0; h0 < hcap; ++i) {
-        int H = i < 4 ? 16 : std::min(kMaxScoreChunk, 16 << (i - 3));
+        int H = i == 0 ? PITT_FIRST_CHUNK : i < 4 ? 16 : std::min(kMaxScoreChunk, 16 << (i - 3));
         H = std::min(H, hcap - h0);
         chunks.push_back(H);
         h0 += H;
@@ -892,8 +915,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         score_recs.push_back(rec);
         auto kern = H <= 64 ? k_score<ORDER, 1> : H <= 128 ? k_score<ORDER, 2> : k_score<ORDER, 4>;
         const int score_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
-        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, hyp_coef, hcap,
-                           hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts);
+        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
+                           hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
         hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride, tiles_max, h0, H,

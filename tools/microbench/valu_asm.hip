@@ -11,6 +11,7 @@
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k(float* out, long long* clk, float s0, int iters) {
+    (void)s0;
     float v0 = threadIdx.x, v1 = v0 + 1, v2 = v0 + 2, v3 = v0 + 3, v4 = v0 + 4, v5 = v0 + 5, v6 = v0 + 6, v7 = v0 + 7;
     const long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; ++it) {
@@ -66,6 +67,42 @@ __global__ __launch_bounds__(256) void k(float* out, long long* clk, float s0, i
                          : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7)
                          : "v"(s0)
                          : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "scc");
+        else if constexpr (MODE == 9)  // one fully dependent chain (latency)
+            asm volatile(R32("v_add_f32 %0, %0, %1\n v_add_f32 %0, %0, %2\n v_add_f32 %0, %0, %3\n v_add_f32 %0, %0, %4\n"
+                             "v_add_f32 %0, %0, %5\n v_add_f32 %0, %0, %6\n v_add_f32 %0, %0, %7\n v_add_f32 %0, %0, %1\n")
+                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7));
+        else if constexpr (MODE == 10)  // two interleaved dependent chains
+            asm volatile(R32("v_add_f32 %0, %0, %2\n v_add_f32 %1, %1, %3\n v_add_f32 %0, %0, %4\n v_add_f32 %1, %1, %5\n"
+                             "v_add_f32 %0, %0, %6\n v_add_f32 %1, %1, %7\n v_add_f32 %0, %0, %2\n v_add_f32 %1, %1, %3\n")
+                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7));
+        else if constexpr (MODE == 11)  // v_mul_f32_dpp row_newbcast (src0 broadcast), independent
+            asm volatile(R32("v_mul_f32_dpp %0, %8, %0 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %1, %8, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %2, %8, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %3, %8, %3 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %4, %8, %4 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %5, %8, %5 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %6, %8, %6 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+                             "v_mul_f32_dpp %7, %8, %7 row_newbcast:8 row_mask:0xf bank_mask:0xf\n")
+                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7)
+                         : "v"(s0));
+        else if constexpr (MODE == 12)  // dpp k_score mix: 3 mul_dpp + add + add_dpp + add + cmp(e64, v)
+            asm volatile(R8("v_mul_f32_dpp %0, %8, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+                            "v_mul_f32_dpp %2, %8, %3 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+                            "v_mul_f32_dpp %4, %8, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+                            "v_add_f32 %6, %0, %4\n"
+                            "v_add_f32_dpp %7, %8, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+                            "v_add_f32 %6, %6, %7\n v_cmp_lt_f32_e64 s[40:41], |%6|, %8\n"
+                            "v_mul_f32_dpp %1, %8, %0 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+                            "v_mul_f32_dpp %3, %8, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+                            "v_mul_f32_dpp %5, %8, %4 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+                            "v_add_f32 %7, %1, %5\n"
+                            "v_add_f32_dpp %6, %8, %3 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_add_f32 %7, %7, %6\n v_cmp_lt_f32_e64 s[42:43], |%7|, %8\n"
+                            "s_bcnt1_i32_b64 s44, s[40:41]\n s_bcnt1_i32_b64 s45, s[42:43]\n s_add_u32 s46, s44, s45\n")
+                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7)
+                         : "v"(s0)
+                         : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "scc");
         else if constexpr (MODE == 5)  // mixed: 3 mul(s,v) + 3 add + cmp, like k_score, 8-way independent
             asm volatile(R8("v_mul_f32 %0, %8, %1\n v_mul_f32 %2, %8, %3\n v_mul_f32 %4, %8, %5\n v_add_f32 %6, %0, %2\n"
                             "v_add_f32 %7, %8, %4\n v_add_f32 %6, %6, %7\n v_cmp_lt_f32_e64 s[40:41], |%6|, %8\n"
@@ -93,8 +130,11 @@ int main() {
     const int iters = 2000;
     const char* names[] = {"v_add_f32 v,v", "v_mul_f32 s,v", "v_cmp_lt_f32_e64 |v|,s", "v_mul_f32 v,v",
                            "v_cmp_lt_f32_e64 |v|,v", "k_score mix (16 incl 2 v_nop)", "v_mov_b32 v,s",
-                           "v_cmp_gt_e32 vcc,v,v + s_bcnt (per cmp)", "all-VGPR mix (14 VALU + 3 SALU)"};
-    for (int mode = 0; mode < 9; ++mode) {
+                           "v_cmp_gt_e32 vcc,v,v + s_bcnt (per cmp)", "all-VGPR mix (14 VALU + 3 SALU)",
+                           "dependent v_add chain", "2 interleaved dependent chains", "v_mul_f32_dpp row_newbcast",
+                           "dpp k_score mix (14 VALU + 3 SALU)"};
+    for (int mode = 0; mode < 13; ++mode) {
+        if (mode != 3 && mode != 8 && mode < 11) continue;
         for (int wpe : {1, 4, 8}) {
             const int blocks = 256 * wpe;
             float ms = 0;
@@ -111,13 +151,17 @@ int main() {
                     case 6: hipLaunchKernelGGL(k<6>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
                     case 7: hipLaunchKernelGGL(k<7>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
                     case 8: hipLaunchKernelGGL(k<8>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
+                    case 9: hipLaunchKernelGGL(k<9>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
+                    case 10: hipLaunchKernelGGL(k<10>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
+                    case 11: hipLaunchKernelGGL(k<11>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
+                    case 12: hipLaunchKernelGGL(k<12>, dim3(blocks), dim3(256), 0, 0, out, clk, 0.999f, iters); break;
                 }
                 (void)hipEventRecord(e1);
                 (void)hipEventSynchronize(e1);
                 (void)hipEventElapsedTime(&ms, e0, e1);
                 (void)hipMemcpy(&c, clk + mode, 8, hipMemcpyDeviceToHost);
             }
-            const double per_wave = (mode == 5) ? iters * 8.0 * 16 : (mode == 8) ? iters * 8.0 * 14 : (mode == 7) ? iters * 32.0 * 4 : iters * 32.0 * 8;
+            const double per_wave = (mode == 5) ? iters * 8.0 * 16 : (mode == 8 || mode == 12) ? iters * 8.0 * 14 : (mode == 7) ? iters * 32.0 * 4 : iters * 32.0 * 8;
             const double per_simd = per_wave * blocks * 4 / 1024.0;
             printf("%-30s waves/SIMD %d: %8.3f ms  %.3f ns/instr/SIMD  memtime %lld ticks/wave (%.1f ticks/instr/wave)\n",
                    names[mode], wpe, ms, ms * 1e6 / per_simd, c, c / per_wave);
