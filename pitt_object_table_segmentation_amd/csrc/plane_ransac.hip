@@ -188,7 +188,7 @@ constexpr int kPts = PITT_SCORE_PTS;       // points per lane per sub-step (4 or
 constexpr int kSub = 64 * kPts;            // points per wave sub-step
 constexpr int kSubs = kTile / kSub;        // sub-steps per item
 #ifndef PITT_SCORE_PF
-#define PITT_SCORE_PF 2
+#define PITT_SCORE_PF 1
 #endif
 constexpr int kPF = PITT_SCORE_PF;         // sub-steps in flight ahead of the scored one
 constexpr int kWaves = kBlock / 64;
@@ -351,12 +351,14 @@ __device__ __forceinline__ void put_coefs(float4* cl, const CoefRegs<NST>& C, in
 // NST coefficient loads with the next item's first sub-step, NST count stores -- with nothing
 // conditional (the prologue stores NST dummy rows into the padding), so every s_waitcnt the
 // compiler places is an exact vmcnt(N) that leaves the prefetched sub-step in flight.
-template <int ORDER, int NST>
+// BOX (the first chunk only): also record each tile's bounding box -- IEEE min/max skip NaN
+// points; the out-of-frame tail of the last tile only widens it -- for k_refine's tile skipping.
+template <int ORDER, int NST, bool BOX>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 || kPts > 4 ? 4 : 6, NST >= 4 || kPts > 4 ? 5 : 8))) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
-    int h0, int H, float thf, int32_t* __restrict__ tile_counts) {
+    int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box) {
     __shared__ float4 wcoef[kWaves][NST * 64];
     __shared__ int32_t wcnt[kWaves][NST * 64];
     const int lane = threadIdx.x & 63;
@@ -380,13 +382,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4
 #pragma unroll
     for (int s = 1; s <= kPF; ++s) load_sub(X, Y, Z, cur.base + s * kSub, lane, P[s]);
     put_coefs<NST>(cl, C, lane);
+    float bx[6] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
         if (s > 0 && s + kPF < kSubs) load_sub(X, Y, Z, cur.base + (s + kPF) * kSub, lane, P[(s + kPF) % (kPF + 1)]);
+        if constexpr (BOX) {
+            const SubPts& Q = P[s % (kPF + 1)];
+#pragma unroll
+            for (int q = 0; q < kPts; ++q) {
+                bx[0] = fminf(bx[0], Q.x[q]);
+                bx[1] = fminf(bx[1], Q.y[q]);
+                bx[2] = fminf(bx[2], Q.z[q]);
+                bx[3] = fmaxf(bx[3], Q.x[q]);
+                bx[4] = fmaxf(bx[4], Q.y[q]);
+                bx[5] = fmaxf(bx[5], Q.z[q]);
+            }
+            // keep the update here: sunk to the end, it would hold every sub-step's points live
+            asm volatile("" ::"v"(bx[0]), "v"(bx[1]), "v"(bx[2]), "v"(bx[3]), "v"(bx[4]), "v"(bx[5]));
+        }
         if (s == 0) score_sub<ORDER, true>(cl, Hf, P[0], cur.rem, tv, lane, wc);
         else score_sub<ORDER, false>(cl, Hf, P[s % (kPF + 1)], cur.rem - s * kSub, tv, lane, wc);
     }
     store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
+    if constexpr (BOX) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                bx[k] = fminf(bx[k], __shfl_xor(bx[k], off, 64));
+                bx[k + 3] = fmaxf(bx[k + 3], __shfl_xor(bx[k + 3], off, 64));
+            }
+        }
+        float v = bx[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k) v = lane == k ? bx[k] : v;
+        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = v;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -498,12 +529,71 @@ constexpr int kRRing = 1024;   // compacted-inlier ring (points): 3 * kRRing flo
 constexpr int kRDepth2 = kRDepth1 + 3 * kRRing / kRSlot;  // pass 2: the whole pool is raw ring
 constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
 
+constexpr int kRMaxTiles = 1024;             // tile list capacity (frames up to 2M points)
+constexpr int kRStepsPerTile = kTile / kRChunk;
+
 struct RefineLds {
     float pool[kRDepth2 * kRSlot];  // pass 1: raw[kRDepth1] | cx | cy | cz;  pass 2: raw[kRDepth2]
     float prod[6][kRBlk];           // xx, xy, xz, yy, yz, zz of the current chain block
+    int tl[kRMaxTiles];             // the pass's tiles that can hold inliers, ascending
     int W, R, done, total;
     float4 coef;
 };
+
+// True when no point in the tile's bounding box can satisfy |d| < thf for plane c: the extremes of
+// the exact plane value over the box (double) clear the threshold by more than any rounding of
+// PCL's float evaluation (<= 4 ulp of |a x| + |b y| + |c z| + |w|; the margin is 1e-5 of it).
+// An empty box (no finite point) holds no inliers; boxes with infinities never clear.
+__device__ __forceinline__ bool box_misses_slab(const float* __restrict__ b, float4 c, float thf) {
+    const double lo[3] = {b[0], b[1], b[2]}, hi[3] = {b[3], b[4], b[5]};
+    if (!(lo[0] <= hi[0])) return true;
+    const double cc[3] = {c.x, c.y, c.z};
+    double dmin = c.w, dmax = c.w, sc = fabs((double)c.w);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double a = cc[k] * lo[k], z = cc[k] * hi[k];
+        dmin += fmin(a, z);
+        dmax += fmax(a, z);
+        sc += fabs(cc[k]) * fmax(fabs(lo[k]), fabs(hi[k]));
+    }
+    const double lim = (double)thf + 1e-5 * sc + 1e-30;
+    return dmin > lim || dmax < -lim;
+}
+
+// The pass's tile list in LDS (ascending).  Pass 1: tiles where the winning hypothesis counted
+// inliers during scoring (exact).  Pass 2: tiles whose box meets the refined plane's slab.
+// Returns the number of tiles, or -1 (stream every tile) for frames beyond the list's capacity.
+template <int PASS>
+__device__ __forceinline__ int refine_tiles(RefineLds& L, int tiles, int lane, float4 c, float thf,
+                                            const int32_t* __restrict__ best_counts, int hstride,
+                                            const float* __restrict__ box) {
+    if (tiles > kRMaxTiles) return -1;
+    int nact = 0;
+    for (int g = 0; g < tiles; g += 64) {
+        const int t = g + lane;
+        bool act = false;
+        if (t < tiles) {
+            if constexpr (PASS == 1) act = best_counts[(int64_t)t * hstride] > 0;
+            else act = !box_misses_slab(box + (int64_t)t * 8, c, thf);
+        }
+        const uint64_t b = __builtin_amdgcn_ballot_w64(act);
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (act) L.tl[nact + pre] = t;
+        nact += __builtin_popcountll(b);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return nact;
+}
+
+// Step s of the pass -> step of the frame.  The list is read in asm: a visible LDS read would make
+// the compiler wait for the ring's in-flight global_load_lds writes.
+__device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact) {
+    if (nact < 0) return s;
+    const uint32_t a = (uint32_t)(uintptr_t)&L.tl[s / kRStepsPerTile];
+    int t;
+    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(a) : "memory");
+    return __builtin_amdgcn_readfirstlane(t) * kRStepsPerTile + s % kRStepsPerTile;
+}
 
 __device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth1 * kRSlot; }
 
@@ -528,10 +618,10 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
 // Step c of the frame into ring slot c % DEPTH; steps past the end re-read the last step so that
 // every iteration issues the same three loads (the waits below are fixed vmcnt counts).
 template <int DEPTH>
-__device__ __forceinline__ void refine_issue(float* raw, const float* xs, const float* ys, const float* zs,
-                                             int c, int nch, int lane) {
+__device__ __forceinline__ void refine_issue(RefineLds& L, float* raw, const float* xs, const float* ys,
+                                             const float* zs, int c, int nsteps, int nact, int lane) {
     typedef __attribute__((address_space(3))) void* lds_ptr;
-    const int cc = min(c, nch - 1);
+    const int cc = refine_step(L, min(c, nsteps - 1), nact);
     float* b = raw + (c % DEPTH) * kRSlot;
     const int64_t o = (int64_t)cc * kRChunk + lane * 4;
     __builtin_amdgcn_global_load_lds(xs + o, (lds_ptr)(b), 16, 0, 0);
@@ -543,23 +633,25 @@ __device__ __forceinline__ void refine_issue(float* raw, const float* xs, const 
 // LDS ring for the consumer; PASS 2 writes their indices to out (when given).  Returns the count.
 template <int ORDER, int PASS>
 __device__ __forceinline__ int refine_stream(RefineLds& L, const float* xs, const float* ys, const float* zs, int64_t n,
-                             float4 c, float thf, int lane, int32_t* __restrict__ out) {
+                             float4 c, float thf, int lane, int32_t* __restrict__ out, int nact) {
     constexpr int DEPTH = PASS == 1 ? kRDepth1 : kRDepth2;
-    const int nch = (int)((n + kRChunk - 1) / kRChunk);
+    const int nsteps = nact < 0 ? (int)((n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+    int wpos = 0;
+    if (nsteps == 0) return 0;
     float* raw = L.pool;
     float* rx = ring_x(L);
     asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));  // plane in registers before the ring starts
 #pragma unroll
-    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(raw, xs, ys, zs, k, nch, lane);
-    int wpos = 0;
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(L, raw, xs, ys, zs, k, nsteps, nact, lane);
+    for (int st = 0; st < nsteps; ++st) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot refilled next are done
-        refine_issue<DEPTH>(raw, xs, ys, zs, ch + DEPTH - 1, nch, lane);
+        refine_issue<DEPTH>(L, raw, xs, ys, zs, st + DEPTH - 1, nsteps, nact, lane);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");  // step ch landed
         __builtin_amdgcn_sched_barrier(0);
         // the slot's reads in asm: the compiler treats any LDS read as aliasing the ring's
         // in-flight global_load_lds writes and would wait for all of them (vmcnt(0))
-        const uint32_t b = (uint32_t)(uintptr_t)(raw + (ch % DEPTH) * kRSlot + lane * 4);
+        const int ch = refine_step(L, st, nact);  // the frame's step
+        const uint32_t b = (uint32_t)(uintptr_t)(raw + (st % DEPTH) * kRSlot + lane * 4);
         float4 x4, y4, z4;
         asm volatile(
             "ds_read_b128 %0, %3\n"
@@ -724,7 +816,8 @@ template <int ORDER, int DIV>
 __global__ __launch_bounds__(128) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
-    const float4* __restrict__ best_coef, float thf, int32_t* __restrict__ inliers,
+    const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
+    int tiles_max, const float* __restrict__ tile_box, int32_t* __restrict__ inliers,
     float4* __restrict__ final_coef, int32_t* __restrict__ n_final) {
     __shared__ RefineLds L;
     const int f = blockIdx.x;
@@ -745,7 +838,10 @@ __global__ __launch_bounds__(128) void k_refine(
     __syncthreads();
     if (s.need_refine && PITT_REFINE_EXP != 2) {
         if (wave == 0) {
-            const int total = refine_stream<ORDER, 1>(L, xs, ys, zs, m.n, L.coef, thf, lane, nullptr);
+            const float4 cb = L.coef;
+            const int nact = refine_tiles<1>(L, m.tiles, lane, cb, thf,
+                                             tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride, nullptr);
+            const int total = refine_stream<ORDER, 1>(L, xs, ys, zs, m.n, cb, thf, lane, nullptr, nact);
             if (lane == 0) {
                 L.total = total;
                 lds_release(&L.done, 1);
@@ -761,7 +857,8 @@ __global__ __launch_bounds__(128) void k_refine(
     }
     if (wave != 0 || PITT_REFINE_EXP == 1) return;
     const float4 c = L.coef;
-    const int nf = refine_stream<ORDER, 2>(L, xs, ys, zs, m.n, c, thf, lane, inliers ? inliers + m.off : nullptr);
+    const int nact = refine_tiles<2>(L, m.tiles, lane, c, thf, nullptr, 0, tile_box + (int64_t)f * tiles_max * 8);
+    const int nf = refine_stream<ORDER, 2>(L, xs, ys, zs, m.n, c, thf, lane, inliers ? inliers + m.off : nullptr, nact);
     if (lane == 0) {
         final_coef[f] = c;
         n_final[f] = nf;
@@ -897,8 +994,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* best_coef = as<float4>(ctx->buf("best_coef", (size_t)nf * sizeof(float4)));
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
     int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
+    float* tile_box = as<float>(ctx->buf("tile_box", (size_t)nf * tiles_max * 8 * sizeof(float)));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !n_final || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
 
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
@@ -913,10 +1011,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int H = chunks[(size_t)c];
         rec = ctx->prof_begin("k_score", 0.0);
         score_recs.push_back(rec);
-        auto kern = H <= 64 ? k_score<ORDER, 1> : H <= 128 ? k_score<ORDER, 2> : k_score<ORDER, 4>;
+        auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
+                           : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
         const int score_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
-                           hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts);
+                           hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
+                           tile_box);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
         hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride, tiles_max, h0, H,
@@ -930,7 +1030,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     // refinement (two passes over refined frames, one over the rest) + the final inlier list
     rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0 * 2.0);
     hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(128), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                       thf, inliers_dev, final_coef, n_final);
+                       thf, tile_counts, hstride, tiles_max, tile_box, inliers_dev, final_coef, n_final);
     ctx->prof_end(rec);
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
