@@ -585,14 +585,26 @@ __device__ __forceinline__ int refine_tiles(RefineLds& L, int tiles, int lane, f
     return nact;
 }
 
-// Step s of the pass -> step of the frame.  The list is read in asm: a visible LDS read would make
-// the compiler wait for the ring's in-flight global_load_lds writes.
-__device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact) {
+// Step s of the pass -> step of the frame, through a cursor that reads the tile list once per tile
+// (tile: the list position it holds; base: that tile's first frame step).  The list is read in
+// asm: a visible LDS read would make the compiler wait for the ring's in-flight global_load_lds
+// writes.
+struct StepCursor {
+    int tile = -1;
+    int base = 0;
+};
+
+__device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact, StepCursor& cur) {
     if (nact < 0) return s;
-    const uint32_t a = (uint32_t)(uintptr_t)&L.tl[s / kRStepsPerTile];
-    int t;
-    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(a) : "memory");
-    return __builtin_amdgcn_readfirstlane(t) * kRStepsPerTile + s % kRStepsPerTile;
+    const int ti = s / kRStepsPerTile;
+    if (ti != cur.tile) {
+        const uint32_t a = (uint32_t)(uintptr_t)&L.tl[ti];
+        int t;
+        asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(a) : "memory");
+        cur.tile = ti;
+        cur.base = __builtin_amdgcn_readfirstlane(t) * kRStepsPerTile;
+    }
+    return cur.base + s % kRStepsPerTile;
 }
 
 __device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth1 * kRSlot; }
@@ -615,14 +627,15 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
     asm volatile("" ::: "memory");
 }
 
-// Step c of the frame into ring slot c % DEPTH; steps past the end re-read the last step so that
-// every iteration issues the same three loads (the waits below are fixed vmcnt counts).
+// Pass step c into ring slot (c - sb) % DEPTH; steps past the range [sb, se) re-read its last step
+// so that every iteration issues the same three loads (the waits below are fixed vmcnt counts).
 template <int DEPTH>
 __device__ __forceinline__ void refine_issue(RefineLds& L, float* raw, const float* xs, const float* ys,
-                                             const float* zs, int c, int nsteps, int nact, int lane) {
+                                             const float* zs, int c, int sb, int se, int nact, int lane,
+                                             StepCursor& cur) {
     typedef __attribute__((address_space(3))) void* lds_ptr;
-    const int cc = refine_step(L, min(c, nsteps - 1), nact);
-    float* b = raw + (c % DEPTH) * kRSlot;
+    const int cc = refine_step(L, min(c, se - 1), nact, cur);
+    float* b = raw + ((c - sb) % DEPTH) * kRSlot;
     const int64_t o = (int64_t)cc * kRChunk + lane * 4;
     __builtin_amdgcn_global_load_lds(xs + o, (lds_ptr)(b), 16, 0, 0);
     __builtin_amdgcn_global_load_lds(ys + o, (lds_ptr)(b + kRChunk), 16, 0, 0);
@@ -631,27 +644,42 @@ __device__ __forceinline__ void refine_issue(RefineLds& L, float* raw, const flo
 
 // Producer: one pass over the frame with plane c.  PASS 1 appends the inliers' coordinates to the
 // LDS ring for the consumer; PASS 2 writes their indices to out (when given).  Returns the count.
-template <int ORDER, int PASS>
-__device__ __forceinline__ int refine_stream(RefineLds& L, const float* xs, const float* ys, const float* zs, int64_t n,
-                             float4 c, float thf, int lane, int32_t* __restrict__ out, int nact) {
-    constexpr int DEPTH = PASS == 1 ? kRDepth1 : kRDepth2;
-    const int nsteps = nact < 0 ? (int)((n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+// OUT (pass 2 with an output buffer): every step issues exactly four index stores -- lanes without
+// an inlier for a store write to their own slot of `dummy` -- so the step's vector-memory ops are a
+// fixed count and the ring's wait can count them (stores share vmcnt with the loads: uncounted,
+// they would cut the look-ahead to a few steps).
+template <int ORDER, int PASS, bool OUT, int DEPTH>
+__device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const float* xs, const float* ys,
+                                             const float* zs, int64_t n, float4 c, float thf, int lane,
+                                             int32_t* __restrict__ out, int32_t* __restrict__ dummy, int nact,
+                                             int sb, int se) {
     int wpos = 0;
-    if (nsteps == 0) return 0;
-    float* raw = L.pool;
+    if (se <= sb) return 0;
     float* rx = ring_x(L);
+    float tv;  // threshold and plane in VGPRs: a VALU op reading an SGPR issues at half rate
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
     asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));  // plane in registers before the ring starts
+    StepCursor ic, pc;  // issue and process cursors
 #pragma unroll
-    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(L, raw, xs, ys, zs, k, nsteps, nact, lane);
-    for (int st = 0; st < nsteps; ++st) {
+    for (int k = 0; k < DEPTH - 1; ++k) {
+        refine_issue<DEPTH>(L, raw, xs, ys, zs, sb + k, sb, se, nact, lane, ic);
+        if constexpr (OUT) {  // the 4 stores a processed step would issue: the count stays exact
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // volatile: not elided; global address space: not a flat store
+                *(__attribute__((address_space(1))) volatile int32_t*)(dummy + lane) = q;
+        }
+    }
+    for (int st = sb; st < se; ++st) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot refilled next are done
-        refine_issue<DEPTH>(L, raw, xs, ys, zs, st + DEPTH - 1, nsteps, nact, lane);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");  // step ch landed
+        refine_issue<DEPTH>(L, raw, xs, ys, zs, st + DEPTH - 1, sb, se, nact, lane, ic);
+        // step st landed: younger are the DEPTH - 1 steps issued since (3 loads each) and, with
+        // OUT, the 4 stores of each of the DEPTH - 1 steps processed since it was issued
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((OUT ? 7 : 3) * (DEPTH - 1)) : "memory");
         __builtin_amdgcn_sched_barrier(0);
         // the slot's reads in asm: the compiler treats any LDS read as aliasing the ring's
         // in-flight global_load_lds writes and would wait for all of them (vmcnt(0))
-        const int ch = refine_step(L, st, nact);  // the frame's step
-        const uint32_t b = (uint32_t)(uintptr_t)(raw + (st % DEPTH) * kRSlot + lane * 4);
+        const int ch = refine_step(L, st, nact, pc);  // the frame's step
+        const uint32_t b = (uint32_t)(uintptr_t)(raw + ((st - sb) % DEPTH) * kRSlot + lane * 4);
         float4 x4, y4, z4;
         asm volatile(
             "ds_read_b128 %0, %3\n"
@@ -661,16 +689,21 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, const float* xs, cons
             : "=&v"(x4), "=&v"(y4), "=&v"(z4)
             : "v"(b)
             : "memory");
-        const float px[4] = {x4.x, x4.y, x4.z, x4.w};
+        float px[4] = {x4.x, x4.y, x4.z, x4.w};
         const float py[4] = {y4.x, y4.y, y4.z, y4.w};
         const float pz[4] = {z4.x, z4.y, z4.z, z4.w};
-        const int64_t p0 = (int64_t)ch * kRChunk + lane * 4;
+        const int64_t s0 = (int64_t)ch * kRChunk;
+        const int p0 = lane * 4;  // point of the step
+        if (s0 + kRChunk > n) {  // the frame's last step: points past its end never count
+            const int lim = (int)(n - s0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (p0 + q >= lim) px[q] = __builtin_nanf("");
+        }
         uint32_t bits = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = (p0 + q < n) && (fabsf(plane_dot<ORDER>(c, px[q], py[q], pz[q])) < thf);
-            bits |= (in ? 1u : 0u) << q;
-        }
+        for (int q = 0; q < 4; ++q)
+            bits |= (fabsf(plane_dot<ORDER>(c, px[q], py[q], pz[q])) < tv ? 1u : 0u) << q;
         // ascending positions: exclusive prefix of the per-lane counts (0..4) from their bit slices
         const int cnt = __builtin_popcount(bits);
         const uint64_t b0 = __builtin_amdgcn_ballot_w64((cnt & 1) != 0);
@@ -698,11 +731,16 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, const float* xs, cons
             (void)k;
             if (lane == 0) lds_release(&L.W, wpos + tot);
         } else {
-            if (out) {
+            if constexpr (OUT) {
                 int k = wpos + pre;
+                const int32_t i0 = (int32_t)s0 + p0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if ((bits >> q) & 1u) out[k++] = (int32_t)(p0 + q);
+                for (int q = 0; q < 4; ++q) {
+                    const bool in = (bits >> q) & 1u;
+                    int32_t* dst = in ? out + k : dummy + lane;
+                    *dst = i0 + q;
+                    k += in ? 1 : 0;
+                }
             }
         }
         wpos += tot;
@@ -817,7 +855,7 @@ __global__ __launch_bounds__(128) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
-    int tiles_max, const float* __restrict__ tile_box, int32_t* __restrict__ inliers,
+    int tiles_max, const float* __restrict__ tile_box, int32_t* __restrict__ inliers, int32_t* __restrict__ dummy,
     float4* __restrict__ final_coef, int32_t* __restrict__ n_final) {
     __shared__ RefineLds L;
     const int f = blockIdx.x;
@@ -841,7 +879,9 @@ __global__ __launch_bounds__(128) void k_refine(
             const float4 cb = L.coef;
             const int nact = refine_tiles<1>(L, m.tiles, lane, cb, thf,
                                              tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride, nullptr);
-            const int total = refine_stream<ORDER, 1>(L, xs, ys, zs, m.n, cb, thf, lane, nullptr, nact);
+            const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+            const int total = refine_stream<ORDER, 1, false, kRDepth1>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane,
+                                                                        nullptr, nullptr, nact, 0, nsteps);
             if (lane == 0) {
                 L.total = total;
                 lds_release(&L.done, 1);
@@ -856,12 +896,19 @@ __global__ __launch_bounds__(128) void k_refine(
         __syncthreads();
     }
     if (wave != 0 || PITT_REFINE_EXP == 1) return;
+    // pass 2 (one wave: the ring depth, not the per-step work, bounds it -- two waves with half a
+    // ring each were slower)
     const float4 c = L.coef;
     const int nact = refine_tiles<2>(L, m.tiles, lane, c, thf, nullptr, 0, tile_box + (int64_t)f * tiles_max * 8);
-    const int nf = refine_stream<ORDER, 2>(L, xs, ys, zs, m.n, c, thf, lane, inliers ? inliers + m.off : nullptr, nact);
+    const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+    const int cnt = inliers ? refine_stream<ORDER, 2, true, kRDepth2>(L, L.pool, xs, ys, zs, m.n, c, thf, lane,
+                                                                      inliers + m.off, dummy + (int64_t)f * 64, nact,
+                                                                      0, nsteps)
+                            : refine_stream<ORDER, 2, false, kRDepth2>(L, L.pool, xs, ys, zs, m.n, c, thf, lane,
+                                                                       nullptr, nullptr, nact, 0, nsteps);
     if (lane == 0) {
         final_coef[f] = c;
-        n_final[f] = nf;
+        n_final[f] = cnt;
     }
 }
 
@@ -995,8 +1042,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
     int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
     float* tile_box = as<float>(ctx->buf("tile_box", (size_t)nf * tiles_max * 8 * sizeof(float)));
+    int32_t* refine_dummy = as<int32_t>(ctx->buf("refine_dummy", (size_t)nf * 64 * 4));  // k_refine's sink
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !refine_dummy || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
 
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
@@ -1030,7 +1078,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     // refinement (two passes over refined frames, one over the rest) + the final inlier list
     rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0 * 2.0);
     hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(128), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                       thf, tile_counts, hstride, tiles_max, tile_box, inliers_dev, final_coef, n_final);
+                       thf, tile_counts, hstride, tiles_max, tile_box, inliers_dev, refine_dummy, final_coef, n_final);
     ctx->prof_end(rec);
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
