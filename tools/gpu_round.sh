@@ -9,5 +9,5 @@ timeout -k 10 1200 python -m pytest tests -m gpu -q --timeout 600 -p no:cachepro
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 exit $rc
