@@ -160,42 +160,35 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
 }
 
 // ------------------------------------------------------------------------------------------
-// k_score: one wave per (active frame, 2048-point tile) item, 4 waves per block, one block per 4
-// items (the grid covers every frame's tiles; waves past the active items exit at once).  A wave
-// walks its item in kSubs sub-steps of 64 * kPts points (kPts per lane: float4s of each coordinate
-// plane), the next sub-step already loading into a second register set while the current one is
-// scored.  (A persistent grid of wave workers was tried: with other streams' kernels holding part
-// of the CUs, blocks that become resident late carry their whole share after everyone else, and a
-// global atomic work counter serialises at ~5 ns per grab.)
+// k_score: inlier counts of the chunk's hypotheses per (active frame, 2048-point tile), one wave
+// per item, 4 waves per block, one block per 4 items (the grid covers every frame's tiles; waves
+// past the active items exit at once).  The wave walks its tile in kSubs sub-steps of kGPS groups
+// of 64 points; lane l holds point 64 g + l of group g, so one VALU instruction covers exactly one
+// group and a (group, hypothesis) pair can be skipped as a whole.  Per sub-step:
 //
-// Per point-hypothesis: 3 mul + 3 add + 1 cmp on the VALU (no FMA: PCL's rounding), the count on
-// the scalar unit (ballot -> s_bcnt1).  Every VALU operand is a VGPR: on gfx950 a wave64 VALU op
-// that reads an SGPR issues at half rate (tools/microbench/valu_asm.hip: v_mul_f32 s,v 1.71 ns vs
-// v,v 0.93 ns per SIMD), so the item's coefficients are staged once into the wave's LDS row and
-// read back per hypothesis with broadcast ds_read_b128, and the threshold lives in a VGPR.
-// Counts accumulate in the wave's LDS row (no block barriers); one coalesced row per item.
-#ifndef PITT_SCORE_EXP
-#define PITT_SCORE_EXP 0  // timing experiments only: 3 = synthetic points (no point loads)
-#endif
-#ifndef PITT_SCORE_PTS
-#define PITT_SCORE_PTS 4
-#endif
-#ifndef PITT_SCORE_NH
-#define PITT_SCORE_NH 4
-#endif
-constexpr int kHypBlock = PITT_SCORE_NH;   // hypotheses per LDS coefficient batch
-constexpr int kPts = PITT_SCORE_PTS;       // points per lane per sub-step (4 or 8)
-constexpr int kSub = 64 * kPts;            // points per wave sub-step
+//   1. box: the groups' bounding boxes (permlane32/16 swaps, then a DPP all-reduce inside each
+//      16-lane row: row g of the six box registers = group g's box);
+//   2. cull: 16 hypotheses per round, lane 16 g + h' tests hypothesis 16 r + h' against group g's
+//      box; a miss is certified only when every point of the box clears the threshold by a margin
+//      far above any rounding (box_clear below), so a culled pair counts 0 exactly;
+//   3. score: every surviving pair in PCL's float order -- 3 mul + 3 add (no FMA) + |d| < t --
+//      ballot -> s_bcnt1, the count written to lane 16 g + h' and accumulated in the wave's LDS row.
+//
+// On the table scenes ~27 % of the (64-point group, hypothesis) pairs survive (~21 % hold an
+// inlier), so a 32-hypothesis chunk costs less VALU than 16 unculled hypotheses.  Coefficients and
+// the threshold are VGPR operands (a wave64 VALU op reading an SGPR issues at half rate on gfx950,
+// tools/microbench/valu_asm.hip): the item's coefficients are staged into the wave's LDS row and
+// read back by broadcast ds_read_b128.
+constexpr int kGrp = 64;                   // points per culling group (one per lane)
+constexpr int kGPS = 4;                    // groups per sub-step (permlane32 + permlane16 swaps)
+constexpr int kSub = kGrp * kGPS;          // points per sub-step
 constexpr int kSubs = kTile / kSub;        // sub-steps per item
-#ifndef PITT_SCORE_PF
-#define PITT_SCORE_PF 1
-#endif
-constexpr int kPF = PITT_SCORE_PF;         // sub-steps in flight ahead of the scored one
+constexpr int kRnd = 16;                   // hypotheses tested per round (16-lane rows)
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 
 struct SubPts {
-    float x[kPts], y[kPts], z[kPts];
+    float x[kGPS], y[kGPS], z[kGPS];
 };
 
 struct ScoreItem {
@@ -208,38 +201,128 @@ struct ScoreItem {
 __device__ __forceinline__ void load_sub(const float* __restrict__ X, const float* __restrict__ Y,
                                          const float* __restrict__ Z, int64_t p0, int lane, SubPts& P) {
 #pragma unroll
-    for (int g = 0; g < kPts / 4; ++g) {
-        const int64_t i = p0 + g * 256 + lane * 4;
-#if PITT_SCORE_EXP == 3
-        const float fi = (float)(int)i * 1e-7f;
-        const float4 vx = make_float4(fi, fi + 1e-3f, fi + 2e-3f, fi + 3e-3f);
-        const float4 vy = make_float4(fi * 0.5f, fi * 0.25f, fi * 0.125f, fi * 0.0625f);
-        const float4 vz = make_float4(fi + 1.0f, fi + 1.5f, fi + 2.0f, fi + 2.5f);
-#else
-        const float4 vx = *reinterpret_cast<const float4*>(X + i);
-        const float4 vy = *reinterpret_cast<const float4*>(Y + i);
-        const float4 vz = *reinterpret_cast<const float4*>(Z + i);
-#endif
-        P.x[4 * g + 0] = vx.x; P.x[4 * g + 1] = vx.y; P.x[4 * g + 2] = vx.z; P.x[4 * g + 3] = vx.w;
-        P.y[4 * g + 0] = vy.x; P.y[4 * g + 1] = vy.y; P.y[4 * g + 2] = vy.z; P.y[4 * g + 3] = vy.w;
-        P.z[4 * g + 0] = vz.x; P.z[4 * g + 1] = vz.y; P.z[4 * g + 2] = vz.z; P.z[4 * g + 3] = vz.w;
+    for (int g = 0; g < kGPS; ++g) {
+        const int64_t i = p0 + g * kGrp + lane;
+        P.x[g] = X[i];
+        P.y[g] = Y[i];
+        P.z[g] = Z[i];
     }
 }
 
-// The item's coefficients, lane i <- hypothesis h0 + i + 64 j (clamped: rows past H are never read).
-template <int NST>
-struct CoefRegs {
-    float4 c[NST];
-};
-
-template <int NST>
-__device__ __forceinline__ void load_coefs(const float4* __restrict__ hc, int H, int lane, CoefRegs<NST>& C) {
-#pragma unroll
-    for (int j = 0; j < NST; ++j) C.c[j] = hc[min(lane + 64 * j, H - 1)];
+// Box arithmetic in asm: clang's fminf/fmaxf canonicalise every operand first (an extra v_max
+// per input), and IEEE v_min/v_max already skip quiet-NaN operands.
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmaxabs(float a, float b) {
+    float r;
+    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// v_permlane32_swap: a's lanes 32..63 <-> b's lanes 0..31.  v_permlane16_swap: a's odd rows <->
+// b's even rows (rows of 16 lanes).
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
 }
 
-// Item it -> (frame, tile).  Tiles past a shorter frame's end (ragged batches) become empty
-// items on the frame's first tile: every item then issues the same memory operations.
+// Row g of lo/hi = the 16-lane partial of group g (v0..v3 = groups 0..3, one point per lane).  The
+// first swaps are undone afterwards (one swap instead of two register copies): the groups' points
+// stay in place for the scoring.
+__device__ __forceinline__ void coord_box(float& v0, float& v1, float& v2, float& v3, float& lo, float& hi) {
+    swap32(v0, v2);  // v0 = [g0 lanes 0-31 | g2 lanes 0-31], v2 = [g0 32-63 | g2 32-63]
+    float mn02 = vmin(v0, v2), mx02 = vmax(v0, v2);
+    swap32(v0, v2);
+    swap32(v1, v3);
+    float mn13 = vmin(v1, v3), mx13 = vmax(v1, v3);
+    swap32(v1, v3);
+    swap16(mn02, mn13);  // rows of mn02 = [g0, g1, g2, g3] halves, mn13 the other halves
+    lo = vmin(mn02, mn13);
+    swap16(mx02, mx13);
+    hi = vmax(mx02, mx13);
+}
+
+struct RowBox {
+    float lo[3], hi[3];
+};
+
+// All-reduce inside each 16-lane row (row_ror 8, 4, 2, 1), the six registers interleaved so that
+// every DPP read is 5 VALU ops behind the write of its source (gfx9 needs 2 wait states).
+__device__ __forceinline__ void row_reduce(RowBox& B) {
+    asm("s_nop 4\n"
+#define PITT_RR(K)                                                                 \
+        "v_min_f32_dpp %0, %0, %0 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"      \
+        "v_min_f32_dpp %1, %1, %1 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"      \
+        "v_min_f32_dpp %2, %2, %2 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"      \
+        "v_max_f32_dpp %3, %3, %3 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"      \
+        "v_max_f32_dpp %4, %4, %4 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"      \
+        "v_max_f32_dpp %5, %5, %5 row_ror:" #K " row_mask:0xf bank_mask:0xf\n"
+        PITT_RR(8) PITT_RR(4) PITT_RR(2) PITT_RR(1)
+#undef PITT_RR
+        : "+v"(B.lo[0]), "+v"(B.lo[1]), "+v"(B.lo[2]), "+v"(B.hi[0]), "+v"(B.hi[1]), "+v"(B.hi[2]));
+}
+
+// Culling geometry of one box (row layout): centre, half extent and the magnitude bound M.
+struct RowGeo {
+    float c[3], h[3], m;
+};
+
+__device__ __forceinline__ RowGeo row_geo(const RowBox& B) {
+    RowGeo G;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        G.c[k] = 0.5f * (B.lo[k] + B.hi[k]);
+        G.h[k] = 0.5f * (B.hi[k] - B.lo[k]);
+    }
+    G.m = vmax(vmaxabs(B.lo[0], B.hi[0]), vmax(vmaxabs(B.lo[1], B.hi[1]), vmaxabs(B.lo[2], B.hi[2])));
+    return G;
+}
+
+// True when every point p of the box certainly fails PCL's |c . (p, 1)| < t.  Exact bound over the
+// box: |d(p)| >= |d(centre)| - sum |c_k| h_k.  Every rounding here and in PCL's own float evaluation
+// is below 1e-6 of S = |w| + (|a| + |b| + |c|) M (M bounds every |coordinate| of the box), so a
+// margin of 1e-5 S (+1e-30 for denormal-scale scenes) certifies the miss.  NaN or infinite boxes
+// (an all-NaN group, infinite coordinates) never compare true, so they are never culled.
+__device__ __forceinline__ bool box_clear(const RowGeo& G, float4 c, float tv) {
+    const float n1 = fabsf(c.x) + fabsf(c.y) + fabsf(c.z);
+    const float s = __builtin_fmaf(n1, G.m, fabsf(c.w) + 1e-25f);
+    const float lim = __builtin_fmaf(1e-5f, s, tv);
+    const float dc = __builtin_fmaf(c.x, G.c[0], __builtin_fmaf(c.y, G.c[1], __builtin_fmaf(c.z, G.c[2], c.w)));
+    const float rr = __builtin_fmaf(fabsf(c.x), G.h[0], __builtin_fmaf(fabsf(c.y), G.h[1], fabsf(c.z) * G.h[2]));
+    return fabsf(dc) - rr > lim;
+}
+
+// v_writelane_b32 (the compiler routes an SGPR lane select through m0: gfx9's constant bus takes
+// one SGPR operand)
+__device__ int writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// One float4 of LDS at a byte address held in a VGPR (ds_read_b128).
+__device__ __forceinline__ float4 lds_row(uint32_t addr) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = *(const __attribute__((address_space(3))) f4v*)(uintptr_t)addr;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// PCL's count of one group for one hypothesis (A3 order, no FMA).
+template <int ORDER>
+__device__ __forceinline__ int count_group(float4 c, float x, float y, float z, float tv) {
+    return __builtin_popcountll(__builtin_amdgcn_ballot_w64(fabsf(plane_dot<ORDER>(c, x, y, z)) < tv));
+}
+
+// Item it -> (frame, tile).  Tiles past a shorter frame's end (ragged batches) are empty items.
 //
 // Hypotheses per frame: RandomSampleConsensus evaluates hypothesis it only while it < k, and k
 // never grows once a hypothesis has been scored (a larger best count means a smaller k), so past
@@ -258,8 +341,8 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
     r.rem = ok ? (int32_t)min(m.n - (int64_t)t * kTile, (int64_t)kTile) : 0;
     r.f = f;
     r.t = t;
-    int h = H;
-    if (h0 > 0) {
+    int h = ok ? H : 0;
+    if (ok && h0 > 0) {
         const double k = st[f].k;
         const int need = k < (double)(h0 + H) ? (int)ceil(k) - h0 : H;  // hypotheses hh < k
         h = max(0, min(h, min(need, st[f].n_avail - h0)));
@@ -268,99 +351,94 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
     return r;
 }
 
-template <int ORDER, int NH, bool FIRST>
-__device__ __forceinline__ void score_block(const float4* cl, const SubPts& P, float tv, int lane,
-                                            int32_t* __restrict__ wc) {
-    float4 c[NH];
+// One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
+template <int ORDER, bool BOX>
+__device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, int rem, float tv, int lane,
+                                          int32_t* __restrict__ wc, RowBox& tbox) {
+    if (__builtin_expect(rem < kSub, 0)) {  // frame tail: points past it never count, never widen a box
 #pragma unroll
-    for (int k = 0; k < NH; ++k) c[k] = cl[k];  // LDS broadcast -> VGPRs
-    int v = 0;  // lane k <- count of hypothesis k (v_writelane), then one LDS op per lane
+        for (int g = 0; g < kGPS; ++g)
+            if (g * kGrp + lane >= rem) P.x[g] = P.y[g] = P.z[g] = __builtin_nanf("");
+    }
+    RowBox B;
+    coord_box(P.x[0], P.x[1], P.x[2], P.x[3], B.lo[0], B.hi[0]);
+    coord_box(P.y[0], P.y[1], P.y[2], P.y[3], B.lo[1], B.hi[1]);
+    coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
+    row_reduce(B);
+    if constexpr (BOX) {
 #pragma unroll
-    for (int k = 0; k < NH; ++k) {
-        // the 8 compare masks land in distinct SGPR pairs before any is counted (one shared mask
-        // register would make every v_cmp wait for the previous s_bcnt1); the products and sums
-        // are formed 4 points at a time so independent chains sit side by side
-        uint64_t m[kPts];
-#pragma unroll
-        for (int q = 0; q < kPts; q += 4) {
-            float a0[4], a1[4], a2[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) a0[p] = c[k].x * P.x[q + p];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) a2[p] = c[k].z * P.z[q + p];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) a1[p] = c[k].y * P.y[q + p];
-            if constexpr (ORDER == 0) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) a0[p] = a0[p] + a2[p];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) a1[p] = a1[p] + c[k].w;
-#pragma unroll
-                for (int p = 0; p < 4; ++p) a0[p] = a0[p] + a1[p];
-            } else {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) a0[p] = red4<ORDER>(a0[p], a1[p], a2[p], c[k].w);
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) m[q + p] = __builtin_amdgcn_ballot_w64(fabsf(a0[p]) < tv);
+        for (int k = 0; k < 3; ++k) {
+            tbox.lo[k] = vmin(tbox.lo[k], B.lo[k]);
+            tbox.hi[k] = vmax(tbox.hi[k], B.hi[k]);
         }
-        int n = 0;
-#pragma unroll
-        for (int p = 0; p < kPts; ++p) n += __builtin_popcountll(m[p]);
-        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(n), "i"(k));
     }
-    if (lane < NH) {
-        if constexpr (FIRST) wc[lane] = v;
-        else __hip_atomic_fetch_add(&wc[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const RowGeo G = row_geo(B);
+    const int rounds = (Hf + kRnd - 1) / kRnd;
+    for (int r = 0; r < rounds; ++r) {
+        const int hl = kRnd * r + (lane & (kRnd - 1));
+        const float4 cr = cl[min(hl, Hf - 1)];
+        const int nb = min(kRnd, Hf - kRnd * r);  // valid hypotheses of this round
+        const uint64_t valid = (((uint64_t)1 << nb) - 1) * 0x0001000100010001ull;
+        const uint64_t need = __builtin_amdgcn_ballot_w64(!box_clear(G, cr, tv)) & valid;
+        if (need == 0) continue;
+        // surviving pairs, group by group (the group's registers are static), hypotheses by
+        // set bit: the bit index is the count's lane 16 g + h', the coefficient row is read at a
+        // VGPR address (v_lshl_add) by LDS broadcast -- 6 scalar ops per pair, so the CU's one
+        // scalar unit keeps pace with its four SIMDs
+        int vc = 0;
+        uint32_t cbase;  // LDS byte address of row 16 r in a VGPR
+        asm("v_mov_b32 %0, %1" : "=v"(cbase) : "s"((uint32_t)(uintptr_t)(cl + kRnd * r)));
+#pragma unroll
+        for (int g = 0; g < kGPS; ++g) {
+            uint64_t bits = need & (0xFFFFull << (16 * g));
+            const uint32_t gbase = cbase - 256u * g;  // row of bit b: gbase + 16 b
+            // two pairs per trip when two are left: both coefficient reads behind one wait, two
+            // independent chains for the VALU
+            while (bits) {
+                int b0, b1;
+                asm("s_ff1_i32_b64 %0, %1" : "=s"(b0) : "s"(bits));
+                asm("s_bitset0_b64 %0, %1" : "+s"(bits) : "s"(b0));
+                if (bits) {
+                    asm("s_ff1_i32_b64 %0, %1" : "=s"(b1) : "s"(bits));
+                    asm("s_bitset0_b64 %0, %1" : "+s"(bits) : "s"(b1));
+                    const float4 c0 = lds_row(gbase + 16u * (uint32_t)b0);
+                    const float4 c1 = lds_row(gbase + 16u * (uint32_t)b1);
+                    const int n0 = count_group<ORDER>(c0, P.x[g], P.y[g], P.z[g], tv);
+                    const int n1 = count_group<ORDER>(c1, P.x[g], P.y[g], P.z[g], tv);
+                    vc = writelane(n0, b0, vc);
+                    vc = writelane(n1, b1, vc);
+                } else {
+                    const float4 c0 = lds_row(gbase + 16u * (uint32_t)b0);
+                    vc = writelane(count_group<ORDER>(c0, P.x[g], P.y[g], P.z[g], tv), b0, vc);
+                }
+            }
+        }
+        __hip_atomic_fetch_add(&wc[64 * r + lane], vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 }
 
-template <int ORDER, bool FIRST>
-__device__ __forceinline__ void score_sub(const float4* cl, int H, SubPts& P, int rem, float tv, int lane,
-                                          int32_t* __restrict__ wc) {
-    if (rem < kSub) {  // frame tail: points past the frame never count (NaN fails every test)
-#pragma unroll
-        for (int g = 0; g < kPts / 4; ++g)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (g * 256 + lane * 4 + q >= rem) P.x[4 * g + q] = __builtin_nanf("");
-    }
-    int h = 0;
-    for (; h + kHypBlock <= H; h += kHypBlock) score_block<ORDER, kHypBlock, FIRST>(cl + h, P, tv, lane, wc + h);
-    for (; h < H; ++h) score_block<ORDER, 1, FIRST>(cl + h, P, tv, lane, wc + h);
-}
-
-// NST = ceil(H / 64) stores per lane, unpredicated (rows are padded by 64 counts).
+// The item's coefficients into the wave's LDS row (rows past H repeat the last: never counted).
 template <int NST>
-__device__ __forceinline__ void store_counts(int32_t* __restrict__ out, const int32_t* row, int lane) {
-    asm volatile("" ::: "memory");  // compiler barrier only: the wave's LDS ops complete in order
+__device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__ hc, int H, int lane) {
+    float4 c[NST];
 #pragma unroll
-    for (int j = 0; j < NST; ++j) out[lane + 64 * j] = row[lane + 64 * j];
+    for (int j = 0; j < NST; ++j) c[j] = hc[min(lane + 64 * j, max(H, 1) - 1)];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NST; ++j) cl[lane + 64 * j] = c[j];
     asm volatile("" ::: "memory");
 }
 
-template <int NST>
-__device__ __forceinline__ void put_coefs(float4* cl, const CoefRegs<NST>& C, int lane) {
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < NST; ++j) cl[lane + 64 * j] = C.c[j];
-    asm volatile("" ::: "memory");
-}
-
-// The loop issues a fixed sequence of vector-memory ops -- per item: 6 point loads per sub-step,
-// NST coefficient loads with the next item's first sub-step, NST count stores -- with nothing
-// conditional (the prologue stores NST dummy rows into the padding), so every s_waitcnt the
-// compiler places is an exact vmcnt(N) that leaves the prefetched sub-step in flight.
-// BOX (the first chunk only): also record each tile's bounding box -- IEEE min/max skip NaN
-// points; the out-of-frame tail of the last tile only widens it -- for k_refine's tile skipping.
+// BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
+// -- for k_refine's tile skipping.
 template <int ORDER, int NST, bool BOX>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4 || kPts > 4 ? 4 : 6, NST >= 4 || kPts > 4 ? 5 : 8))) void k_score(
+__global__ __launch_bounds__(kBlock) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box) {
     __shared__ float4 wcoef[kWaves][NST * 64];
-    __shared__ int32_t wcnt[kWaves][NST * 64];
+    __shared__ int32_t wcnt[kWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
@@ -372,51 +450,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NST >= 4
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
     const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H);
     const int Hf = cur.h;
-    // kPF sub-steps in flight ahead of the one being scored (rotating register sets): k_score is
-    // VALU-bound alone, but beside other streams' k_refine the memory latency grows and a single
-    // sub-step of look-ahead leaves the VALU waiting
-    SubPts P[kPF + 1];
-    CoefRegs<NST> C;
+    if (Hf <= 0) return;  // an empty item, or a frame that needs none of this chunk
+    const int rounds = (Hf + kRnd - 1) / kRnd;
+    SubPts P[2];
     load_sub(X, Y, Z, cur.base, lane, P[0]);
-    load_coefs<NST>(hyp_coef + (int64_t)cur.f * hcap + h0, H, lane, C);
+    put_coefs<NST>(cl, hyp_coef + (int64_t)cur.f * hcap + h0, Hf, lane);
+    for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
+    RowBox tbox;
 #pragma unroll
-    for (int s = 1; s <= kPF; ++s) load_sub(X, Y, Z, cur.base + s * kSub, lane, P[s]);
-    put_coefs<NST>(cl, C, lane);
-    float bx[6] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-#pragma unroll
-    for (int s = 0; s < kSubs; ++s) {
-        if (s > 0 && s + kPF < kSubs) load_sub(X, Y, Z, cur.base + (s + kPF) * kSub, lane, P[(s + kPF) % (kPF + 1)]);
-        if constexpr (BOX) {
-            const SubPts& Q = P[s % (kPF + 1)];
-#pragma unroll
-            for (int q = 0; q < kPts; ++q) {
-                bx[0] = fminf(bx[0], Q.x[q]);
-                bx[1] = fminf(bx[1], Q.y[q]);
-                bx[2] = fminf(bx[2], Q.z[q]);
-                bx[3] = fmaxf(bx[3], Q.x[q]);
-                bx[4] = fmaxf(bx[4], Q.y[q]);
-                bx[5] = fmaxf(bx[5], Q.z[q]);
-            }
-            // keep the update here: sunk to the end, it would hold every sub-step's points live
-            asm volatile("" ::"v"(bx[0]), "v"(bx[1]), "v"(bx[2]), "v"(bx[3]), "v"(bx[4]), "v"(bx[5]));
-        }
-        if (s == 0) score_sub<ORDER, true>(cl, Hf, P[0], cur.rem, tv, lane, wc);
-        else score_sub<ORDER, false>(cl, Hf, P[s % (kPF + 1)], cur.rem - s * kSub, tv, lane, wc);
+    for (int k = 0; k < 3; ++k) {
+        tbox.lo[k] = __builtin_inff();
+        tbox.hi[k] = -__builtin_inff();
     }
-    store_counts<NST>(tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0, wc, lane);
-    if constexpr (BOX) {
+    // sub-steps in pairs: the next sub-step loads into the other register set while this one is
+    // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
+    for (int s = 0; s < kSubs; s += 2) {
+        load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
+        score_sub<ORDER, BOX>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox);
+        if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
+        score_sub<ORDER, BOX>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox);
+    }
+    // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
+    asm volatile("" ::: "memory");
+    int32_t* out = tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                bx[k] = fminf(bx[k], __shfl_xor(bx[k], off, 64));
-                bx[k + 3] = fmaxf(bx[k + 3], __shfl_xor(bx[k + 3], off, 64));
-            }
+    for (int j = 0; j < NST; ++j) {
+        const int h = lane + 64 * j;
+        if (h < Hf) {
+            const int32_t* row = wc + 64 * (h / kRnd) + (h % kRnd);
+            out[h] = row[0] + row[16] + row[32] + row[48];
         }
-        float v = bx[0];
+    }
+    if constexpr (BOX) {
+        // rows -> tile: the four rows' boxes combined (xor 16, xor 32 through ds_bpermute)
+        float v[6] = {tbox.lo[0], tbox.lo[1], tbox.lo[2], tbox.hi[0], tbox.hi[1], tbox.hi[2]};
 #pragma unroll
-        for (int k = 1; k < 6; ++k) v = lane == k ? bx[k] : v;
-        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = v;
+        for (int off = 16; off <= 32; off <<= 1)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const float o = __shfl_xor(v[k], off, 64);
+                v[k] = k < 3 ? vmin(v[k], o) : vmax(v[k], o);
+            }
+        float b = v[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k) b = lane == k ? v[k] : b;
+        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = b;
     }
 }
 
@@ -1009,13 +1087,14 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     FrameMeta* meta = as<FrameMeta>(ctx->buf("meta", (size_t)nf * sizeof(FrameMeta)));
     PITT_HIP_TRY(hipMemcpyAsync(meta, hm, (size_t)nf * sizeof(FrameMeta), hipMemcpyHostToDevice, sm));
 
-    // --- chunk schedule (geometric after the first few HBM-bound 16-hypothesis passes) ---
+    // --- chunk schedule: a culled first chunk that finishes most table frames (T <= 32 for 64 % of
+    //     them, tools/make_golden-style oracle runs), then geometric chunks ---
     std::vector<int> chunks;
 #ifndef PITT_FIRST_CHUNK
-#define PITT_FIRST_CHUNK 16
+#define PITT_FIRST_CHUNK 32
 #endif
     for (int h0 = 0, i = 0; h0 < hcap; ++i) {
-        int H = i == 0 ? PITT_FIRST_CHUNK : i < 4 ? 16 : std::min(kMaxScoreChunk, 16 << (i - 3));
+        int H = i == 0 ? PITT_FIRST_CHUNK : std::min(kMaxScoreChunk, 64 << (i - 1));
         H = std::min(H, hcap - h0);
         chunks.push_back(H);
         h0 += H;
