@@ -191,7 +191,7 @@ def main():
         ctx.plane_segment_batch(batch, params, outs[0])
     launches, ms, nbytes = ctx.profile_get("k_score")
     if rank == 0:
-        for k in ("k_hypothesize", "k_score", "k_replay", "k_refine"):
+        for k in ("k_hypothesize", "k_score", "k_replay", "k_refine", "k_sel_mark", "k_sel_write"):
             n_, ms_, b_ = ctx.profile_get(k)
             log(f"[rank 0] {k:15s} launches {n_:5d}  {ms_ / roof_steps:8.3f} ms/batch  "
                 f"avg {ms_ / max(1, n_) * 1e3:9.1f} us  {b_ / max(1e-9, ms_) / 1e6:8.1f} GB/s")

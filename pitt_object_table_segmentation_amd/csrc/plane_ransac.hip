@@ -505,18 +505,33 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     double log_probability, const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
     int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
     ChunkStat* __restrict__ next_stat) {
+    __shared__ int32_t part[kBlock / 64][kMaxChunk];
     __shared__ int32_t tot[kMaxChunk];
     const int f = blockIdx.x;
     if (st[f].done) return;
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int h = w; h < H; h += kBlock / 64) {
-        const int32_t* col = tile_counts + (int64_t)f * tiles_max * hstride + h0 + h;
-        int s = 0;
-        for (int t = lane; t < m.tiles; t += 64) s += col[(int64_t)t * hstride];
+    // the hypotheses k_score scored for this frame (resolve_item's limit); the loop below stops
+    // before any later one
+    int Hn = H;
+    if (h0 > 0) {
+        const double k = st[f].k;
+        const int need = k < (double)(h0 + H) ? (int)ceil(k) - h0 : H;
+        Hn = max(0, min(H, min(need, st[f].n_avail - h0)));
+    }
+    // per-tile count rows summed with lanes across hypotheses (coalesced rows), waves across tiles
+    const int32_t* base = tile_counts + (int64_t)f * tiles_max * hstride + h0;
+    for (int h = lane; h < Hn; h += 64) {
+        int acc = 0;
+        for (int t = w; t < m.tiles; t += kBlock / 64) acc += base[(int64_t)t * hstride + h];
+        part[w][h] = acc;
+    }
+    __syncthreads();
+    for (int h = threadIdx.x; h < Hn; h += kBlock) {
+        int acc = 0;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-        if (lane == 0) tot[h] = s;
+        for (int k = 0; k < kBlock / 64; ++k) acc += part[k][h];
+        tot[h] = acc;
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -839,6 +854,28 @@ __device__ __forceinline__ void chain16(float& s, const float4& a, const float4&
           "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// 8 x ds_read_b128 (32 consecutive floats from LDS byte address a), issued back to back.
+__device__ __forceinline__ void lds_read32(f4v (&v)[8], uint32_t a) {
+    asm volatile(
+        "ds_read_b128 %0, %8\n ds_read_b128 %1, %8 offset:16\n ds_read_b128 %2, %8 offset:32\n"
+        "ds_read_b128 %3, %8 offset:48\n ds_read_b128 %4, %8 offset:64\n ds_read_b128 %5, %8 offset:80\n"
+        "ds_read_b128 %6, %8 offset:96\n ds_read_b128 %7, %8 offset:112"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+        : "v"(a)
+        : "memory");
+}
+
+// 32 dependent adds, in order.
+__device__ __forceinline__ void chain32(float& s, const f4v (&v)[8]) {
+#pragma unroll
+    for (int t = 0; t < 8; t += 4)
+        chain16(s, make_float4(v[t].x, v[t].y, v[t].z, v[t].w), make_float4(v[t + 1].x, v[t + 1].y, v[t + 1].z, v[t + 1].w),
+                make_float4(v[t + 2].x, v[t + 2].y, v[t + 2].z, v[t + 2].w),
+                make_float4(v[t + 3].x, v[t + 3].y, v[t + 3].z, v[t + 3].w));
+}
+
 // Consumer: lane k < 9 accumulates stream k of computeMeanAndCovarianceMatrix (xx, xy, xz, yy, yz,
 // zz, x, y, z) over the ring in ascending inlier order.  Per 256-element block all 64 lanes first
 // form the six product streams (separately rounded, as PCL) into LDS; lanes 0..8 then run their
@@ -873,13 +910,23 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
             }
             asm volatile("" ::: "memory");  // this wave's LDS writes precede its reads (in order)
             const float* p = k < 6 ? &L.prod[k][0] : rx + (k - 6) * kRRing + q;
+            // the next 32 elements' reads are in flight while these 32 are added (reads and waits
+            // in asm: the compiler would otherwise sink each read to just before its use)
+            const uint32_t pa = (uint32_t)(uintptr_t)p;
+            f4v A[8], B[8];
+            lds_read32(A, pa);
 #pragma unroll
-            for (int i = 0; i < kRBlk; i += 32) {
-                float4 v[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const float4*>(p + i + 4 * t);
-                chain16(s, v[0], v[1], v[2], v[3]);
-                chain16(s, v[4], v[5], v[6], v[7]);
+            for (int i = 0; i < kRBlk / 32; i += 2) {
+                lds_read32(B, pa + 128u * (i + 1));
+                asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                chain32(s, A);
+                if (i + 2 < kRBlk / 32) {
+                    lds_read32(A, pa + 128u * (i + 2));
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                chain32(s, B);
             }
             r += kRBlk;
             if (lane == 0) lds_release(&L.R, r);
@@ -933,12 +980,11 @@ __global__ __launch_bounds__(128) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
-    int tiles_max, const float* __restrict__ tile_box, int32_t* __restrict__ inliers, int32_t* __restrict__ dummy,
-    float4* __restrict__ final_coef, int32_t* __restrict__ n_final) {
+    int tiles_max, float4* __restrict__ final_coef) {
     __shared__ RefineLds L;
     const int f = blockIdx.x;
     const FrameState s = st[f];
-    if (!s.has_model) return;
+    if (!s.has_model || !s.need_refine) return;
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -952,41 +998,107 @@ __global__ __launch_bounds__(128) void k_refine(
         L.coef = best_coef[f];
     }
     __syncthreads();
-    if (s.need_refine && PITT_REFINE_EXP != 2) {
-        if (wave == 0) {
-            const float4 cb = L.coef;
-            const int nact = refine_tiles<1>(L, m.tiles, lane, cb, thf,
-                                             tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride, nullptr);
-            const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
-            const int total = refine_stream<ORDER, 1, false, kRDepth1>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane,
-                                                                        nullptr, nullptr, nact, 0, nsteps);
-            if (lane == 0) {
-                L.total = total;
-                lds_release(&L.done, 1);
-            }
-        } else {
-            const float acc = refine_chain(L, lane);
-            float a9[9];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
-            if (lane == 0) L.coef = refine_plane<ORDER, DIV>(a9, lds_acquire(&L.W));
+    if (wave == 0) {
+        const float4 cb = L.coef;
+        const int nact = refine_tiles<1>(L, m.tiles, lane, cb, thf,
+                                         tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride, nullptr);
+        const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+        const int total = refine_stream<ORDER, 1, false, kRDepth1>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane,
+                                                                    nullptr, nullptr, nact, 0, nsteps);
+        if (lane == 0) {
+            L.total = total;
+            lds_release(&L.done, 1);
         }
-        __syncthreads();
+    } else {
+        const float acc = refine_chain(L, lane);
+        float a9[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
+        if (lane == 0) final_coef[f] = refine_plane<ORDER, DIV>(a9, lds_acquire(&L.W));
     }
-    if (wave != 0 || PITT_REFINE_EXP == 1) return;
-    // pass 2 (one wave: the ring depth, not the per-step work, bounds it -- two waves with half a
-    // ring each were slower)
-    const float4 c = L.coef;
-    const int nact = refine_tiles<2>(L, m.tiles, lane, c, thf, nullptr, 0, tile_box + (int64_t)f * tiles_max * 8);
-    const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
-    const int cnt = inliers ? refine_stream<ORDER, 2, true, kRDepth2>(L, L.pool, xs, ys, zs, m.n, c, thf, lane,
-                                                                      inliers + m.off, dummy + (int64_t)f * 64, nact,
-                                                                      0, nsteps)
-                            : refine_stream<ORDER, 2, false, kRDepth2>(L, L.pool, xs, ys, zs, m.n, c, thf, lane,
-                                                                       nullptr, nullptr, nact, 0, nsteps);
-    if (lane == 0) {
-        final_coef[f] = c;
-        n_final[f] = cnt;
+}
+
+// ------------------------------------------------------------------------------------------
+// Final selection: selectWithinDistance on each frame's final model (the refined plane, or the
+// winning hypothesis without refinement) -> the ascending inlier list.  Two launches, one wave per
+// (frame, tile), the whole chip on the batch instead of one streaming wave per frame:
+//   k_sel_mark   the tile's predicate bits (lane l, bit g <=> point 64 g + l of the tile is an
+//                inlier) and its inlier count; a tile whose bounding box certainly misses the
+//                model's slab (box_misses_slab) is marked empty without reading a point;
+//   k_sel_write  the tile's output offset (the frame's earlier tile counts) and its inliers'
+//                indices, ascending, from the predicate bits alone.
+constexpr int kSelGroups = kTile / 64;  // 32 predicate bits per lane
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_sel_mark(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ final_coef,
+    float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, uint32_t* __restrict__ sel_bits,
+    int32_t* __restrict__ sel_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    const int f = it / tiles_max, t = it - f * tiles_max;
+    if (f >= n_frames) return;
+    const FrameMeta m = meta[f];
+    if (t >= m.tiles || !st[f].has_model) return;
+    const float4 c = final_coef[f];
+    const int64_t row = (int64_t)f * tiles_max + t;
+    uint32_t word = 0;
+    if (!box_misses_slab(tile_box + row * 8, c, thf)) {
+        const int rem = (int)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
+        const int64_t p0 = m.off + (int64_t)t * kTile + lane;
+        float tv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+        float px[kSelGroups], py[kSelGroups], pz[kSelGroups];  // the whole tile in flight
+#pragma unroll
+        for (int g = 0; g < kSelGroups; ++g) {
+            px[g] = X[p0 + 64 * g];
+            py[g] = Y[p0 + 64 * g];
+            pz[g] = Z[p0 + 64 * g];
+        }
+#pragma unroll
+        for (int g = 0; g < kSelGroups; ++g) {
+            const bool in = (64 * g + lane < rem) & (fabsf(plane_dot<ORDER>(c, px[g], py[g], pz[g])) < tv);
+            word |= (in ? 1u : 0u) << g;  // no branch per group
+        }
+    }
+    sel_bits[row * 64 + lane] = word;
+    const int n = wave_sum(__builtin_popcount(word));
+    if (lane == 0) sel_cnt[row] = n;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sel_write(
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, int n_frames, int tiles_max,
+    const uint32_t* __restrict__ sel_bits, const int32_t* __restrict__ sel_cnt, int32_t* __restrict__ inliers,
+    int32_t* __restrict__ n_final) {
+    const int lane = threadIdx.x & 63;
+    const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    const int f = it / tiles_max, t = it - f * tiles_max;
+    if (f >= n_frames) return;
+    const FrameMeta m = meta[f];
+    if (t >= m.tiles || !st[f].has_model) return;
+    const int32_t* cnt = sel_cnt + (int64_t)f * tiles_max;
+    int pre = 0;
+    for (int j = lane; j < t; j += 64) pre += cnt[j];
+    pre = __builtin_amdgcn_readfirstlane(wave_sum(pre));
+    const int mine = cnt[t];
+    if (t == m.tiles - 1 && lane == 0) n_final[f] = pre + mine;
+    if (!inliers || mine == 0) return;
+    const uint32_t word = sel_bits[((int64_t)f * tiles_max + t) * 64 + lane];
+    int32_t* out = inliers + m.off + pre;
+    const int32_t i0 = t * kTile + lane;
+#pragma unroll
+    for (int g = 0; g < kSelGroups; ++g) {
+        const bool in = (word >> g) & 1u;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(in);
+        if (in) out[__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = i0 + 64 * g;
+        out += __builtin_popcountll(b);
     }
 }
 
@@ -1121,9 +1233,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
     int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
     float* tile_box = as<float>(ctx->buf("tile_box", (size_t)nf * tiles_max * 8 * sizeof(float)));
-    int32_t* refine_dummy = as<int32_t>(ctx->buf("refine_dummy", (size_t)nf * 64 * 4));  // k_refine's sink
+    uint32_t* sel_bits = as<uint32_t>(ctx->buf("sel_bits", (size_t)nf * tiles_max * 64 * 4));
+    int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !refine_dummy || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
 
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
@@ -1154,10 +1267,19 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        p->optimize ? 1 : 0, best_coef, final_coef);
-    // refinement (two passes over refined frames, one over the rest) + the final inlier list
-    rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0 * 2.0);
+    // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
+    rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0);
     hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(128), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                       thf, tile_counts, hstride, tiles_max, tile_box, inliers_dev, refine_dummy, final_coef, n_final);
+                       thf, tile_counts, hstride, tiles_max, final_coef);
+    ctx->prof_end(rec);
+    const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
+    rec = ctx->prof_begin("k_sel_mark", (double)total_pts * 12.0);
+    hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
+                       final_coef, thf, nf, tiles_max, tile_box, sel_bits, sel_cnt);
+    ctx->prof_end(rec);
+    rec = ctx->prof_begin("k_sel_write", 0.0);
+    hipLaunchKernelGGL(k_sel_write, dim3(sel_blocks), dim3(kBlock), 0, sm, meta, st, nf, tiles_max, sel_bits, sel_cnt,
+                       inliers_dev, n_final);
     ctx->prof_end(rec);
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
