@@ -28,7 +28,6 @@
 namespace pitt {
 
 constexpr int kMaxAttempts = 8192;
-constexpr int kMaxAttemptWords = kMaxAttempts / 32;
 
 struct FrameMeta {
     int64_t off;    // first point (multiple of 4)
@@ -43,6 +42,9 @@ struct FrameState {
     int32_t it, best_count, best_h, done;
     int32_t n_avail, exhausted, flags, status;
     int32_t has_model, need_refine, pad0, pad1;
+    // hypothesis generation so far (hyp_extend): attempts examined, good samples before the
+    // 1000-rejection cut-off, the current run of rejections, and whether generation has ended
+    int32_t gen_att, gen_good, gen_run, gen_done;
 };
 
 struct ChunkStat {
@@ -52,102 +54,133 @@ struct ChunkStat {
 };
 
 // ------------------------------------------------------------------------------------------
-// k_hypothesize: one block per frame.  Attempt a uses table triple a (the sampler's draws depend
-// only on (n, seed) until a sample is rejected; rejected attempts are simply skipped and
-// hypothesis h is the h-th good attempt).  getSamples gives up after 1000 consecutive rejects.
+// Hypotheses, generated lazily in windows of kBlock sampler-table attempts.  Attempt a uses table
+// triple a (the sampler's draws depend only on (n, seed) until a sample is rejected; rejected
+// attempts are simply skipped and hypothesis h is the h-th good attempt).  getSamples gives up
+// after 1000 consecutive rejects: good attempts past such a run are never used.  A frame's
+// hypotheses are generated only as far as the chunks that score it need them (k_hypothesize for
+// the first chunk, k_replay for the next), so a table frame that stops after ~30 hypotheses
+// examines ~256 attempts instead of max_iterations + slack.
+struct GenLds {
+    uint32_t bits[kBlock / 32];
+    int32_t wpre[kBlock / 32];
+    FrameState s;
+};
+
+// One block: extend frame f's hypotheses until n_avail >= target or generation ends.  G.s holds
+// the frame's state (read and written by thread 0 only, between barriers).
 template <int ORDER, int DIV>
-__global__ __launch_bounds__(kBlock) void k_hypothesize(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const FrameMeta* __restrict__ meta, const int32_t* __restrict__ tables, int A, int hcap,
-    int runnable_all, float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt,
-    FrameState* __restrict__ st, int32_t* __restrict__ list0, int32_t* __restrict__ cnt0,
-    ChunkStat* __restrict__ stat0) {
-    __shared__ uint32_t bits[kMaxAttemptWords];
-    __shared__ int32_t wpre[kMaxAttemptWords];
-    __shared__ int32_t s_avail, s_exh;
-    const int f = blockIdx.x;
-    const FrameMeta m = meta[f];
-    const int nw = (A + 31) >> 5;
-    for (int i = threadIdx.x; i < nw; i += kBlock) bits[i] = 0u;
-    __syncthreads();
-    const bool runnable = runnable_all && m.n >= 3;
+__device__ void hyp_extend(GenLds& G, int f, const FrameMeta& m, const float* __restrict__ X,
+                           const float* __restrict__ Y, const float* __restrict__ Z,
+                           const int32_t* __restrict__ tab, int A, int hcap, int target,
+                           float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt) {
     const float* x = X + m.off;
     const float* y = Y + m.off;
     const float* z = Z + m.off;
-    const int32_t* tab = tables + m.tab;
-    if (runnable) {
-        for (int a = threadIdx.x; a < A; a += kBlock) {
-            const int i0 = tab[3 * a], i1 = tab[3 * a + 1], i2 = tab[3 * a + 2];
-            float3 p0 = make_float3(x[i0], y[i0], z[i0]);
-            float3 p1 = make_float3(x[i1], y[i1], z[i1]);
-            float3 p2 = make_float3(x[i2], y[i2], z[i2]);
-            if (sample_good(p0, p1, p2)) atomicOr(&bits[a >> 5], 1u << (a & 31));
-        }
-    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int good = 0, run = 0, avail = -1;
-        for (int w = 0; w < nw; ++w) {
-            const uint32_t word = bits[w];
-            const int nbits = min(32, A - 32 * w);
-            wpre[w] = good;
-            if (avail >= 0) continue;
-            if (word == 0u) {
-                run += nbits;
-                if (run >= 1000) avail = good;
-                continue;
+    while (G.s.n_avail < target && !G.s.gen_done) {
+        const int a0 = G.s.gen_att;  // multiple of kBlock
+        const int a = a0 + (int)threadIdx.x;
+        bool good = false;
+        float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a < A) {
+            const int i0 = tab[3 * a], i1 = tab[3 * a + 1], i2 = tab[3 * a + 2];
+            const float3 p0 = make_float3(x[i0], y[i0], z[i0]);
+            const float3 p1 = make_float3(x[i1], y[i1], z[i1]);
+            const float3 p2 = make_float3(x[i2], y[i2], z[i2]);
+            good = sample_good(p0, p1, p2);
+            if (good) cf = plane_from3<ORDER, DIV>(p0, p1, p2);
+        }
+        const uint64_t bw = __builtin_amdgcn_ballot_w64(good);
+        if ((threadIdx.x & 63) == 0) {
+            G.bits[2 * (threadIdx.x >> 6)] = (uint32_t)bw;
+            G.bits[2 * (threadIdx.x >> 6) + 1] = (uint32_t)(bw >> 32);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // the serial getSamples scan over the window's 32-attempt words
+            FrameState& st = G.s;
+            int good_n = st.gen_good, run = st.gen_run, cut = 0;
+            for (int w = 0; w < kBlock / 32; ++w) {
+                const int nbits = min(32, A - (a0 + 32 * w));
+                G.wpre[w] = good_n;
+                if (cut || nbits <= 0) continue;
+                const uint32_t word = G.bits[w];
+                if (word == 0u) {
+                    run += nbits;
+                    if (run >= 1000) cut = 1;
+                    continue;
+                }
+                const int tz = __builtin_ctz(word);
+                if (run + tz >= 1000) { cut = 1; continue; }
+                good_n += __builtin_popcount(word);
+                run = nbits - 1 - (31 - __builtin_clz(word));
             }
-            const int tz = __builtin_ctz(word);
-            if (run + tz >= 1000) { avail = good; continue; }
-            good += __builtin_popcount(word);
-            const int hb = 31 - __builtin_clz(word);
-            run = nbits - 1 - hb;
+            st.gen_att = min(A, a0 + kBlock);
+            st.gen_good = good_n;
+            st.gen_run = run;
+            st.n_avail = min(good_n, hcap);
+            if (cut) {  // "No samples could be selected!": RANSAC stops at hypothesis good_n
+                st.gen_done = 1;
+            } else if (st.gen_att >= A) {  // the table ran out first (documented limit)
+                st.gen_done = 1;
+                st.exhausted = good_n < hcap ? 1 : 0;
+            } else if (good_n >= hcap) {
+                st.gen_done = 1;
+            }
         }
-        int exh = 0;
-        if (avail < 0) {
-            avail = good;
-            exh = (run < 1000 && good < hcap) ? 1 : 0;
+        __syncthreads();
+        if (good) {
+            const int w = (int)threadIdx.x >> 5;
+            const int h = G.wpre[w] + __builtin_popcount(G.bits[w] & ((1u << (threadIdx.x & 31)) - 1u));
+            if (h < G.s.n_avail && h < G.s.gen_good) {
+                hyp_coef[(int64_t)f * hcap + h] = cf;
+                hyp_attempt[(int64_t)f * hcap + h] = a;
+            }
         }
-        s_avail = min(avail, hcap);
-        s_exh = exh;
+        __syncthreads();
     }
-    __syncthreads();
-    const int avail = s_avail;
-    if (runnable) {
-        for (int a = threadIdx.x; a < A; a += kBlock) {
-            const uint32_t word = bits[a >> 5];
-            if (!((word >> (a & 31)) & 1u)) continue;
-            const int h = wpre[a >> 5] + __builtin_popcount(word & ((1u << (a & 31)) - 1u));
-            if (h >= avail) continue;
-            const int i0 = tab[3 * a], i1 = tab[3 * a + 1], i2 = tab[3 * a + 2];
-            float3 p0 = make_float3(x[i0], y[i0], z[i0]);
-            float3 p1 = make_float3(x[i1], y[i1], z[i1]);
-            float3 p2 = make_float3(x[i2], y[i2], z[i2]);
-            hyp_coef[(int64_t)f * hcap + h] = plane_from3<ORDER, DIV>(p0, p1, p2);
-            hyp_attempt[(int64_t)f * hcap + h] = a;
-        }
-    }
+}
+
+// k_hypothesize: one block per frame -- initial state and the first chunk's hypotheses.
+template <int ORDER, int DIV>
+__global__ __launch_bounds__(kBlock) void k_hypothesize(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const int32_t* __restrict__ tables, int A, int hcap, int target,
+    int runnable_all, float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt,
+    FrameState* __restrict__ st, int32_t* __restrict__ list0, int32_t* __restrict__ cnt0,
+    ChunkStat* __restrict__ stat0) {
+    __shared__ GenLds G;
+    const int f = blockIdx.x;
+    const FrameMeta m = meta[f];
+    const bool runnable = runnable_all && m.n >= 3;
     if (threadIdx.x == 0) {
-        FrameState s;
+        FrameState& s = G.s;
         s.k = 1.0;
         s.it = 0;
         s.best_count = -INT_MAX;
         s.best_h = -1;
-        s.n_avail = avail;
-        s.exhausted = s_exh;
+        s.done = 0;
+        s.n_avail = 0;
+        s.exhausted = 0;
         s.flags = 0;
         s.status = PITT_OK;
         s.has_model = 0;
         s.need_refine = 0;
         s.pad0 = s.pad1 = 0;
-        s.done = 0;
+        s.gen_att = s.gen_good = s.gen_run = 0;
+        s.gen_done = runnable ? 0 : 1;
+    }
+    if (runnable) hyp_extend<ORDER, DIV>(G, f, m, X, Y, Z, tables + m.tab, A, hcap, target, hyp_coef, hyp_attempt);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        FrameState s = G.s;
         if (!runnable) {
             s.done = 1;
             s.status = PITT_NO_MODEL;
-        } else if (avail == 0) {
+        } else if (s.n_avail == 0) {  // generation ended without a single sample
             s.done = 1;
-            s.status = s_exh ? PITT_E_SAMPLER : PITT_NO_MODEL;
-            s.pad0 = s_exh ? 0 : 1;
+            s.status = s.exhausted ? PITT_E_SAMPLER : PITT_NO_MODEL;
+            s.pad0 = s.exhausted ? 0 : 1;
         }
         st[f] = s;
         if (!s.done) {
@@ -500,11 +533,17 @@ __global__ __launch_bounds__(kBlock) void k_score(
 
 // ------------------------------------------------------------------------------------------
 // k_replay: RandomSampleConsensus::computeModel's serial control over the chunk's counts.
+// A frame that goes on to the next chunk first gets that chunk's hypotheses (hyp_extend up to
+// target_next), so every scored hypothesis index is below n_avail unless generation has ended.
+template <int ORDER, int DIV>
 __global__ __launch_bounds__(kBlock) void k_replay(
     const int32_t* __restrict__ tile_counts, int hcap, int hstride, int tiles_max, int h0, int H, int max_iter,
     double log_probability, const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
     int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
-    ChunkStat* __restrict__ next_stat) {
+    ChunkStat* __restrict__ next_stat, const float* __restrict__ X, const float* __restrict__ Y,
+    const float* __restrict__ Z, const int32_t* __restrict__ tables, int A, int target_next,
+    float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt) {
+    __shared__ GenLds G;
     __shared__ int32_t part[kBlock / 64][kMaxChunk];
     __shared__ int32_t tot[kMaxChunk];
     const int f = blockIdx.x;
@@ -534,8 +573,11 @@ __global__ __launch_bounds__(kBlock) void k_replay(
         tot[h] = acc;
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    FrameState s = st[f];
+    if (threadIdx.x == 0) G.s = st[f];
+    __syncthreads();
+    if (threadIdx.x != 0) goto extend;
+    {
+    FrameState& s = G.s;
     const double one_over_indices = 1.0 / (double)m.n;
     const double eps = 2.220446049250313e-16;
     for (int h = 0; h < H; ++h) {
@@ -568,12 +610,20 @@ __global__ __launch_bounds__(kBlock) void k_replay(
         if (s.it > max_iter) { s.done = 1; break; }
     }
     if (!s.done && !((double)s.it < s.k)) s.done = 1;
-    st[f] = s;
-    if (!s.done) {
-        const int idx = atomicAdd(next_cnt, 1);
-        next_list[idx] = f;
-        atomicAdd(&next_stat->tiles, m.tiles);
-        atomicAdd((unsigned long long*)&next_stat->points, (unsigned long long)m.n);
+    }
+extend:
+    __syncthreads();
+    if (!G.s.done && G.s.n_avail < target_next)
+        hyp_extend<ORDER, DIV>(G, f, m, X, Y, Z, tables + m.tab, A, hcap, target_next, hyp_coef, hyp_attempt);
+    if (threadIdx.x == 0) {
+        const FrameState s = G.s;
+        st[f] = s;
+        if (!s.done) {
+            const int idx = atomicAdd(next_cnt, 1);
+            next_list[idx] = f;
+            atomicAdd(&next_stat->tiles, m.tiles);
+            atomicAdd((unsigned long long*)&next_stat->points, (unsigned long long)m.n);
+        }
     }
 }
 
@@ -1243,7 +1293,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     int rec;
     rec = ctx->prof_begin("k_hypothesize", (double)nf * A * 48.0);
     hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta,
-                       tables, A, hcap, runnable_all, hyp_coef, hyp_attempt, st, lists, counters, cstat);
+                       tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
+                       counters, cstat);
     ctx->prof_end(rec);
     const double log_prob = std::log(1.0 - p->probability);
     std::vector<int> score_recs;
@@ -1259,10 +1310,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            tile_box);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
-        hipLaunchKernelGGL(k_replay, dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride, tiles_max, h0, H,
-                           max_iter,
-                           log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf, counters + c + 1,
-                           cstat + c + 1);
+        const int target_next = c + 1 < nchunks ? std::min(h0 + H + chunks[(size_t)c + 1], hcap) : 0;
+        hipLaunchKernelGGL((k_replay<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride,
+                           tiles_max, h0, H, max_iter, log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf,
+                           counters + c + 1, cstat + c + 1, fr->x, fr->y, fr->z, tables, A, target_next, hyp_coef,
+                           hyp_attempt);
         ctx->prof_end(rec);
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,

@@ -91,3 +91,24 @@ def test_later_chunks_and_hypothesis_limit(ctx):
               _plane_scene(rng, 24, range(24), noise=0.001), pitt.synth_frame(0, 3002, 320, 240)]
     res, inls = _run_batch(ctx, frames)
     _check(ctx, frames, res, inls)
+
+
+def test_lazy_hypothesis_generation_across_windows(ctx):
+    """Hypotheses are generated in windows of 256 sampler attempts, only as far as the chunks
+    need them.  Mostly-collinear clouds (exact line x = t, y = 2t, z = 3t: every all-line sample is
+    rejected) spread the good samples over many windows, put runs of rejections across window
+    borders, and at 99.9 % on the line hit getSamples' 1000-rejection cut-off mid-stream."""
+    rng = np.random.default_rng(15)
+    frames = []
+    for frac, n in ((0.95, 20000), (0.99, 20000), (0.999, 30000), (0.8, 5000)):
+        t = (rng.integers(0, 4000, n) * 0.25).astype(np.float32)
+        x, y, z = t.copy(), np.float32(2) * t, np.float32(3) * t
+        off = rng.random(n) >= frac
+        k = int(off.sum())
+        x[off] = rng.uniform(-50, 50, k).astype(np.float32)
+        y[off] = rng.uniform(-50, 50, k).astype(np.float32)
+        z[off] = rng.uniform(-50, 50, k).astype(np.float32)
+        frames.append((x, y, z))
+    kw = dict(max_iterations=150, sampler_slack=7000)
+    res, inls = _run_batch(ctx, frames, **kw)
+    _check(ctx, frames, res, inls, max_iterations=150)
