@@ -675,9 +675,15 @@ constexpr int kRBlk = 256;     // chain block: products formed by all lanes, the
 constexpr int kRMaxTiles = 1024;             // tile list capacity (frames up to 2M points)
 constexpr int kRStepsPerTile = kTile / kRChunk;
 
+// The nine chain lanes read nine different streams at the same offset in one ds_read_b128: the
+// streams' strides are padded by 4 floats so that they start on different LDS banks (unpadded,
+// all nine land on one bank group and each read serialises).
+constexpr int kRS = kRRing + 4;  // ring stream stride (x | y | z), floats
+constexpr int kPS = kRBlk + 4;   // product stream stride, floats
+
 struct RefineLds {
-    float pool[kRDepth2 * kRSlot];  // pass 1: raw[kRDepth1] | cx | cy | cz;  pass 2: raw[kRDepth2]
-    float prod[6][kRBlk];           // xx, xy, xz, yy, yz, zz of the current chain block
+    float pool[kRDepth2 * kRSlot + 12];  // raw[kRDepth1] | cx | cy | cz (stride kRS)
+    float prod[6 * kPS];                 // xx, xy, xz, yy, yz, zz of the current chain block
     int tl[kRMaxTiles];             // the pass's tiles that can hold inliers, ascending
     int W, R, done, total;
     float4 coef;
@@ -866,8 +872,8 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
                 if ((bits >> q) & 1u) {
                     const int r = k & (kRRing - 1);
                     rx[r] = px[q];
-                    rx[kRRing + r] = py[q];
-                    rx[2 * kRRing + r] = pz[q];
+                    rx[kRS + r] = py[q];
+                    rx[2 * kRS + r] = pz[q];
                     ++k;
                 }
 #endif
@@ -947,10 +953,10 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
             const int q = r & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
             {
                 const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
-                const float4 y = *reinterpret_cast<const float4*>(rx + kRRing + q + 4 * lane);
-                const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRRing + q + 4 * lane);
-                float4* o = reinterpret_cast<float4*>(&L.prod[0][0]) + lane;
-                constexpr int S = kRBlk / 4;
+                const float4 y = *reinterpret_cast<const float4*>(rx + kRS + q + 4 * lane);
+                const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRS + q + 4 * lane);
+                float4* o = reinterpret_cast<float4*>(&L.prod[0]) + lane;
+                constexpr int S = kPS / 4;
                 o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
                 o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
                 o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
@@ -959,7 +965,7 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
                 o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
             }
             asm volatile("" ::: "memory");  // this wave's LDS writes precede its reads (in order)
-            const float* p = k < 6 ? &L.prod[k][0] : rx + (k - 6) * kRRing + q;
+            const float* p = k < 6 ? &L.prod[k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
             // in asm: the compiler would otherwise sink each read to just before its use)
             const uint32_t pa = (uint32_t)(uintptr_t)p;
@@ -984,8 +990,8 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
         }
         if (lds_acquire(&L.done)) {
             const int wf = lds_acquire(&L.W);
-            const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRRing : rx + 2 * kRRing;
-            const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRRing : rx + 2 * kRRing;
+            const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRS : rx + 2 * kRS;
+            const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRS : rx + 2 * kRS;
             for (; r < wf; ++r) {
                 const int q = r & (kRRing - 1);
                 s += k >= 6 ? U[q] : U[q] * V[q];
