@@ -809,6 +809,7 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
     asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));  // plane in registers before the ring starts
     StepCursor ic, pc;  // issue and process cursors
+    int rfree = 0;      // PASS 1: the consumer's ring position as last read
 #pragma unroll
     for (int k = 0; k < DEPTH - 1; ++k) {
         refine_issue<DEPTH>(L, raw, xs, ys, zs, sb + k, sb, se, nact, lane, ic);
@@ -864,18 +865,22 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
                         4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b2 & lo), 0u));
         const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
         if constexpr (PASS == 1) {
-            while (wpos + tot - lds_acquire(&L.R) > kRRing) __builtin_amdgcn_s_sleep(1);
+            // ring space: the consumer's position is re-read only when the cached one is too old
+            if (wpos + tot - rfree > kRRing) {
+                while (wpos + tot - (rfree = lds_acquire(&L.R)) > kRRing) __builtin_amdgcn_s_sleep(1);
+            }
             int k = wpos + pre;
 #if PITT_REFINE_EXP != 4
+            // branch-free: a point that is not an inlier writes into the streams' padding (never read)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if ((bits >> q) & 1u) {
-                    const int r = k & (kRRing - 1);
-                    rx[r] = px[q];
-                    rx[kRS + r] = py[q];
-                    rx[2 * kRS + r] = pz[q];
-                    ++k;
-                }
+            for (int q = 0; q < 4; ++q) {
+                const bool in = (bits >> q) & 1u;
+                const int r = in ? (k & (kRRing - 1)) : kRRing;
+                rx[r] = px[q];
+                rx[kRS + r] = py[q];
+                rx[2 * kRS + r] = pz[q];
+                k += in ? 1 : 0;
+            }
 #endif
             (void)k;
             if (lane == 0) lds_release(&L.W, wpos + tot);
