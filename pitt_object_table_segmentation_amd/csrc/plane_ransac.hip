@@ -218,6 +218,10 @@ constexpr int kSub = kGrp * kGPS;          // points per sub-step
 constexpr int kSubs = kTile / kSub;        // sub-steps per item
 constexpr int kRnd = 16;                   // hypotheses tested per round (16-lane rows)
 constexpr int kWaves = kBlock / 64;
+#ifndef PITT_SCORE_WAVES
+#define PITT_SCORE_WAVES 2
+#endif
+constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score block
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 
 struct SubPts {
@@ -465,17 +469,17 @@ __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__
 // BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
 // -- for k_refine's tile skipping.
 template <int ORDER, int NST, bool BOX>
-__global__ __launch_bounds__(kBlock) void k_score(
+__global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box) {
-    __shared__ float4 wcoef[kWaves][NST * 64];
-    __shared__ int32_t wcnt[kWaves][NST * 64 * (64 / kRnd)];
+    __shared__ float4 wcoef[kScoreWaves][NST * 64];
+    __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
-    const int it = blockIdx.x * kWaves + w;
+    const int it = blockIdx.x * kScoreWaves + w;
     if (it >= items) return;
     float4* cl = wcoef[w];
     int32_t* wc = wcnt[w];
@@ -1315,8 +1319,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         score_recs.push_back(rec);
         auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
                            : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
-        const int score_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
-        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
+        const int score_blocks = (int)(((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves);
+        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
                            tile_box);
         ctx->prof_end(rec);
