@@ -391,7 +391,7 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
 template <int ORDER, bool BOX>
 __device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, int rem, float tv, int lane,
-                                          int32_t* __restrict__ wc, RowBox& tbox) {
+                                          int32_t* __restrict__ wc, RowBox& tbox, float* __restrict__ gbox) {
     if (__builtin_expect(rem < kSub, 0)) {  // frame tail: points past it never count, never widen a box
 #pragma unroll
         for (int g = 0; g < kGPS; ++g)
@@ -408,6 +408,16 @@ __device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, i
             tbox.lo[k] = vmin(tbox.lo[k], B.lo[k]);
             tbox.hi[k] = vmax(tbox.hi[k], B.hi[k]);
         }
+        // the four groups' boxes for the final selection's group skipping: lane 16 g + i (i < 6)
+        // stores value i of group g (one masked store per sub-step)
+        const int i = lane & 15;
+        float v = B.lo[0];
+        v = i == 1 ? B.lo[1] : v;
+        v = i == 2 ? B.lo[2] : v;
+        v = i == 3 ? B.hi[0] : v;
+        v = i == 4 ? B.hi[1] : v;
+        v = i == 5 ? B.hi[2] : v;
+        if (i < 6) gbox[(lane >> 4) * 8 + i] = v;
     }
     const RowGeo G = row_geo(B);
     const int rounds = (Hf + kRnd - 1) / kRnd;
@@ -473,7 +483,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
-    int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box) {
+    int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box,
+    float* __restrict__ group_box) {
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
     __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
@@ -493,6 +504,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     load_sub(X, Y, Z, cur.base, lane, P[0]);
     put_coefs<NST>(cl, hyp_coef + (int64_t)cur.f * hcap + h0, Hf, lane);
     for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
+    float* gb = group_box + ((int64_t)cur.f * tiles_max + cur.t) * (kTile / kGrp) * 8;  // BOX only
     RowBox tbox;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -503,9 +515,9 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
-        score_sub<ORDER, BOX>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox);
+        score_sub<ORDER, BOX>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox, gb + s * kGPS * 8);
         if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
-        score_sub<ORDER, BOX>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox);
+        score_sub<ORDER, BOX>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox, gb + (s + 1) * kGPS * 8);
     }
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
     asm volatile("" ::: "memory");
@@ -1104,8 +1116,8 @@ template <int ORDER>
 __global__ __launch_bounds__(kBlock) void k_sel_mark(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ final_coef,
-    float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, uint32_t* __restrict__ sel_bits,
-    int32_t* __restrict__ sel_cnt) {
+    float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, const float* __restrict__ group_box,
+    uint32_t* __restrict__ sel_bits, int32_t* __restrict__ sel_cnt) {
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -1120,17 +1132,23 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
         const int64_t p0 = m.off + (int64_t)t * kTile + lane;
         float tv;
         asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
-        float px[kSelGroups], py[kSelGroups], pz[kSelGroups];  // the whole tile in flight
+        // groups whose box certainly misses the slab hold no inlier: not read (lane g tests group g)
+        const bool gact = lane < kSelGroups && !box_misses_slab(group_box + (row * kSelGroups + lane) * 8, c, thf);
+        const uint32_t gm = (uint32_t)__builtin_amdgcn_ballot_w64(gact);
+        float px[kSelGroups], py[kSelGroups], pz[kSelGroups];  // the tile's live groups in flight
 #pragma unroll
         for (int g = 0; g < kSelGroups; ++g) {
-            px[g] = X[p0 + 64 * g];
-            py[g] = Y[p0 + 64 * g];
-            pz[g] = Z[p0 + 64 * g];
+            px[g] = py[g] = pz[g] = __builtin_nanf("");
+            if ((gm >> g) & 1u) {
+                px[g] = X[p0 + 64 * g];
+                py[g] = Y[p0 + 64 * g];
+                pz[g] = Z[p0 + 64 * g];
+            }
         }
 #pragma unroll
         for (int g = 0; g < kSelGroups; ++g) {
             const bool in = (64 * g + lane < rem) & (fabsf(plane_dot<ORDER>(c, px[g], py[g], pz[g])) < tv);
-            word |= (in ? 1u : 0u) << g;  // no branch per group
+            word |= (in ? 1u : 0u) << g;  // no branch per group (NaN never counts)
         }
     }
     sel_bits[row * 64 + lane] = word;
@@ -1298,10 +1316,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
     int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
     float* tile_box = as<float>(ctx->buf("tile_box", (size_t)nf * tiles_max * 8 * sizeof(float)));
+    float* group_box = as<float>(ctx->buf("group_box", (size_t)nf * tiles_max * (kTile / kGrp) * 8 * sizeof(float)));
     uint32_t* sel_bits = as<uint32_t>(ctx->buf("sel_bits", (size_t)nf * tiles_max * 64 * 4));
     int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
 
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
@@ -1322,7 +1341,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int score_blocks = (int)(((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves);
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
-                           tile_box);
+                           tile_box, group_box);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
         const int target_next = c + 1 < nchunks ? std::min(h0 + H + chunks[(size_t)c + 1], hcap) : 0;
@@ -1342,7 +1361,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
     rec = ctx->prof_begin("k_sel_mark", (double)total_pts * 12.0);
     hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
-                       final_coef, thf, nf, tiles_max, tile_box, sel_bits, sel_cnt);
+                       final_coef, thf, nf, tiles_max, tile_box, group_box, sel_bits, sel_cnt);
     ctx->prof_end(rec);
     rec = ctx->prof_begin("k_sel_write", 0.0);
     hipLaunchKernelGGL(k_sel_write, dim3(sel_blocks), dim3(kBlock), 0, sm, meta, st, nf, tiles_max, sel_bits, sel_cnt,
