@@ -697,11 +697,13 @@ constexpr int kRStepsPerTile = kTile / kRChunk;
 constexpr int kRS = kRRing + 4;  // ring stream stride (x | y | z), floats
 constexpr int kPS = kRBlk + 4;   // product stream stride, floats
 
+constexpr int kRProdSlots = 2;   // product blocks formed ahead of the chain
+
 struct RefineLds {
     float pool[kRDepth2 * kRSlot + 12];  // raw[kRDepth1] | cx | cy | cz (stride kRS)
-    float prod[6 * kPS];                 // xx, xy, xz, yy, yz, zz of the current chain block
+    float prod[kRProdSlots][6 * kPS];    // xx, xy, xz, yy, yz, zz of the next chain blocks
     int tl[kRMaxTiles];             // the pass's tiles that can hold inliers, ascending
-    int W, R, done, total;
+    int W, R, F, done, total;  // produced, consumed (chain), formed (products)
     float4 coef;
 };
 
@@ -953,40 +955,61 @@ __device__ __forceinline__ void chain32(float& s, const f4v (&v)[8]) {
                 make_float4(v[t + 3].x, v[t + 3].y, v[t + 3].z, v[t + 3].w));
 }
 
-// Consumer: lane k < 9 accumulates stream k of computeMeanAndCovarianceMatrix (xx, xy, xz, yy, yz,
-// zz, x, y, z) over the ring in ascending inlier order.  Per 256-element block all 64 lanes first
-// form the six product streams (separately rounded, as PCL) into LDS; lanes 0..8 then run their
-// chain as pure dependent adds, 64 elements per batched read.  Lanes >= 9 repeat lane 0's stream
-// (uniform control flow; results unused).  The last partial block goes element by element.
+// Former wave: the six product streams of each full 256-inlier block (formed by all 64 lanes,
+// separately rounded as PCL) into a product slot, up to kRProdSlots blocks ahead of the chain.
+__device__ __forceinline__ void refine_form(RefineLds& L, int lane) {
+    float* rx = ring_x(L);
+    int rf = 0, rc = 0;  // formed; the chain's position as last read
+    while (true) {
+        const int w = lds_acquire(&L.W);
+        if (w - rf >= kRBlk) {
+            if (rf - rc >= kRProdSlots * kRBlk) {  // the slot is still being summed
+                rc = lds_acquire(&L.R);
+                if (rf - rc >= kRProdSlots * kRBlk) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+            }
+            const int q = rf & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
+            const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
+            const float4 y = *reinterpret_cast<const float4*>(rx + kRS + q + 4 * lane);
+            const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRS + q + 4 * lane);
+            float4* o = reinterpret_cast<float4*>(&L.prod[(rf / kRBlk) % kRProdSlots][0]) + lane;
+            constexpr int S = kPS / 4;
+            o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
+            o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+            o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
+            o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
+            o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
+            o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
+            rf += kRBlk;
+            if (lane == 0) lds_release(&L.F, rf);  // after the block's writes (in-order LDS)
+            continue;
+        }
+        if (lds_acquire(&L.done) && lds_acquire(&L.W) - rf < kRBlk) break;  // the rest is the chain's tail
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Chain wave: lane k < 9 accumulates stream k of computeMeanAndCovarianceMatrix (xx, xy, xz, yy,
+// yz, zz, x, y, z) in ascending inlier order as pure dependent adds, 64 elements per batched read:
+// the products from the former's slots, x, y, z from the inlier ring.  Lanes >= 9 repeat lane 0's
+// stream (uniform control flow; results unused).  The last partial block goes element by element.
 __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
     const int k = lane < 9 ? lane : 0;
     float* rx = ring_x(L);
     float s = 0.0f;
     int r = 0;
     while (true) {
-        const int w = lds_acquire(&L.W);
-        if (w - r >= kRBlk) {
+        const int formed = lds_acquire(&L.F);
+        if (formed - r >= kRBlk) {
 #if PITT_REFINE_EXP == 3
             r += kRBlk;
             if (lane == 0) lds_release(&L.R, r);
             continue;
 #endif
-            const int q = r & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
-            {
-                const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
-                const float4 y = *reinterpret_cast<const float4*>(rx + kRS + q + 4 * lane);
-                const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRS + q + 4 * lane);
-                float4* o = reinterpret_cast<float4*>(&L.prod[0]) + lane;
-                constexpr int S = kPS / 4;
-                o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
-                o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
-                o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
-                o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
-                o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
-                o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
-            }
-            asm volatile("" ::: "memory");  // this wave's LDS writes precede its reads (in order)
-            const float* p = k < 6 ? &L.prod[k * kPS] : rx + (k - 6) * kRS + q;
+            const int q = r & (kRRing - 1);
+            const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
             // in asm: the compiler would otherwise sink each read to just before its use)
             const uint32_t pa = (uint32_t)(uintptr_t)p;
@@ -1011,13 +1034,15 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
         }
         if (lds_acquire(&L.done)) {
             const int wf = lds_acquire(&L.W);
-            const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRS : rx + 2 * kRS;
-            const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRS : rx + 2 * kRS;
-            for (; r < wf; ++r) {
-                const int q = r & (kRRing - 1);
-                s += k >= 6 ? U[q] : U[q] * V[q];
+            if (wf - r < kRBlk) {  // every full block summed: the tail element by element
+                const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRS : rx + 2 * kRS;
+                const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRS : rx + 2 * kRS;
+                for (; r < wf; ++r) {
+                    const int q = r & (kRRing - 1);
+                    s += k >= 6 ? U[q] : U[q] * V[q];
+                }
+                break;
             }
-            break;
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -1053,7 +1078,7 @@ __device__ float4 refine_plane(float a9[9], int n) {
 }
 
 template <int ORDER, int DIV>
-__global__ __launch_bounds__(128) void k_refine(
+__global__ __launch_bounds__(192) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
@@ -1071,6 +1096,7 @@ __global__ __launch_bounds__(128) void k_refine(
     if (threadIdx.x == 0) {
         L.W = 0;
         L.R = 0;
+        L.F = 0;
         L.done = 0;
         L.coef = best_coef[f];
     }
@@ -1086,6 +1112,8 @@ __global__ __launch_bounds__(128) void k_refine(
             L.total = total;
             lds_release(&L.done, 1);
         }
+    } else if (wave == 1) {
+        refine_form(L, lane);
     } else {
         const float acc = refine_chain(L, lane);
         float a9[9];
@@ -1355,7 +1383,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                        p->optimize ? 1 : 0, best_coef, final_coef);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
     rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0);
-    hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(128), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+    hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(192), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
                        thf, tile_counts, hstride, tiles_max, final_coef);
     ctx->prof_end(rec);
     const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
