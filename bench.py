@@ -190,8 +190,9 @@ def main():
     for _ in range(roof_steps):
         ctx.plane_segment_batch(batch, params, outs[0])
     launches, ms, nbytes = ctx.profile_get("k_score")
+    n_empty, ms_empty, _ = ctx.profile_get("k_score:empty")
     if rank == 0:
-        for k in ("k_hypothesize", "k_score", "k_replay", "k_refine", "k_sel_mark", "k_sel_write"):
+        for k in ("k_hypothesize", "k_score", "k_score:empty", "k_replay", "k_refine", "k_sel_mark", "k_sel_write"):
             n_, ms_, b_ = ctx.profile_get(k)
             log(f"[rank 0] {k:15s} launches {n_:5d}  {ms_ / roof_steps:8.3f} ms/batch  "
                 f"avg {ms_ / max(1, n_) * 1e3:9.1f} us  {b_ / max(1e-9, ms_) / 1e6:8.1f} GB/s")
@@ -234,7 +235,10 @@ def main():
                 "traffic": traffic,
                 "launches": launches,
                 "measured": f"HIP events on k_score's stream over a separate {roof_steps}-batch pass with one "
-                            "batch in flight (the timed pass overlaps batches on several streams)",
+                            "batch in flight (the timed pass overlaps batches on several streams); launches "
+                            "that score at least one tile (chunks with no active frame are listed apart)",
+                "empty_launches": n_empty,
+                "empty_us_per_batch": round(ms_empty / roof_steps * 1e3, 1),
                 "avg_launch_us": round(avg_ms * 1e3, 2),
                 "algorithmic_bytes_per_launch": round(nbytes / max(1, launches), 1),
             },

@@ -39,11 +39,15 @@ def main(tag):
             if line.startswith("{") and '"metric"' in line:
                 bench = json.loads(line)
     n_roof = bench["roofline"]["launches"]
+    n_empty = bench["roofline"].get("empty_launches", 0)
     tr = rows(os.path.join(trace_dir, "trace_kernel_trace.csv"))
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     score = [r for r in tr if "k_score" in r["Kernel_Name"]]
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in score]
-    roof = dur[-n_roof:]
+    # the roofline pass's dispatches; the chunks with no active frame (bench.py lists them apart)
+    # are its n_empty shortest
+    last = dur[-(n_roof + n_empty):]
+    roof = sorted(last)[n_empty:]
     stats = {}
     for r in rows(os.path.join(trace_dir, "trace_kernel_stats.csv")):
         name = r["Name"].split("(")[0].replace("void ", "")
@@ -59,7 +63,10 @@ def main(tag):
         if not os.path.exists(p):
             continue
         vals = [float(r["Counter_Value"]) for r in rows(p) if r["Counter_Name"] == counter]
-        pmc[counter] = vals[-n_roof:]
+        pmc[counter] = vals[-(n_roof + n_empty):]
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:  # drop the empty chunks (the smallest fetches)
+        keep = sorted(range(len(pmc["FETCH_SIZE"])), key=lambda i: pmc["FETCH_SIZE"][i])[n_empty:]
+        pmc = {k: [v[i] for i in sorted(keep)] for k, v in pmc.items()}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         per = [f * 1024 * 2 + w * 1024 for f, w in zip(pmc["FETCH_SIZE"], pmc["WRITE_SIZE"])]
         hbm = sum(per) / len(per)
