@@ -664,28 +664,23 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
 }
 
 // ------------------------------------------------------------------------------------------
-// k_refine: everything after RANSAC for one frame, one 2-wave block per frame.
+// k_refine: optimizeModelCoefficients (A6/A7) for one frame, one 3-wave block per frame.
 //
-//   pass 1 (optimizeModelCoefficients, A6/A7): the producer wave streams the frame (4 points per
-//     lane per 256-point step, global_load_lds ring kRDepth1 steps deep), selects the winning
-//     model's inliers and appends them -- ascending -- to an LDS ring; the consumer wave's lanes
-//     0..8 run the nine float accumulators of computeMeanAndCovarianceMatrix over that ring in
-//     exact PCL order (product formed per element, separately rounded; 32 elements per batched
-//     read).  Consumer lane 0 then divides (Eigen 3.2 `accu /= n`), runs eigen33 and forms the
-//     refined plane.
-//   pass 2 (selectWithinDistance on the refined model): the producer wave streams the frame again
-//     and writes the ascending inlier indices straight to the caller's buffer.
+//   producer  streams the frame's tiles that hold inliers of the winning hypothesis (4 points per
+//             lane per 256-point step, a global_load_lds ring kRDepth steps deep), selects the
+//             inliers and appends their coordinates -- ascending -- to an LDS ring;
+//   former    forms the six products of each full 256-inlier block (xx, xy, xz, yy, yz, zz, each
+//             separately rounded as PCL) with all 64 lanes into a product slot;
+//   chain     lanes 0..8 run the nine float accumulators of computeMeanAndCovarianceMatrix in
+//             exact PCL order as pure dependent adds; lane 0 then divides (Eigen 3.2
+//             `accu /= n`), runs eigen33 and writes the refined plane.
 //
-// The two waves hand over ring space through LDS counters (W: produced, R: consumed) with
-// release/acquire ordering at workgroup scope.  Frames without refinement run pass 2 only.
-#ifndef PITT_REFINE_EXP
-#define PITT_REFINE_EXP 0  // timing experiments only: 1 = skip pass 2, 2 = skip pass 1,
-#endif                     // 3 = consumer skips the chain, 4 = producer skips the ring writes
+// The waves hand over ring space through LDS counters (W: produced, F: formed, R: summed).  The
+// final inlier list of every frame (refined or not) is the job of k_sel_mark / k_sel_write.
 constexpr int kRChunk = 256;   // points per producer step (4 per lane)
 constexpr int kRSlot = 3 * kRChunk;          // floats per raw ring slot (x, y, z)
-constexpr int kRDepth1 = 6;    // pass 1: raw steps in flight (the rest of the pool is the inlier ring)
-constexpr int kRRing = 1024;   // compacted-inlier ring (points): 3 * kRRing floats = 4 slots
-constexpr int kRDepth2 = kRDepth1 + 3 * kRRing / kRSlot;  // pass 2: the whole pool is raw ring
+constexpr int kRDepth = 6;     // raw steps in flight
+constexpr int kRRing = 1024;   // compacted-inlier ring (points)
 constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
 
 constexpr int kRMaxTiles = 1024;             // tile list capacity (frames up to 2M points)
@@ -700,7 +695,7 @@ constexpr int kPS = kRBlk + 4;   // product stream stride, floats
 constexpr int kRProdSlots = 2;   // product blocks formed ahead of the chain
 
 struct RefineLds {
-    float pool[kRDepth2 * kRSlot + 12];  // raw[kRDepth1] | cx | cy | cz (stride kRS)
+    float pool[kRDepth * kRSlot + 3 * kRS];  // raw[kRDepth] | cx | cy | cz (stride kRS)
     float prod[kRProdSlots][6 * kPS];    // xx, xy, xz, yy, yz, zz of the next chain blocks
     int tl[kRMaxTiles];             // the pass's tiles that can hold inliers, ascending
     int W, R, F, done, total;  // produced, consumed (chain), formed (products)
@@ -727,22 +722,17 @@ __device__ __forceinline__ bool box_misses_slab(const float* __restrict__ b, flo
     return dmin > lim || dmax < -lim;
 }
 
-// The pass's tile list in LDS (ascending).  Pass 1: tiles where the winning hypothesis counted
-// inliers during scoring (exact).  Pass 2: tiles whose box meets the refined plane's slab.
-// Returns the number of tiles, or -1 (stream every tile) for frames beyond the list's capacity.
-template <int PASS>
-__device__ __forceinline__ int refine_tiles(RefineLds& L, int tiles, int lane, float4 c, float thf,
-                                            const int32_t* __restrict__ best_counts, int hstride,
-                                            const float* __restrict__ box) {
+// The tile list in LDS (ascending): tiles where the winning hypothesis counted inliers during
+// scoring (exact).  Returns the number of tiles, or -1 (stream every tile) for frames beyond the
+// list's capacity.
+__device__ __forceinline__ int refine_tiles(RefineLds& L, int tiles, int lane,
+                                            const int32_t* __restrict__ best_counts, int hstride) {
     if (tiles > kRMaxTiles) return -1;
     int nact = 0;
     for (int g = 0; g < tiles; g += 64) {
         const int t = g + lane;
         bool act = false;
-        if (t < tiles) {
-            if constexpr (PASS == 1) act = best_counts[(int64_t)t * hstride] > 0;
-            else act = !box_misses_slab(box + (int64_t)t * 8, c, thf);
-        }
+        if (t < tiles) act = best_counts[(int64_t)t * hstride] > 0;
         const uint64_t b = __builtin_amdgcn_ballot_w64(act);
         const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
         if (act) L.tl[nact + pre] = t;
@@ -774,7 +764,7 @@ __device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact, StepCu
     return cur.base + s % kRStepsPerTile;
 }
 
-__device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth1 * kRSlot; }
+__device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth * kRSlot; }
 
 typedef __attribute__((address_space(3))) volatile int lds_vint;  // ds_read/ds_write, not flat
 
@@ -809,17 +799,12 @@ __device__ __forceinline__ void refine_issue(RefineLds& L, float* raw, const flo
     __builtin_amdgcn_global_load_lds(zs + o, (lds_ptr)(b + 2 * kRChunk), 16, 0, 0);
 }
 
-// Producer: one pass over the frame with plane c.  PASS 1 appends the inliers' coordinates to the
-// LDS ring for the consumer; PASS 2 writes their indices to out (when given).  Returns the count.
-// OUT (pass 2 with an output buffer): every step issues exactly four index stores -- lanes without
-// an inlier for a store write to their own slot of `dummy` -- so the step's vector-memory ops are a
-// fixed count and the ring's wait can count them (stores share vmcnt with the loads: uncounted,
-// they would cut the look-ahead to a few steps).
-template <int ORDER, int PASS, bool OUT, int DEPTH>
+// Producer: one pass over the frame's listed steps [sb, se) with plane c, appending the inliers'
+// coordinates to the LDS ring for the former and the chain.  Returns the inlier count.
+template <int ORDER, int DEPTH>
 __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const float* xs, const float* ys,
                                              const float* zs, int64_t n, float4 c, float thf, int lane,
-                                             int32_t* __restrict__ out, int32_t* __restrict__ dummy, int nact,
-                                             int sb, int se) {
+                                             int nact, int sb, int se) {
     int wpos = 0;
     if (se <= sb) return 0;
     float* rx = ring_x(L);
@@ -827,22 +812,15 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
     asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));  // plane in registers before the ring starts
     StepCursor ic, pc;  // issue and process cursors
-    int rfree = 0;      // PASS 1: the consumer's ring position as last read
+    int rfree = 0;      // the chain's ring position as last read
 #pragma unroll
-    for (int k = 0; k < DEPTH - 1; ++k) {
-        refine_issue<DEPTH>(L, raw, xs, ys, zs, sb + k, sb, se, nact, lane, ic);
-        if constexpr (OUT) {  // the 4 stores a processed step would issue: the count stays exact
-#pragma unroll
-            for (int q = 0; q < 4; ++q)  // volatile: not elided; global address space: not a flat store
-                *(__attribute__((address_space(1))) volatile int32_t*)(dummy + lane) = q;
-        }
-    }
+    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(L, raw, xs, ys, zs, sb + k, sb, se, nact, lane, ic);
     for (int st = sb; st < se; ++st) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot refilled next are done
         refine_issue<DEPTH>(L, raw, xs, ys, zs, st + DEPTH - 1, sb, se, nact, lane, ic);
-        // step st landed: younger are the DEPTH - 1 steps issued since (3 loads each) and, with
-        // OUT, the 4 stores of each of the DEPTH - 1 steps processed since it was issued
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((OUT ? 7 : 3) * (DEPTH - 1)) : "memory");
+        // step st landed: younger are the DEPTH - 1 steps issued since (3 loads each; the producer
+        // issues no other vector-memory op, so the count is exact)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
         __builtin_amdgcn_sched_barrier(0);
         // the slot's reads in asm: the compiler treats any LDS read as aliasing the ring's
         // in-flight global_load_lds writes and would wait for all of them (vmcnt(0))
@@ -882,39 +860,22 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
                         2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b1 & lo), 0u)) +
                         4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b2 & lo), 0u));
         const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
-        if constexpr (PASS == 1) {
-            // ring space: the consumer's position is re-read only when the cached one is too old
-            if (wpos + tot - rfree > kRRing) {
-                while (wpos + tot - (rfree = lds_acquire(&L.R)) > kRRing) __builtin_amdgcn_s_sleep(1);
-            }
-            int k = wpos + pre;
-#if PITT_REFINE_EXP != 4
-            // branch-free: a point that is not an inlier writes into the streams' padding (never read)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const bool in = (bits >> q) & 1u;
-                const int r = in ? (k & (kRRing - 1)) : kRRing;
-                rx[r] = px[q];
-                rx[kRS + r] = py[q];
-                rx[2 * kRS + r] = pz[q];
-                k += in ? 1 : 0;
-            }
-#endif
-            (void)k;
-            if (lane == 0) lds_release(&L.W, wpos + tot);
-        } else {
-            if constexpr (OUT) {
-                int k = wpos + pre;
-                const int32_t i0 = (int32_t)s0 + p0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const bool in = (bits >> q) & 1u;
-                    int32_t* dst = in ? out + k : dummy + lane;
-                    *dst = i0 + q;
-                    k += in ? 1 : 0;
-                }
-            }
+        // ring space: the chain's position is re-read only when the cached one is too old
+        if (wpos + tot - rfree > kRRing) {
+            while (wpos + tot - (rfree = lds_acquire(&L.R)) > kRRing) __builtin_amdgcn_s_sleep(1);
         }
+        int k = wpos + pre;
+        // branch-free: a point that is not an inlier writes into the streams' padding (never read)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = (bits >> q) & 1u;
+            const int r = in ? (k & (kRRing - 1)) : kRRing;
+            rx[r] = px[q];
+            rx[kRS + r] = py[q];
+            rx[2 * kRS + r] = pz[q];
+            k += in ? 1 : 0;
+        }
+        if (lane == 0) lds_release(&L.W, wpos + tot);
         wpos += tot;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read steps land before the pool is reused
@@ -1003,11 +964,6 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
     while (true) {
         const int formed = lds_acquire(&L.F);
         if (formed - r >= kRBlk) {
-#if PITT_REFINE_EXP == 3
-            r += kRBlk;
-            if (lane == 0) lds_release(&L.R, r);
-            continue;
-#endif
             const int q = r & (kRRing - 1);
             const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
@@ -1103,11 +1059,10 @@ __global__ __launch_bounds__(192) void k_refine(
     __syncthreads();
     if (wave == 0) {
         const float4 cb = L.coef;
-        const int nact = refine_tiles<1>(L, m.tiles, lane, cb, thf,
-                                         tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride, nullptr);
+        const int nact = refine_tiles(L, m.tiles, lane, tile_counts + (int64_t)f * tiles_max * hstride + s.best_h,
+                                      hstride);
         const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
-        const int total = refine_stream<ORDER, 1, false, kRDepth1>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane,
-                                                                    nullptr, nullptr, nact, 0, nsteps);
+        const int total = refine_stream<ORDER, kRDepth>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane, nact, 0, nsteps);
         if (lane == 0) {
             L.total = total;
             lds_release(&L.done, 1);
