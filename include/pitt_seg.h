@@ -190,6 +190,26 @@ int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const float* y, const
                             int64_t n, double tolerance, int32_t min_size, int32_t max_size,
                             pitt_cluster_list* out);
 
+/* --- preprocessing in front of findSupports ------------------------------ */
+/* deepFiltering, src/segmentation_services/deep_filter_srv.cpp:27-44: points whose z is NaN are
+ * dropped; the rest go to "further" when z > threshold, else to "closer", both in input order.
+ * deep_threshold follows getServiceFloatParameter (src/point_cloud_library/srv_manager.h:163-167):
+ * a value >= 0 is used, anything else selects the service default 3.0 m (deep_filter_srv.cpp:19);
+ * used_threshold (optional) receives the value applied.  Device SoA in; device SoA outputs of
+ * capacity n each; either output triple may be NULL (that cloud is only counted). */
+int pitt_deep_filter(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                     float deep_threshold, float* closer_x, float* closer_y, float* closer_z,
+                     int64_t* n_closer, float* further_x, float* further_y, float* further_z,
+                     int64_t* n_further, float* used_threshold);
+
+/* pcl::transformPointCloud(cloud, out, Eigen::Matrix4f) as called at src/obj_segmentation.cpp:248
+ * (PCL 1.7 common/impl/transforms.hpp): out.k = m(k,0) x + m(k,1) y + m(k,2) z + m(k,3) in float,
+ * left to right, no FMA.  matrix: host, row-major 4x4 (the last row is ignored, as the Affine3f
+ * PCL builds from it).  dense = cloud.is_dense: when 0, points with a non-finite coordinate are
+ * copied unchanged.  Device SoA in and out (out may not alias in). */
+int pitt_transform_cloud(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                         const float matrix[16], int32_t dense, float* out_x, float* out_y, float* out_z);
+
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };
 /* 640x480 Kinect-like pinhole cloud in the camera optical frame, row-major pixel order.

@@ -690,4 +690,51 @@ int orc_cluster_get(const orc_cluster_list* L, int32_t c, int32_t* idx, float ce
 }
 void orc_cluster_free(orc_cluster_list* L) { delete L; }
 
+// --- preprocessing in front of findSupports ---------------------------------
+// srv_manager.h:163-167 getServiceFloatParameter: a request value >= 0 is used, anything else
+// (the -1 sentinel, NaN) selects the default.
+float orc_service_float_param(float input, float default_value) { return input >= 0.0f ? input : default_value; }
+
+// deep_filter_srv.cpp:37-44 deepFiltering: points with z == z (not NaN) split at z > th into
+// "further", else "closer", each in input order.  Either output may be NULL (counted only).
+int orc_deep_filter(const float* x, const float* y, const float* z, int64_t n, float th, float* cx, float* cy,
+                    float* cz, int64_t* n_closer, float* fx, float* fy, float* fz, int64_t* n_further) {
+    int64_t nc = 0, nf = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!(z[i] == z[i])) continue;
+        if (z[i] > th) {
+            if (fx) { fx[nf] = x[i]; fy[nf] = y[i]; fz[nf] = z[i]; }
+            ++nf;
+        } else {
+            if (cx) { cx[nc] = x[i]; cy[nc] = y[i]; cz[nc] = z[i]; }
+            ++nc;
+        }
+    }
+    if (n_closer) *n_closer = nc;
+    if (n_further) *n_further = nf;
+    return 0;
+}
+
+// pcl::transformPointCloud(cloud, out, Eigen::Matrix4f) as called at obj_segmentation.cpp:248
+// (PCL 1.7 common/impl/transforms.hpp, absent here): the Matrix4f becomes an Affine3f and every
+// point is  out.k = m(k,0) * x + m(k,1) * y + m(k,2) * z + m(k,3)  evaluated left to right in
+// float, no FMA (the x86 build).  A non-dense cloud (is_dense == false) copies every point first
+// and transforms only the points whose x, y and z are all finite.  m: row-major 4x4.
+int orc_transform_cloud(const float* x, const float* y, const float* z, int64_t n, const float m[16], int32_t dense,
+                        float* ox, float* oy, float* oz) {
+    for (int64_t i = 0; i < n; ++i) {
+        const float px = x[i], py = y[i], pz = z[i];
+        if (!dense && !(std::isfinite(px) && std::isfinite(py) && std::isfinite(pz))) {
+            ox[i] = px;
+            oy[i] = py;
+            oz[i] = pz;
+            continue;
+        }
+        ox[i] = m[0] * px + m[1] * py + m[2] * pz + m[3];
+        oy[i] = m[4] * px + m[5] * py + m[6] * pz + m[7];
+        oz[i] = m[8] * px + m[9] * py + m[10] * pz + m[11];
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -108,6 +108,14 @@ int64_t orc_cluster_size(const orc_cluster_list*, int32_t c);
 int     orc_cluster_get(const orc_cluster_list*, int32_t c, int32_t* idx, float centroid[3]);
 void    orc_cluster_free(orc_cluster_list*);
 
+/* --- preprocessing (deep_filter_srv.cpp:27-44, obj_segmentation.cpp:248) --- */
+float   orc_service_float_param(float input, float default_value);
+int     orc_deep_filter(const float* x, const float* y, const float* z, int64_t n, float th,
+                        float* cx, float* cy, float* cz, int64_t* n_closer,
+                        float* fx, float* fy, float* fz, int64_t* n_further);
+int     orc_transform_cloud(const float* x, const float* y, const float* z, int64_t n, const float m[16],
+                            int32_t dense, float* ox, float* oy, float* oz);
+
 #ifdef __cplusplus
 }
 #endif

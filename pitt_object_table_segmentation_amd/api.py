@@ -269,6 +269,40 @@ class Context:
         k = nout.value
         return ox[:k], oy[:k], oz[:k]
 
+    # ---- preprocessing (deep_filter_srv.cpp:27-44, obj_segmentation.cpp:248) ----------------
+    def deep_filter(self, x, y, z, deep_threshold: float = -1.0, closer: bool = True, further: bool = True):
+        """deepFiltering on device tensors: returns (closer (x, y, z), further (x, y, z), used_threshold);
+        a cloud not asked for comes back as None (it is only counted)."""
+        import torch
+        n = x.numel()
+
+        def planes(want):
+            return [torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(3)] if want else None
+
+        c, f = planes(closer), planes(further)
+        nc, nf = ctypes.c_int64(), ctypes.c_int64()
+        used = ctypes.c_float()
+
+        def ptrs(p):
+            return (None, None, None) if p is None else tuple(a.data_ptr() for a in p)
+
+        self._check(lib.pitt_deep_filter(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, float(deep_threshold),
+                                         *ptrs(c), ctypes.byref(nc), *ptrs(f), ctypes.byref(nf), ctypes.byref(used)),
+                    "pitt_deep_filter")
+        cout = None if c is None else tuple(a[:nc.value] for a in c)
+        fout = None if f is None else tuple(a[:nf.value] for a in f)
+        return cout, fout, used.value
+
+    def transform_cloud(self, x, y, z, matrix, dense: bool = True):
+        """pcl::transformPointCloud with a row-major 4x4 float matrix; device tensors in and out."""
+        import torch
+        m = np.ascontiguousarray(np.asarray(matrix, np.float32).reshape(16))
+        ox, oy, oz = (torch.empty_like(a) for a in (x, y, z))
+        self._check(lib.pitt_transform_cloud(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), x.numel(), _fp(m),
+                                             1 if dense else 0, ox.data_ptr(), oy.data_ptr(), oz.data_ptr()),
+                    "pitt_transform_cloud")
+        return ox, oy, oz
+
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
         x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))

@@ -178,3 +178,37 @@ def euclidean_clusters(x, y, z, tolerance=0.03, min_rate=0.01, max_rate=0.99, mi
     finally:
         O.orc_cluster_free(h)
     return out
+
+
+O.orc_service_float_param.restype = ctypes.c_float
+O.orc_service_float_param.argtypes = [ctypes.c_float, ctypes.c_float]
+O.orc_deep_filter.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_float] + [ctypes.c_void_p] * 8
+O.orc_transform_cloud.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32] + \
+    [ctypes.c_void_p] * 3
+
+
+def service_float_param(value: float, default: float) -> float:
+    """srv_manager.h:163-167 getServiceFloatParameter."""
+    return float(O.orc_service_float_param(value, default))
+
+
+def deep_filter(x, y, z, threshold: float):
+    """deep_filter_srv.cpp:37-44 at an already-resolved float threshold: (closer Nx3, further Nx3)."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    c = np.empty((3, max(n, 1)), np.float32)
+    f = np.empty((3, max(n, 1)), np.float32)
+    nc, nf = ctypes.c_int64(), ctypes.c_int64()
+    O.orc_deep_filter(_fp(x), _fp(y), _fp(z), n, threshold, _fp(c[0]), _fp(c[1]), _fp(c[2]), ctypes.byref(nc),
+                      _fp(f[0]), _fp(f[1]), _fp(f[2]), ctypes.byref(nf))
+    return c[:, :nc.value].T.copy(), f[:, :nf.value].T.copy()
+
+
+def transform_cloud(x, y, z, matrix, dense: bool = True):
+    """pcl::transformPointCloud(cloud, out, Matrix4f) restated (obj_segmentation.cpp:248): Nx3."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    m = np.ascontiguousarray(np.asarray(matrix, np.float32).reshape(16))
+    n = len(x)
+    o = np.empty((3, max(n, 1)), np.float32)
+    O.orc_transform_cloud(_fp(x), _fp(y), _fp(z), n, _fp(m), 1 if dense else 0, _fp(o[0]), _fp(o[1]), _fp(o[2]))
+    return o[:, :n].T.copy()

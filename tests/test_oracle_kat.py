@@ -147,3 +147,50 @@ def test_supports_table_with_object_known_answer():
     assert len(s["on_support_cloud"]) == len(bg)
     assert np.all(s["idx_map"][:len(table)] == -2)
     assert np.array_equal(s["idx_map"][len(table):], np.arange(len(bg)))
+
+
+# --- preprocessing (deep_filter_srv.cpp:27-44, obj_segmentation.cpp:248) ---------------------------
+def test_service_float_param_sentinels():
+    """srv_manager.h:163-167: >= 0 is used as given; -1 and NaN select the default."""
+    assert orc.service_float_param(-1.0, 3.0) == 3.0
+    assert orc.service_float_param(float("nan"), 3.0) == 3.0
+    assert orc.service_float_param(0.0, 3.0) == 0.0
+    assert orc.service_float_param(2.5, 3.0) == 2.5
+
+
+def test_deep_filter_known_answer():
+    x = np.arange(7, dtype=np.float32)
+    y = x + 10
+    z = np.array([1.0, np.nan, 3.5, 3.0, -1.0, np.inf, 2.9999998], np.float32)
+    closer, further = orc.deep_filter(x, y, z, 3.0)
+    assert closer[:, 0].tolist() == [0, 3, 4, 6]      # z <= 3 (ties closer), input order
+    assert further[:, 0].tolist() == [2, 5]           # z > 3, +inf included; NaN z dropped
+    assert np.array_equal(closer[:, 2], z[[0, 3, 4, 6]])
+
+
+def test_transform_known_answers():
+    rng = np.random.default_rng(3)
+    x, y, z = rng.normal(size=(3, 1000)).astype(np.float32)
+    ident = np.eye(4, dtype=np.float32)
+    assert np.array_equal(orc.transform_cloud(x, y, z, ident), np.stack([x, y, z], 1))
+    # the published float order, restated in numpy float32 (IEEE single ops, no FMA)
+    m = rng.normal(size=(4, 4)).astype(np.float32)
+    ref = np.stack([((m[k, 0] * x + m[k, 1] * y) + m[k, 2] * z) + m[k, 3] for k in range(3)], 1)
+    assert np.array_equal(orc.transform_cloud(x, y, z, m), ref)
+    # a 90-degree turn about z plus a translation is exact
+    rot = np.array([[0, -1, 0, 1], [1, 0, 0, 2], [0, 0, 1, 3], [0, 0, 0, 1]], np.float32)
+    assert np.array_equal(orc.transform_cloud(x, y, z, rot), np.stack([-y + 1, x + 2, z + 3], 1))
+
+
+def test_transform_non_dense_copies_non_finite():
+    x = np.array([1.0, np.nan, 2.0], np.float32)
+    y = np.array([1.0, 1.0, np.inf], np.float32)
+    z = np.array([1.0, 1.0, 1.0], np.float32)
+    m = np.eye(4, dtype=np.float32)
+    m[:3, 3] = 5
+    out = orc.transform_cloud(x, y, z, m, dense=False)
+    assert out[0].tolist() == [6, 6, 6]
+    assert np.isnan(out[1, 0]) and out[1, 1:].tolist() == [1, 1]   # copied, not transformed
+    assert out[2, 0] == 2 and np.isinf(out[2, 1]) and out[2, 2] == 1
+    dense = orc.transform_cloud(x, y, z, m, dense=True)
+    assert np.isnan(dense[1]).all()                                 # dense: NaN propagates

@@ -1,0 +1,119 @@
+"""Parity of the device preprocessing steps in front of findSupports with the
+oracle restatement: deepFiltering (deep_filter_srv.cpp:27-44) and pcl::transformPointCloud as
+called at obj_segmentation.cpp:248.  Both are exact float / order-preserving byte work, so every
+output must be bit-equal.  PCL 1.7's transforms.hpp is absent here: the transform's float order is
+the published expression (oracle/pitt_oracle.cpp orc_transform_cloud), pinned by the analytic cases
+in tests/test_oracle_kat.py."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_binding as orc
+import pitt_object_table_segmentation_amd as pitt
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(*arrays):
+    return [torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda() for a in arrays]
+
+
+def _host(planes):
+    return np.stack([p.cpu().numpy() for p in planes], 1) if planes is not None else None
+
+
+def _same(a, b):
+    """Bit-equality of float arrays (NaN payloads included)."""
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _pose(yaw_deg, pitch_deg, cam):
+    """Camera optical frame -> z-up world frame (tools' synthetic look_at), row-major 4x4 float."""
+    yaw, pitch = np.radians(yaw_deg), np.radians(pitch_deg)
+    f = np.array([np.sin(yaw) * np.cos(pitch), np.cos(yaw) * np.cos(pitch), -np.sin(pitch)])
+    r = np.array([np.cos(yaw), -np.sin(yaw), 0.0])
+    d = np.cross(f, r)
+    m = np.eye(4)
+    m[:3, 0], m[:3, 1], m[:3, 2], m[:3, 3] = r, d, f, cam
+    return m.astype(np.float32)
+
+
+@pytest.mark.parametrize("scene,seed,th", [(0, 1000, -1.0), (0, 1001, 1.2), (2, 1002, -1.0), (2, 1003, 0.9),
+                                           (1, 1004, 2.0), (0, 1005, 0.0), (0, 1006, 100.0),
+                                           (0, 1007, float("nan"))])
+def test_deep_filter_matches_oracle(ctx, scene, seed, th):
+    x, y, z = pitt.synth_frame(scene, seed)
+    closer, further, used = ctx.deep_filter(*_dev(x, y, z), deep_threshold=th)
+    assert used == orc.service_float_param(th, 3.0)
+    rc, rf = orc.deep_filter(x, y, z, used)
+    assert _same(_host(closer), rc) and _same(_host(further), rf)
+    assert len(rc) + len(rf) == int(np.sum(~np.isnan(z)))
+
+
+@pytest.mark.parametrize("n", [0, 1, 2047, 2048, 2049, 5000, 1228800])
+def test_deep_filter_ragged_and_large(ctx, n):
+    rng = np.random.default_rng(n)
+    x, y = rng.normal(size=(2, n)).astype(np.float32)
+    z = rng.uniform(0.0, 6.0, n).astype(np.float32)
+    z[rng.uniform(size=n) < 0.1] = np.nan
+    z[rng.uniform(size=n) < 0.05] = np.float32(3.0)  # ties at the default threshold stay closer
+    x[rng.uniform(size=n) < 0.05] = np.nan           # a NaN x with a finite z is kept
+    closer, further, used = ctx.deep_filter(*_dev(x, y, z))
+    rc, rf = orc.deep_filter(x, y, z, used)
+    assert _same(_host(closer), rc) and _same(_host(further), rf)
+
+
+def test_deep_filter_single_output(ctx):
+    x, y, z = pitt.synth_frame(0, 1010)
+    closer, further, used = ctx.deep_filter(*_dev(x, y, z), deep_threshold=1.5, further=False)
+    assert further is None
+    rc, _ = orc.deep_filter(x, y, z, used)
+    assert _same(_host(closer), rc)
+
+
+@pytest.mark.parametrize("dense", [True, False])
+@pytest.mark.parametrize("scene,seed", [(0, 1100), (2, 1101)])
+def test_transform_matches_oracle(ctx, scene, seed, dense):
+    x, y, z = pitt.synth_frame(scene, seed)
+    m = _pose(3.7, 35.2, (0.013, -0.021, 1.37))
+    out = ctx.transform_cloud(*_dev(x, y, z), m, dense=dense)
+    ref = orc.transform_cloud(x, y, z, m, dense=dense)
+    assert _same(_host(out), ref)
+    if not dense:  # non-finite points are copied unchanged
+        bad = ~(np.isfinite(x) & np.isfinite(y) & np.isfinite(z))
+        assert _same(ref[bad], np.stack([x, y, z], 1)[bad])
+
+
+def test_transform_random_matrices(ctx):
+    rng = np.random.default_rng(7)
+    n = 100003
+    x, y, z = (rng.normal(scale=3.0, size=(3, n))).astype(np.float32)
+    x[:5] = [np.inf, -np.inf, np.nan, 0.0, -0.0]
+    for _ in range(4):
+        m = rng.normal(size=(4, 4)).astype(np.float32)
+        for dense in (True, False):
+            out = ctx.transform_cloud(*_dev(x, y, z), m, dense=dense)
+            assert _same(_host(out), orc.transform_cloud(x, y, z, m, dense=dense))
+    # planes that are not 16-byte aligned take the scalar kernel
+    dx, dy, dz = (a[1:] for a in _dev(x, y, z))
+    out = ctx.transform_cloud(dx, dy, dz, m)
+    assert _same(_host(out), orc.transform_cloud(x[1:], y[1:], z[1:], m))
+
+
+def test_preprocessing_chain_into_supports(ctx):
+    """deepFiltering -> transformPointCloud -> findSupports (obj_segmentation.cpp:241-260, minus the
+    out-of-scope VoxelGrid and arm filter), device chain against the oracle chain."""
+    x, y, z = pitt.synth_frame(0, 1200, 320, 240)
+    closer, _, used = ctx.deep_filter(*_dev(x, y, z), further=False)
+    m = _pose(0.0, 35.0, (0.0, 0.0, 1.35))
+    wx, wy, wz = ctx.transform_cloud(*closer, m)
+    w = np.stack([a.cpu().numpy() for a in (wx, wy, wz)], 1)
+    rc, _ = orc.deep_filter(x, y, z, used)
+    rw = orc.transform_cloud(*rc.T, m)
+    assert _same(w, rw)
+    dev = ctx.find_supports(*w.T)
+    ref = orc.find_supports(*rw.T)
+    assert len(dev) == len(ref)
+    for d, r in zip(dev, ref):
+        assert np.array_equal(d.idx_map, r["idx_map"])
+        assert np.array_equal(d.coefficients, r["coefficients"])

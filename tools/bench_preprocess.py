@@ -1,0 +1,82 @@
+"""Throughput of the device preprocessing steps on one GPU: deepFiltering and
+transformPointCloud over a 256-frame batch of synthetic 640x480 camera clouds concatenated into one
+78.6M-point cloud, resident in HBM.  Prints one JSON line: per-kernel average duration (HIP events),
+algorithmic bytes and the fraction of the 8 TB/s HBM peak, plus a CPU (oracle) sample for scale.
+
+    python tools/bench_preprocess.py [--frames 256] [--reps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import pitt_object_table_segmentation_amd as pitt  # noqa: E402
+
+PEAK = 8000.0  # GB/s, MI355X HBM3E spec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    n1 = 640 * 480
+    x = np.empty(args.frames * n1, np.float32)
+    y = np.empty_like(x)
+    z = np.empty_like(x)
+    for f in range(min(args.frames, 16)):  # 16 distinct frames, cycled
+        fx, fy, fz = pitt.synth_frame(2 if f % 4 == 3 else 0, 1000 + f)
+        x[f * n1:(f + 1) * n1], y[f * n1:(f + 1) * n1], z[f * n1:(f + 1) * n1] = fx, fy, fz
+    for f in range(16, args.frames):
+        s = f % 16
+        x[f * n1:(f + 1) * n1], y[f * n1:(f + 1) * n1], z[f * n1:(f + 1) * n1] = (
+            x[s * n1:(s + 1) * n1], y[s * n1:(s + 1) * n1], z[s * n1:(s + 1) * n1])
+    n = len(x)
+    dx, dy, dz = (torch.from_numpy(a).cuda() for a in (x, y, z))
+    m = np.eye(4, dtype=np.float32)
+    m[:3, :3] = [[0.9986, -0.0523, 0.0], [-0.0300, -0.5726, -0.8192], [0.0428, 0.8181, -0.5736]]
+    m[:3, 3] = [0.01, -0.02, 1.37]
+    with pitt.Context(0) as ctx:
+        closer, further, used = ctx.deep_filter(dx, dy, dz)  # warm-up (buffers)
+        ctx.transform_cloud(dx, dy, dz, m)
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        for _ in range(args.reps):
+            closer, further, used = ctx.deep_filter(dx, dy, dz)
+            ctx.transform_cloud(dx, dy, dz, m)
+        torch.cuda.synchronize()
+        kept = len(closer[0]) + len(further[0])
+        res = {}
+        for k, extra in (("k_deep_count", 0.0), ("k_scan_pair", 0.0), ("k_deep_write", 12.0 * kept),
+                         ("k_transform", 0.0)):
+            launches, ms, algo = ctx.profile_get(k)
+            per = ms / launches * 1e3
+            byts = algo / launches + extra
+            res[k] = {"avg_us": round(per, 1), "algorithmic_bytes": byts,
+                      "GB_s": round(byts / per / 1e3, 1), "frac": round(byts / per / 1e3 / PEAK, 3)}
+        ctx.profile(False)
+    import oracle_binding as orc
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < 3.0:
+        sl = slice((k % 16) * n1, (k % 16 + 1) * n1)
+        rc, rf = orc.deep_filter(x[sl], y[sl], z[sl], used)
+        orc.transform_cloud(*rc.T, m)
+        k += 1
+    cpu = k * n1 / (time.perf_counter() - t0)
+    print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
+                                  f"(th {used}) + transform, {args.reps} reps", "points": n, "kept": kept,
+                      "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu),
+                      "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
+
+
+if __name__ == "__main__":
+    main()
