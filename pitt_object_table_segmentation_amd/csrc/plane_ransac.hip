@@ -679,17 +679,9 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
 // final inlier list of every frame (refined or not) is the job of k_sel_mark / k_sel_write.
 constexpr int kRChunk = 256;   // points per producer step (4 per lane)
 constexpr int kRSlot = 3 * kRChunk;          // floats per raw ring slot (x, y, z)
-#ifndef PITT_REFINE_EXP
-#define PITT_REFINE_EXP 0  // timing experiments only: 1 = chain skips its adds, 2 = former skips
-#endif                     // its products
-#ifndef PITT_RDEPTH
-#define PITT_RDEPTH 6
-#endif
-#ifndef PITT_RRING
-#define PITT_RRING 1024
-#endif
-constexpr int kRDepth = PITT_RDEPTH;  // raw steps in flight
-constexpr int kRRing = PITT_RRING;    // compacted-inlier ring (points, a power of two)
+constexpr int kRDepth = 6;     // raw steps in flight (12 measured the same: the producer is
+                               // compute-bound, ~436 us per batch without the chain)
+constexpr int kRRing = 1024;   // compacted-inlier ring (points, a power of two; 4096 measured the same)
 constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
 
 constexpr int kRMaxTiles = 1024;             // tile list capacity (frames up to 2M points)
@@ -940,11 +932,6 @@ __device__ __forceinline__ void refine_form(RefineLds& L, int lane) {
                     continue;
                 }
             }
-#if PITT_REFINE_EXP == 2
-            rf += kRBlk;
-            if (lane == 0) lds_release(&L.F, rf);
-            continue;
-#endif
             const int q = rf & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
             const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
             const float4 y = *reinterpret_cast<const float4*>(rx + kRS + q + 4 * lane);
@@ -978,11 +965,6 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
     while (true) {
         const int formed = lds_acquire(&L.F);
         if (formed - r >= kRBlk) {
-#if PITT_REFINE_EXP == 1
-            r += kRBlk;
-            if (lane == 0) lds_release(&L.R, r);
-            continue;
-#endif
             const int q = r & (kRRing - 1);
             const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
@@ -1089,9 +1071,6 @@ __global__ __launch_bounds__(192) void k_refine(
     } else if (wave == 1) {
         refine_form(L, lane);
     } else {
-#ifdef PITT_CHAIN_PRIO
-        __builtin_amdgcn_s_setprio(PITT_CHAIN_PRIO);
-#endif
         const float acc = refine_chain(L, lane);
         float a9[9];
 #pragma unroll
