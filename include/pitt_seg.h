@@ -210,6 +210,16 @@ int pitt_deep_filter(pitt_ctx* ctx, const float* x, const float* y, const float*
 int pitt_transform_cloud(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                          const float matrix[16], int32_t dense, float* out_x, float* out_y, float* out_z);
 
+/* fromROSMsg(PointCloud2 -> PointCloud<PointXYZ>) as called by PCManager::cloudForRosMsg,
+ * src/point_cloud_library/pc_manager.cpp:94-104: the XYZ fields of a device-
+ * resident little-endian PointCloud2 payload into SoA planes, row-major (point r * width + c at byte
+ * r * row_step + c * point_step; x, y, z FLOAT32 at off_x, off_y, off_z).  Offsets, point_step and
+ * row_step must be multiples of 4 and data 4-byte aligned; PointXYZ (point_step 16, offsets 0/4/8)
+ * takes one 16-byte load per point. */
+int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int32_t width, int32_t height, int32_t point_step,
+                            int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
+                            float* x, float* y, float* z);
+
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };
 /* 640x480 Kinect-like pinhole cloud in the camera optical frame, row-major pixel order.

@@ -715,6 +715,21 @@ int orc_deep_filter(const float* x, const float* y, const float* z, int64_t n, f
     return 0;
 }
 
+// fromROSMsg of the XYZ fields as called by PCManager::cloudForRosMsg (pc_manager.cpp:94-104):
+// point r * width + c is read at byte r * row_step + c * point_step (little-endian host).
+int orc_unpack_pointcloud2(const uint8_t* data, int32_t width, int32_t height, int32_t point_step, int64_t row_step,
+                           int32_t off_x, int32_t off_y, int32_t off_z, float* x, float* y, float* z) {
+    for (int64_t r = 0; r < height; ++r)
+        for (int64_t c = 0; c < width; ++c) {
+            const uint8_t* p = data + r * row_step + c * point_step;
+            const int64_t i = r * width + c;
+            std::memcpy(&x[i], p + off_x, 4);
+            std::memcpy(&y[i], p + off_y, 4);
+            std::memcpy(&z[i], p + off_z, 4);
+        }
+    return 0;
+}
+
 // pcl::transformPointCloud(cloud, out, Eigen::Matrix4f) as called at obj_segmentation.cpp:248
 // (PCL 1.7 common/impl/transforms.hpp, absent here): the Matrix4f becomes an Affine3f and every
 // point is  out.k = m(k,0) * x + m(k,1) * y + m(k,2) * z + m(k,3)  evaluated left to right in

@@ -113,6 +113,9 @@ float   orc_service_float_param(float input, float default_value);
 int     orc_deep_filter(const float* x, const float* y, const float* z, int64_t n, float th,
                         float* cx, float* cy, float* cz, int64_t* n_closer,
                         float* fx, float* fy, float* fz, int64_t* n_further);
+int     orc_unpack_pointcloud2(const uint8_t* data, int32_t width, int32_t height, int32_t point_step,
+                               int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
+                               float* x, float* y, float* z);
 int     orc_transform_cloud(const float* x, const float* y, const float* z, int64_t n, const float m[16],
                             int32_t dense, float* ox, float* oy, float* oz);
 

@@ -303,6 +303,18 @@ class Context:
                     "pitt_transform_cloud")
         return ox, oy, oz
 
+    def unpack_pointcloud2(self, data, width: int, height: int, point_step: int, row_step: int,
+                           offsets=(0, 4, 8)):
+        """fromROSMsg of the XYZ fields: `data` a device uint8 tensor holding the PointCloud2 payload;
+        returns device (x, y, z) of width * height points, row-major."""
+        import torch
+        n = width * height
+        x, y, z = (torch.empty(max(n, 1), dtype=torch.float32, device=data.device) for _ in range(3))
+        self._check(lib.pitt_unpack_pointcloud2(self.h, data.data_ptr(), width, height, point_step, row_step,
+                                                offsets[0], offsets[1], offsets[2], x.data_ptr(), y.data_ptr(),
+                                                z.data_ptr()), "pitt_unpack_pointcloud2")
+        return x[:n], y[:n], z[:n]
+
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
         x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))

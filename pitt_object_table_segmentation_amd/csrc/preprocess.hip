@@ -6,6 +6,9 @@
 //                         "further" and "closer" clouds, both in input order.
 //   pitt_transform_cloud  pcl::transformPointCloud(cloud, out, Eigen::Matrix4f) as called at
 //                         src/obj_segmentation.cpp:248 (PCL 1.7 common/impl/transforms.hpp).
+//   pitt_unpack_pointcloud2  fromROSMsg of the XYZ fields as called by
+//                         PCManager::cloudForRosMsg (src/point_cloud_library/pc_manager.cpp:94-104),
+//                         on a device-resident PointCloud2 payload.
 //
 // Both are HBM-bound byte streams: 12 B read per point, 12 B written per kept / transformed point.
 //
@@ -272,6 +275,30 @@ __global__ __launch_bounds__(256) void k_transform4(const float4* __restrict__ x
     }
 }
 
+// fromROSMsg for the XYZ fields of a sensor_msgs/PointCloud2 payload: point (r, c) at byte
+// r * row_step + c * point_step, x / y / z little-endian float32 at byte offsets ox / oy / oz.
+// Point-major (one thread per point); with point_step 16 and x, y, z at 0, 4, 8 (PointXYZ), one
+// dwordx4 per point.
+__global__ __launch_bounds__(256) void k_unpack_pc2(const uint8_t* __restrict__ data, int32_t width, int64_t n,
+                                                    int32_t point_step, int64_t row_step, int32_t ox, int32_t oy,
+                                                    int32_t oz, int xyz16, float* __restrict__ x,
+                                                    float* __restrict__ y, float* __restrict__ z) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / width, c = i - r * width;
+        const uint8_t* p = data + r * row_step + c * point_step;
+        if (xyz16) {
+            const float4 v = *(const float4*)p;
+            x[i] = v.x;
+            y[i] = v.y;
+            z[i] = v.z;
+        } else {
+            x[i] = *(const float*)(p + ox);
+            y[i] = *(const float*)(p + oy);
+            z[i] = *(const float*)(p + oz);
+        }
+    }
+}
+
 static inline int stream_grid(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
 }
@@ -328,6 +355,32 @@ int pitt_deep_filter(pitt_ctx* ctx, const float* x, const float* y, const float*
     if (used_threshold) *used_threshold = th;
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
     return pitt::deep_filter_impl(ctx, x, y, z, n, th, cx, cy, cz, n_closer, fx, fy, fz, n_further);
+}
+
+int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int32_t width, int32_t height, int32_t point_step,
+                            int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z, float* x, float* y,
+                            float* z) {
+    if (!ctx) return PITT_E_INVALID;
+    const int64_t n = (int64_t)width * height;
+    if (width < 0 || height < 0 || (n > 0 && (!data || !x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
+    const int32_t offs[3] = {off_x, off_y, off_z};
+    for (int32_t o : offs)
+        if (o < 0 || o % 4 != 0 || o + 4 > point_step) return ctx->fail(PITT_E_INVALID, "field offset");
+    if (point_step % 4 != 0 || row_step % 4 != 0 || ((uintptr_t)data & 3u) != 0 ||
+        (height > 1 && row_step < (int64_t)width * point_step))
+        return ctx->fail(PITT_E_INVALID, "point_step / row_step / alignment");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    const int xyz16 = point_step == 16 && off_x == 0 && off_y == 4 && off_z == 8 && row_step % 16 == 0 &&
+                      ((uintptr_t)data & 15u) == 0;
+    hipStream_t s = ctx->stream;
+    const int rec = ctx->prof_begin("k_unpack_pc2", (double)n * (12.0 + (xyz16 ? 16.0 : 12.0)));
+    if (n > 0)
+        hipLaunchKernelGGL(pitt::k_unpack_pc2, dim3(pitt::stream_grid(n)), dim3(256), 0, s, (const uint8_t*)data,
+                           width, n, point_step, row_step, off_x, off_y, off_z, xyz16, x, y, z);
+    ctx->prof_end(rec);
+    PITT_HIP_TRY(hipGetLastError());
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    return PITT_OK;
 }
 
 int pitt_transform_cloud(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

@@ -212,3 +212,17 @@ def transform_cloud(x, y, z, matrix, dense: bool = True):
     o = np.empty((3, max(n, 1)), np.float32)
     O.orc_transform_cloud(_fp(x), _fp(y), _fp(z), n, _fp(m), 1 if dense else 0, _fp(o[0]), _fp(o[1]), _fp(o[2]))
     return o[:, :n].T.copy()
+
+
+O.orc_unpack_pointcloud2.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 3
+
+
+def unpack_pointcloud2(data: np.ndarray, width, height, point_step, row_step, offsets=(0, 4, 8)):
+    """fromROSMsg XYZ restated (pc_manager.cpp:94-104): Nx3 float32, row-major."""
+    data = np.ascontiguousarray(data, np.uint8)
+    n = width * height
+    o = np.empty((3, max(n, 1)), np.float32)
+    O.orc_unpack_pointcloud2(data.ctypes.data, width, height, point_step, row_step, *offsets,
+                             _fp(o[0]), _fp(o[1]), _fp(o[2]))
+    return o[:, :n].T.copy()

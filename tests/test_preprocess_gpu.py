@@ -117,3 +117,51 @@ def test_preprocessing_chain_into_supports(ctx):
     for d, r in zip(dev, ref):
         assert np.array_equal(d.idx_map, r["idx_map"])
         assert np.array_equal(d.coefficients, r["coefficients"])
+
+
+
+def _pc2(xyz, point_step, row_pad, offsets, width, height, rng):
+    """A PointCloud2 payload with random bytes in the unused fields and row padding."""
+    row_step = width * point_step + row_pad
+    buf = rng.integers(0, 256, size=height * row_step, dtype=np.uint8)
+    for k in range(3):
+        col = np.frombuffer(xyz[:, k].astype("<f4").tobytes(), np.uint8).reshape(-1, 4)
+        for r in range(height):
+            base = r * row_step + offsets[k]
+            idx = base + np.arange(width)[:, None] * point_step + np.arange(4)[None, :]
+            buf[idx] = col[r * width:(r + 1) * width]
+    return buf, row_step
+
+
+@pytest.mark.parametrize("point_step,row_pad,offsets", [(16, 0, (0, 4, 8)), (32, 0, (0, 4, 8)), (16, 16, (0, 4, 8)),
+                                                        (20, 8, (8, 12, 16)), (12, 4, (0, 4, 8))])
+def test_unpack_pointcloud2_matches_oracle(ctx, point_step, row_pad, offsets):
+    rng = np.random.default_rng(point_step * 100 + row_pad)
+    width, height = 160, 120
+    x, y, z = pitt.synth_frame(2, 1300, width, height)  # NaN pixels included
+    xyz = np.stack([x, y, z], 1)
+    buf, row_step = _pc2(xyz, point_step, row_pad, offsets, width, height, rng)
+    dx, dy, dz = ctx.unpack_pointcloud2(torch.from_numpy(buf).cuda(), width, height, point_step, row_step, offsets)
+    ref = orc.unpack_pointcloud2(buf, width, height, point_step, row_step, offsets)
+    assert _same(_host((dx, dy, dz)), ref)
+    assert _same(ref, xyz.astype(np.float32))
+
+
+def test_unpack_pointcloud2_full_frame(ctx):
+    """640x480 PointXYZ (point_step 16): the 16-byte load path."""
+    rng = np.random.default_rng(5)
+    x, y, z = pitt.synth_frame(0, 1301)
+    xyz = np.stack([x, y, z], 1)
+    buf = np.zeros((len(x), 4), np.float32)
+    buf[:, :3] = xyz
+    buf[:, 3] = rng.normal(size=len(x))
+    dx, dy, dz = ctx.unpack_pointcloud2(torch.from_numpy(buf.view(np.uint8).reshape(-1)).cuda(), 640, 480, 16, 640 * 16)
+    assert _same(_host((dx, dy, dz)), xyz)
+
+
+def test_unpack_pointcloud2_rejects_bad_layout(ctx):
+    buf = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(pitt.PittError):
+        ctx.unpack_pointcloud2(buf, 2, 1, 16, 32, (0, 4, 14))   # field past point_step
+    with pytest.raises(pitt.PittError):
+        ctx.unpack_pointcloud2(buf, 2, 2, 16, 16, (0, 4, 8))    # row_step shorter than a row

@@ -1,5 +1,5 @@
-"""Throughput of the device preprocessing steps on one GPU: deepFiltering and
-transformPointCloud over a 256-frame batch of synthetic 640x480 camera clouds concatenated into one
+"""Throughput of the device preprocessing steps on one GPU: PointCloud2
+unpacking, deepFiltering and transformPointCloud over a 256-frame batch of synthetic 640x480 camera clouds concatenated into one
 78.6M-point cloud, resident in HBM.  Prints one JSON line: per-kernel average duration (HIP events),
 algorithmic bytes and the fraction of the 8 TB/s HBM peak, plus a CPU (oracle) sample for scale.
 
@@ -43,20 +43,24 @@ def main():
     m = np.eye(4, dtype=np.float32)
     m[:3, :3] = [[0.9986, -0.0523, 0.0], [-0.0300, -0.5726, -0.8192], [0.0428, 0.8181, -0.5736]]
     m[:3, 3] = [0.01, -0.02, 1.37]
+    aos = torch.stack([dx, dy, dz, torch.zeros_like(dx)], 1).contiguous().view(torch.uint8).reshape(-1)
     with pitt.Context(0) as ctx:
+        ux, uy, uz = ctx.unpack_pointcloud2(aos, n1, n // n1, 16, n1 * 16)  # PointXYZ payload -> SoA
+        assert all(torch.equal(u.view(torch.int32), d.view(torch.int32)) for u, d in ((ux, dx), (uy, dy), (uz, dz)))
         closer, further, used = ctx.deep_filter(dx, dy, dz)  # warm-up (buffers)
         ctx.transform_cloud(dx, dy, dz, m)
         torch.cuda.synchronize()
         ctx.profile(True)
         ctx.profile_reset()
         for _ in range(args.reps):
+            ctx.unpack_pointcloud2(aos, n1, n // n1, 16, n1 * 16)
             closer, further, used = ctx.deep_filter(dx, dy, dz)
             ctx.transform_cloud(dx, dy, dz, m)
         torch.cuda.synchronize()
         kept = len(closer[0]) + len(further[0])
         res = {}
-        for k, extra in (("k_deep_count", 0.0), ("k_scan_pair", 0.0), ("k_deep_write", 12.0 * kept),
-                         ("k_transform", 0.0)):
+        for k, extra in (("k_unpack_pc2", 0.0), ("k_deep_count", 0.0), ("k_scan_pair", 0.0),
+                         ("k_deep_write", 12.0 * kept), ("k_transform", 0.0)):
             launches, ms, algo = ctx.profile_get(k)
             per = ms / launches * 1e3
             byts = algo / launches + extra
@@ -73,7 +77,7 @@ def main():
         k += 1
     cpu = k * n1 / (time.perf_counter() - t0)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
-                                  f"(th {used}) + transform, {args.reps} reps", "points": n, "kept": kept,
+                                  f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
                       "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu),
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
