@@ -14,6 +14,12 @@
  *        src/segmentation_services/supports_segmentation_srv.cpp:241-361
  *   pitt_euclidean_clusters       replaces  EuclideanClusterExtraction::extract + KdTree
  *        src/segmentation_services/cluster_segmentation_srv.cpp:54-69
+ *   pitt_deep_filter              replaces  the deepFiltering loop
+ *        src/segmentation_services/deep_filter_srv.cpp:37-44
+ *   pitt_transform_cloud          replaces  pcl::transformPointCloud(cloud, out, Matrix4f)
+ *        src/obj_segmentation.cpp:248
+ *   pitt_unpack_pointcloud2       replaces  fromROSMsg (PointCloud2 -> PointCloud<PointXYZ>)
+ *        src/point_cloud_library/pc_manager.cpp:94-104
  *
  * Conventions: plain pointers and sizes, no C++ types, no exceptions.  Every call returns an
  * int status (PITT_OK, PITT_NO_MODEL, or a negative PITT_E_*).  A context is not thread-safe;
