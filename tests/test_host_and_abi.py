@@ -109,3 +109,15 @@ def test_create_without_device_fails_cleanly():
         pytest.skip("a device is present")
     with pytest.raises(pitt.PittError):
         pitt.Context(0)
+
+
+def test_preprocessing_entry_points_reject_null_context():
+    """The C ABI validates before touching a device: a NULL context is PITT_E_INVALID (no GPU needed)."""
+    import ctypes
+    from pitt_object_table_segmentation_amd import _lib as L
+    lib = L.lib
+    m = (ctypes.c_float * 16)()
+    assert lib.pitt_deep_filter(None, None, None, None, 0, -1.0, None, None, None, None, None, None, None, None,
+                                None) == L.PITT_E_INVALID
+    assert lib.pitt_transform_cloud(None, None, None, None, 0, m, 1, None, None, None) == L.PITT_E_INVALID
+    assert lib.pitt_unpack_pointcloud2(None, None, 0, 0, 16, 0, 0, 4, 8, None, None, None) == L.PITT_E_INVALID
