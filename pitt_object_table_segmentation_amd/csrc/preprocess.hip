@@ -51,23 +51,37 @@ __device__ __forceinline__ int lane_rank(uint64_t b) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
-// One 512-thread block per super-tile: wave w counts tile w of it (32 slices of 64 points, lane l:
-// point 64 j + l), the block adds the eight wave totals.
+// One 512-thread block per super-tile: wave w counts tile w of it (8 chunks of 256 points, lane l:
+// points 256 j + 4 l .. +3 with one dwordx4; the count needs no order), the block adds the eight
+// wave totals.  z is 16-byte aligned in every full chunk when the plane is (the tail goes point by
+// point).
 __global__ __launch_bounds__(64 * kDSuper) void k_deep_count(const float* __restrict__ z, int64_t n, float th,
                                                              int32_t* __restrict__ cnt_closer,
                                                              int32_t* __restrict__ cnt_further) {
     __shared__ int32_t part[2][kDSuper];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t ns = dsupers(n);
+    const bool al16 = ((uintptr_t)z & 15u) == 0;
     for (int64_t t = blockIdx.x; t < ns; t += gridDim.x) {
         int nc = 0, nf = 0;
-        const int64_t b = t * kDSuperPts + (int64_t)w * kCTile + lane;
-#pragma unroll 8
-        for (int j = 0; j < kCTile / 64; ++j) {
-            const int64_t i = b + 64 * j;
-            const int c = i < n ? deep_class(z[i], th) : 0;
-            nc += c == 1 ? 1 : 0;  // per lane; summed across the wave once per tile
-            nf += c == 2 ? 1 : 0;
+        const int64_t b = t * kDSuperPts + (int64_t)w * kCTile + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < kCTile / 256; ++j) {
+            const int64_t i = b + 256 * j;
+            float v[4];
+            if (al16 && i + 4 <= n) {
+                const float4 q = *(const float4*)(z + i);
+                v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = i + k < n ? z[i + k] : __builtin_nanf("");
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = deep_class(v[k], th);
+                nc += c == 1 ? 1 : 0;  // per lane; summed across the wave once per tile
+                nf += c == 2 ? 1 : 0;
+            }
         }
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
