@@ -165,3 +165,33 @@ def test_unpack_pointcloud2_rejects_bad_layout(ctx):
         ctx.unpack_pointcloud2(buf, 2, 1, 16, 32, (0, 4, 14))   # field past point_step
     with pytest.raises(pitt.PittError):
         ctx.unpack_pointcloud2(buf, 2, 2, 16, 16, (0, 4, 8))    # row_step shorter than a row
+
+
+def test_preprocessed_frames_through_plane_batch(ctx):
+    """PointCloud2 payloads -> unpack -> deep filter -> world transform on the device, then the frames
+    (now of different sizes) through the batched plane RANSAC; every stage and the RANSAC results
+    against the oracle chain."""
+    rng = np.random.default_rng(11)
+    m = _pose(2.0, 36.0, (0.01, 0.0, 1.36))
+    frames, ref_frames = [], []
+    for k, scene in enumerate((0, 2, 0, 1)):
+        x, y, z = pitt.synth_frame(scene, 1400 + k, 320, 240)
+        xyz = np.stack([x, y, z], 1)
+        buf, row_step = _pc2(xyz, 16, 0, (0, 4, 8), 320, 240, rng)
+        ux, uy, uz = ctx.unpack_pointcloud2(torch.from_numpy(buf).cuda(), 320, 240, 16, row_step)
+        closer, _, used = ctx.deep_filter(ux, uy, uz, deep_threshold=2.5 if k % 2 else -1.0, further=False)
+        wx, wy, wz = ctx.transform_cloud(*closer, m)
+        frames.append(tuple(a.cpu().numpy() for a in (wx, wy, wz)))
+        rc, _ = orc.deep_filter(*orc.unpack_pointcloud2(buf, 320, 240, 16, row_step).T, used)
+        ref_frames.append(tuple(orc.transform_cloud(*rc.T, m).T))
+    for f, r in zip(frames, ref_frames):
+        assert _same(np.stack(f, 1), np.stack(r, 1))
+    b = pitt.FrameBatch.from_host(frames)
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda")
+    res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+    inl = inl.cpu().numpy()
+    for i, (f, r) in enumerate(zip(ref_frames, res)):
+        o = orc.plane_segment(*f)
+        assert r["hypotheses"] == o.hypotheses and r["best_count"] == o.best_count
+        assert np.array_equal(inl[b.offsets[i]:b.offsets[i] + r["n_inliers"]], o.inliers)
+        assert np.array_equal(r["coefficients"][:r["n_coeff"]], o.coefficients)
