@@ -192,7 +192,8 @@ def main():
     launches, ms, nbytes = ctx.profile_get("k_score")
     n_empty, ms_empty, _ = ctx.profile_get("k_score:empty")
     if rank == 0:
-        for k in ("k_hypothesize", "k_score", "k_score:empty", "k_replay", "k_refine", "k_sel_mark", "k_sel_write"):
+        for k in ("k_hypothesize", "k_score", "k_score.first", "k_score:empty", "k_replay", "k_refine", "k_sel_mark",
+                  "k_sel_write"):
             n_, ms_, b_ = ctx.profile_get(k)
             log(f"[rank 0] {k:15s} launches {n_:5d}  {ms_ / roof_steps:8.3f} ms/batch  "
                 f"avg {ms_ / max(1, n_) * 1e3:9.1f} us  {b_ / max(1e-9, ms_) / 1e6:8.1f} GB/s")

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PITT_ABI_VERSION 1
+#define PITT_ABI_VERSION 2
 /* Points per scoring tile; frames are scored in tiles of this many points. */
 #define PITT_TILE_POINTS 2048
 
@@ -67,7 +67,8 @@ typedef struct {
     int32_t  optimize;        /* setOptimizeCoefficients                                     */
     int32_t  reduce_order;    /* PITT_REDUCE_*                                               */
     int32_t  div_mode;        /* PITT_DIV_*                                                  */
-    int32_t  sampler_slack;   /* extra sampler attempts beyond max_it+1 for rejected samples */
+    int32_t  sampler_slack;   /* sampler attempts beyond max_it+1 for rejected samples; at least  *
+                               * 1000 are always provided (getSamples' consecutive-draw limit)  */
 } pitt_sac_params;
 
 /* plane_segmentation_srv.cpp:19-21 defaults: th 0.007, 1000 iterations, seed 12345. */
@@ -221,9 +222,10 @@ int pitt_transform_cloud(pitt_ctx* ctx, const float* x, const float* y, const fl
  * resident little-endian PointCloud2 payload into SoA planes, row-major (point r * width + c at byte
  * r * row_step + c * point_step; x, y, z FLOAT32 at off_x, off_y, off_z).  Offsets, point_step and
  * row_step must be multiples of 4 and data 4-byte aligned; PointXYZ (point_step 16, offsets 0/4/8)
- * takes one 16-byte load per point. */
-int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int32_t width, int32_t height, int32_t point_step,
-                            int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
+ * takes one 16-byte load per point.  data_bytes is the payload size (msg.data.size()); a layout
+ * that would read past it is rejected with PITT_E_INVALID before any device access. */
+int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes, int32_t width, int32_t height,
+                            int32_t point_step, int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
                             float* x, float* y, float* z);
 
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */

@@ -143,7 +143,7 @@ SIGNATURES = {
     "pitt_deep_filter": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, _i64p, _vp, _vp, _vp,
                                 _i64p, _f32p]),
     "pitt_transform_cloud": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp]),
-    "pitt_unpack_pointcloud2": (_i32, [_vp, _vp, _i32, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "pitt_unpack_pointcloud2": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
     "pitt_find_supports": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.POINTER(SupportParams),
                                   ctypes.POINTER(SupportList)]),

@@ -35,7 +35,7 @@ class PittError(RuntimeError):
 
 def sac_params(threshold: float = 0.007, max_iterations: int = 1000, probability: float = 0.99,
                seed: int = 12345, optimize: bool = True, reduce_order: int = L.REDUCE_SSE2,
-               div_mode: int = L.DIV_EIGEN32, sampler_slack: int = 64) -> L.SacParams:
+               div_mode: int = L.DIV_EIGEN32, sampler_slack: int = 1000) -> L.SacParams:
     """SACSegmentation parameters (defaults: plane_segmentation_srv.cpp:19-21)."""
     p = L.SacParams()
     lib.pitt_sac_params_default(ctypes.byref(p))
@@ -199,6 +199,8 @@ class Context:
         return rc
 
     def set_stream(self, stream) -> None:
+        if getattr(self, "_inflight", None) is not None:  # finish the batch on the stream it was queued on
+            self.wait()
         handle = getattr(stream, "cuda_stream", stream)
         self._check(lib.pitt_set_stream(self.h, ctypes.c_void_p(handle or 0)), "pitt_set_stream")
 
@@ -235,18 +237,24 @@ class Context:
         """Enqueue a batch on this context's stream and return immediately; the returned record
         array is filled by wait().  One batch in flight per context."""
         p = params or sac_params()
+        # the previous batch completes into its own record array first (the C side would finish it
+        # inside the call below; doing it here keeps that array alive while it is written)
+        if getattr(self, "_inflight", None) is not None:
+            self.wait()
         res = np.zeros(batch.n_frames, RESULT_DTYPE)
         fr = batch.abi()
-        self._inflight = (res, fr, p, batch)  # keep the buffers alive until wait()
         ptr = ctypes.c_void_p(inliers_out.data_ptr()) if inliers_out is not None else ctypes.c_void_p()
         self._check(lib.pitt_plane_segment_batch_async(self.h, ctypes.byref(fr), ctypes.byref(p),
                                                        res.ctypes.data_as(ctypes.POINTER(L.PlaneResult)), ptr),
                     "pitt_plane_segment_batch_async")
+        self._inflight = (res, fr, p, batch)  # keep the buffers alive until wait()
         return res
 
     def wait(self) -> None:
-        self._check(lib.pitt_wait(self.h), "pitt_wait")
-        self._inflight = None
+        try:
+            self._check(lib.pitt_wait(self.h), "pitt_wait")
+        finally:
+            self._inflight = None
 
     def hypothesis_counts(self, frame: int, cap: int) -> np.ndarray:
         out = np.zeros(cap, np.int32)
@@ -310,7 +318,8 @@ class Context:
         import torch
         n = width * height
         x, y, z = (torch.empty(max(n, 1), dtype=torch.float32, device=data.device) for _ in range(3))
-        self._check(lib.pitt_unpack_pointcloud2(self.h, data.data_ptr(), width, height, point_step, row_step,
+        self._check(lib.pitt_unpack_pointcloud2(self.h, data.data_ptr(), data.numel() * data.element_size(), width,
+                                                height, point_step, row_step,
                                                 offsets[0], offsets[1], offsets[2], x.data_ptr(), y.data_ptr(),
                                                 z.data_ptr()), "pitt_unpack_pointcloud2")
         return x[:n], y[:n], z[:n]

@@ -40,14 +40,27 @@ __device__ __forceinline__ uint32_t hash64(uint64_t k) {
     return (uint32_t)k;
 }
 
+__device__ __forceinline__ bool finite3(float x, float y, float z) {
+    return isfinite(x) && isfinite(y) && isfinite(z);
+}
+
+// Grid origin: per-axis minimum over the FINITE points only (the oracle's and KdTreeFLANN's view:
+// a point with an infinite or NaN coordinate is never indexed, so it must not move the origin --
+// one -inf would otherwise overflow every cell index).  Grid-stride partial minima per block, then
+// one block combines them (k_minxyz_final).
+constexpr int kMinBlocks = 512;
+
 __global__ __launch_bounds__(kBlock) void k_minxyz(const float* __restrict__ x, const float* __restrict__ y,
-                                                   const float* __restrict__ z, int64_t n, float* __restrict__ mn) {
+                                                   const float* __restrict__ z, int64_t n, float* __restrict__ part) {
     __shared__ float s[3][kBlock / 64];
-    float a = INFINITY, b = INFINITY, c = INFINITY;  // fminf ignores NaN points
-    for (int64_t i = threadIdx.x; i < n; i += kBlock) {
-        a = fminf(a, x[i]);
-        b = fminf(b, y[i]);
-        c = fminf(c, z[i]);
+    float a = INFINITY, b = INFINITY, c = INFINITY;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const float px = x[i], py = y[i], pz = z[i];
+        if (finite3(px, py, pz)) {
+            a = fminf(a, px);
+            b = fminf(b, py);
+            c = fminf(c, pz);
+        }
     }
     for (int d = 32; d >= 1; d >>= 1) {
         a = fminf(a, __shfl_xor(a, d, 64));
@@ -57,19 +70,31 @@ __global__ __launch_bounds__(kBlock) void k_minxyz(const float* __restrict__ x, 
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { s[0][w] = a; s[1][w] = b; s[2][w] = c; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int i = 1; i < kBlock / 64; ++i) { a = fminf(a, s[0][i]); b = fminf(b, s[1][i]); c = fminf(c, s[2][i]); }
-        mn[0] = a; mn[1] = b; mn[2] = c;
+    if (threadIdx.x < 3) {
+        float m = s[threadIdx.x][0];
+        for (int i = 1; i < kBlock / 64; ++i) m = fminf(m, s[threadIdx.x][i]);
+        part[3 * blockIdx.x + threadIdx.x] = m;
     }
+}
+
+__global__ __launch_bounds__(64) void k_minxyz_final(const float* __restrict__ part, int nb, float* __restrict__ mn) {
+    float a = INFINITY, b = INFINITY, c = INFINITY;
+    for (int i = threadIdx.x; i < nb; i += 64) {
+        a = fminf(a, part[3 * i]);
+        b = fminf(b, part[3 * i + 1]);
+        c = fminf(c, part[3 * i + 2]);
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        a = fminf(a, __shfl_xor(a, d, 64));
+        b = fminf(b, __shfl_xor(b, d, 64));
+        c = fminf(c, __shfl_xor(c, d, 64));
+    }
+    if (threadIdx.x == 0) { mn[0] = a; mn[1] = b; mn[2] = c; }
 }
 
 __global__ void k_iota_cl(int32_t* __restrict__ v, int64_t n) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
         v[k] = (int32_t)k;
-}
-
-__device__ __forceinline__ bool finite3(float x, float y, float z) {
-    return isfinite(x) && isfinite(y) && isfinite(z);
 }
 
 struct Grid {
@@ -362,7 +387,13 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     PITT_HIP_TRY(hipMemsetAsync(CCNT, 0, ((size_t)hsize + 1) * 4, s));
     PITT_HIP_TRY(hipMemsetAsync(CUR, 0, (size_t)hsize * 4, s));
     PITT_HIP_TRY(hipMemsetAsync(SIZE, 0, N * 4, s));
-    hipLaunchKernelGGL(k_minxyz, dim3(1), dim3(kBlock), 0, s, X, Y, Z, n, MN);
+    {
+        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMinBlocks));
+        float* PART = (float*)ctx->buf("cl_minpart", (size_t)kMinBlocks * 3 * sizeof(float));
+        if (!PART) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
+        hipLaunchKernelGGL(k_minxyz, dim3(nb), dim3(kBlock), 0, s, X, Y, Z, n, PART);
+        hipLaunchKernelGGL(k_minxyz_final, dim3(1), dim3(64), 0, s, PART, nb, MN);
+    }
     hipLaunchKernelGGL(k_iota_cl, dim3(ew(n)), dim3(256), 0, s, PAR, n);
     Grid g{X, Y, Z, MN, 1.0 / cell, KEYS, SLOT, CCNT, hsize - 1};
     hipLaunchKernelGGL(k_cells, dim3(ew(n)), dim3(256), 0, s, g, n);

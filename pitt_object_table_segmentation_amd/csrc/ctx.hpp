@@ -29,6 +29,7 @@ struct DevBuf {
 
 struct ProfRec {
     std::string name;
+    std::string alias;  // optional second total the launch is also counted in (e.g. one chunk)
     hipEvent_t a = nullptr, b = nullptr;
     double bytes = 0;
 };
@@ -96,6 +97,9 @@ struct pitt_ctx {
     void prof_end(int rec);
     void prof_set_bytes(int rec, double bytes) {
         if (rec >= 0 && rec < (int)pending.size()) pending[(size_t)rec].bytes = bytes;
+    }
+    void prof_alias(int rec, const char* alias) {
+        if (rec >= 0 && rec < (int)pending.size()) pending[(size_t)rec].alias = alias;
     }
     int prof_collect();
 };

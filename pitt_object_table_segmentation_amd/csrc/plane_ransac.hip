@@ -22,12 +22,15 @@
 
 #include "ctx.hpp"
 #include "device_common.hpp"
+#include "score_list_asm.inc"
 
 #pragma clang fp contract(off)
 
 namespace pitt {
 
-constexpr int kMaxAttempts = 8192;
+// Sampler attempts per frame (table triples).  Only memory bounds it: the table is 12 B per attempt
+// and per distinct point count, generated on the host once per (n, seed, attempts).
+constexpr int kMaxAttempts = 1 << 24;
 
 struct FrameMeta {
     int64_t off;    // first point (multiple of 4)
@@ -353,6 +356,13 @@ __device__ __forceinline__ float4 lds_row(uint32_t addr) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// The same through a volatile read: it is issued where it stands (not sunk past a branch).
+__device__ __forceinline__ float4 lds_row_v(uint32_t addr) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = *(const volatile __attribute__((address_space(3))) f4v*)(uintptr_t)addr;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // PCL's count of one group for one hypothesis (A3 order, no FMA).
 template <int ORDER>
 __device__ __forceinline__ int count_group(float4 c, float x, float y, float z, float tv) {
@@ -388,9 +398,37 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
     return r;
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// The surviving hypotheses of group GR, compacted in ascending order into its 16-entry LDS list
+// (lb + 256 GR): entry k is scored in PCL's float order and its count written to lane 16 GR + k of
+// vc (PCL order A3, no FMA).  Hand-scheduled (tools/gen_score_asm.py -> score_list_asm.inc): two
+// entries per step as two interleaved chains, the next two rows already in flight, an odd list's
+// first entry alone; the lane of every count is an immediate (no m0), so the scalar work per entry
+// is its s_bcnt1 and half a loop test.
+template <int ORDER, int GR>
+__device__ __forceinline__ void score_list(uint32_t lb, int c, float x, float y, float z, float tv, int& vc) {
+    if (c == 0) return;
+    uint32_t base;  // ds_read's address operand lives in a VGPR
+    asm("v_mov_b32 %0, %1" : "=v"(base) : "s"(lb + 256u * GR));
+    float d0, t0, d1, t1;
+    uint64_t m0, m1;
+    uint32_t n0, n1;
+#define PITT_LIST_OPERANDS                                                                              \
+    : [d0] "=&v"(d0), [t0] "=&v"(t0), [d1] "=&v"(d1), [t1] "=&v"(t1), [m0] "=&s"(m0), [m1] "=&s"(m1),  \
+      [n0] "=&s"(n0), [n1] "=&s"(n1), [vc] "+v"(vc)                                                     \
+    : [base] "v"(base), [c] "s"(c), [x] "v"(x), [y] "v"(y), [z] "v"(z), [tv] "v"(tv), [L] "n"(16 * GR) \
+    : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69",  \
+      "v70", "v71", "scc", "memory"
+    if constexpr (ORDER == 0) asm volatile(PITT_SCORE_LIST_ASM_0 PITT_LIST_OPERANDS);
+    else if constexpr (ORDER == 1) asm volatile(PITT_SCORE_LIST_ASM_1 PITT_LIST_OPERANDS);
+    else asm volatile(PITT_SCORE_LIST_ASM_2 PITT_LIST_OPERANDS);
+#undef PITT_LIST_OPERANDS
+}
+
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
 template <int ORDER, bool BOX>
-__device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, int rem, float tv, int lane,
+__device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, SubPts& P, int rem, float tv, int lane,
                                           int32_t* __restrict__ wc, RowBox& tbox, float* __restrict__ gbox) {
     if (__builtin_expect(rem < kSub, 0)) {  // frame tail: points past it never count, never widen a box
 #pragma unroll
@@ -421,6 +459,7 @@ __device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, i
     }
     const RowGeo G = row_geo(B);
     const int rounds = (Hf + kRnd - 1) / kRnd;
+    const uint32_t lrow = (uint32_t)(uintptr_t)wl + 256u * (uint32_t)(lane >> 4);  // this lane's group list
     for (int r = 0; r < rounds; ++r) {
         const int hl = kRnd * r + (lane & (kRnd - 1));
         const float4 cr = cl[min(hl, Hf - 1)];
@@ -428,39 +467,22 @@ __device__ __forceinline__ void score_sub(const float4* cl, int Hf, SubPts& P, i
         const uint64_t valid = (((uint64_t)1 << nb) - 1) * 0x0001000100010001ull;
         const uint64_t need = __builtin_amdgcn_ballot_w64(!box_clear(G, cr, tv)) & valid;
         if (need == 0) continue;
-        // surviving pairs, group by group (the group's registers are static), hypotheses by
-        // set bit: the bit index is the count's lane 16 g + h', the coefficient row is read at a
-        // VGPR address (v_lshl_add) by LDS broadcast -- 6 scalar ops per pair, so the CU's one
-        // scalar unit keeps pace with its four SIMDs
+        // compaction: the surviving hypotheses of group g, in ascending order, into list slots
+        // 16 g + k (k = the bit's rank inside its 16-lane row)
+        const bool mine = (need >> lane) & 1u;
+        const uint32_t rowbits = (uint32_t)(need >> (lane & 48));
+        const int k = __builtin_popcount(rowbits & ((1u << (lane & 15)) - 1u));
+        if (mine) *(__attribute__((address_space(3))) f4v*)(uintptr_t)(lrow + 16u * (uint32_t)k) = f4v{cr.x, cr.y, cr.z, cr.w};
+        // each list in order; entry k's count lands in lane 16 g + k of vc
         int vc = 0;
-        uint32_t cbase;  // LDS byte address of row 16 r in a VGPR
-        asm("v_mov_b32 %0, %1" : "=v"(cbase) : "s"((uint32_t)(uintptr_t)(cl + kRnd * r)));
-#pragma unroll
-        for (int g = 0; g < kGPS; ++g) {
-            uint64_t bits = need & (0xFFFFull << (16 * g));
-            const uint32_t gbase = cbase - 256u * g;  // row of bit b: gbase + 16 b
-            // two pairs per trip when two are left: both coefficient reads behind one wait, two
-            // independent chains for the VALU
-            while (bits) {
-                int b0, b1;
-                asm("s_ff1_i32_b64 %0, %1" : "=s"(b0) : "s"(bits));
-                asm("s_bitset0_b64 %0, %1" : "+s"(bits) : "s"(b0));
-                if (bits) {
-                    asm("s_ff1_i32_b64 %0, %1" : "=s"(b1) : "s"(bits));
-                    asm("s_bitset0_b64 %0, %1" : "+s"(bits) : "s"(b1));
-                    const float4 c0 = lds_row(gbase + 16u * (uint32_t)b0);
-                    const float4 c1 = lds_row(gbase + 16u * (uint32_t)b1);
-                    const int n0 = count_group<ORDER>(c0, P.x[g], P.y[g], P.z[g], tv);
-                    const int n1 = count_group<ORDER>(c1, P.x[g], P.y[g], P.z[g], tv);
-                    vc = writelane(n0, b0, vc);
-                    vc = writelane(n1, b1, vc);
-                } else {
-                    const float4 c0 = lds_row(gbase + 16u * (uint32_t)b0);
-                    vc = writelane(count_group<ORDER>(c0, P.x[g], P.y[g], P.z[g], tv), b0, vc);
-                }
-            }
-        }
-        __hip_atomic_fetch_add(&wc[64 * r + lane], vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)wl);
+        score_list<ORDER, 0>(lb, __builtin_popcount((uint32_t)need & 0xFFFFu), P.x[0], P.y[0], P.z[0], tv, vc);
+        score_list<ORDER, 1>(lb, __builtin_popcount((uint32_t)(need >> 16) & 0xFFFFu), P.x[1], P.y[1], P.z[1], tv, vc);
+        score_list<ORDER, 2>(lb, __builtin_popcount((uint32_t)(need >> 32) & 0xFFFFu), P.x[2], P.y[2], P.z[2], tv, vc);
+        score_list<ORDER, 3>(lb, __builtin_popcount((uint32_t)(need >> 48)), P.x[3], P.y[3], P.z[3], tv, vc);
+        // back to the hypothesis lanes: lane 16 g + h' reads lane 16 g + k
+        const int got = __builtin_amdgcn_ds_bpermute(4 * ((lane & 48) + k), vc);
+        wc[64 * r + lane] += mine ? got : 0;
     }
 }
 
@@ -486,6 +508,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box,
     float* __restrict__ group_box) {
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
+    __shared__ float4 wlist[kScoreWaves][64];  // four 16-entry survivor lists, one per group
     __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -493,6 +516,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     const int it = blockIdx.x * kScoreWaves + w;
     if (it >= items) return;
     float4* cl = wcoef[w];
+    float4* wl = wlist[w];
     int32_t* wc = wcnt[w];
     float tv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
@@ -515,9 +539,9 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
-        score_sub<ORDER, BOX>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox, gb + s * kGPS * 8);
+        score_sub<ORDER, BOX>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox, gb + s * kGPS * 8);
         if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
-        score_sub<ORDER, BOX>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox, gb + (s + 1) * kGPS * 8);
+        score_sub<ORDER, BOX>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox, gb + (s + 1) * kGPS * 8);
     }
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
     asm volatile("" ::: "memory");
@@ -895,8 +919,6 @@ __device__ __forceinline__ void chain16(float& s, const float4& a, const float4&
           "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
 }
 
-typedef float f4v __attribute__((ext_vector_type(4)));
-
 // 8 x ds_read_b128 (32 consecutive floats from LDS byte address a), issued back to back.
 __device__ __forceinline__ void lds_read32(f4v (&v)[8], uint32_t a) {
     asm volatile(
@@ -1223,8 +1245,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     const int max_iter = p->max_iterations;
     const int hcap = max_iter >= 0 ? max_iter + 1 : 1;
     const int runnable_all = ((unsigned)max_iter * 10u) != 0u ? 1 : 0;
-    const int A = hcap + std::max(0, p->sampler_slack);
-    if (A > kMaxAttempts) return ctx->fail(PITT_E_INVALID, "max_iterations + sampler_slack exceeds 8191");
+    // getSamples gives up after 1000 consecutive rejected draws (sac_model.hpp); the table always
+    // covers that run past the last hypothesis, so a degenerate cloud ends in PCL's "no samples"
+    // outcome rather than in an exhausted table.
+    const int64_t A64 = (int64_t)hcap + std::max(1000, p->sampler_slack);
+    if (A64 > kMaxAttempts) return ctx->fail(PITT_E_INVALID, "max_iterations + sampler_slack exceeds 2^24");
+    const int A = (int)A64;
     const float thf = float_threshold(p->threshold);
     if ((int64_t)nf * tiles_max >= ((int64_t)1 << 31) || (int64_t)nf * hcap * tiles_max >= ((int64_t)1 << 40))
         return ctx->fail(PITT_E_INVALID, "batch too large (frames x tiles must stay below 2^31)");
@@ -1319,6 +1345,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     for (int c = 0, h0 = 0; c < nchunks; h0 += chunks[(size_t)c], ++c) {
         const int H = chunks[(size_t)c];
         rec = ctx->prof_begin("k_score", 0.0);
+        if (c == 0) ctx->prof_alias(rec, "k_score.first");  // the first chunk: every frame, H hypotheses
         score_recs.push_back(rec);
         auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
                            : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);

@@ -371,9 +371,9 @@ int pitt_deep_filter(pitt_ctx* ctx, const float* x, const float* y, const float*
     return pitt::deep_filter_impl(ctx, x, y, z, n, th, cx, cy, cz, n_closer, fx, fy, fz, n_further);
 }
 
-int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int32_t width, int32_t height, int32_t point_step,
-                            int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z, float* x, float* y,
-                            float* z) {
+int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes, int32_t width, int32_t height,
+                            int32_t point_step, int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
+                            float* x, float* y, float* z) {
     if (!ctx) return PITT_E_INVALID;
     const int64_t n = (int64_t)width * height;
     if (width < 0 || height < 0 || (n > 0 && (!data || !x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
@@ -383,6 +383,11 @@ int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int32_t width, int3
     if (point_step % 4 != 0 || row_step % 4 != 0 || ((uintptr_t)data & 3u) != 0 ||
         (height > 1 && row_step < (int64_t)width * point_step))
         return ctx->fail(PITT_E_INVALID, "point_step / row_step / alignment");
+    if (n > 0) {  // the last point's last field must lie inside the payload
+        const int32_t omax = std::max(off_x, std::max(off_y, off_z));
+        const int64_t need = (int64_t)(height - 1) * row_step + (int64_t)(width - 1) * point_step + omax + 4;
+        if (data_bytes < need) return ctx->fail(PITT_E_INVALID, "PointCloud2 payload shorter than its layout");
+    }
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
     const int xyz16 = point_step == 16 && off_x == 0 && off_y == 4 && off_z == 8 && row_step % 16 == 0 &&
                       ((uintptr_t)data & 15u) == 0;

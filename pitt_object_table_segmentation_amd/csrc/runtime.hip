@@ -93,6 +93,7 @@ int pitt_ctx::prof_begin(const char* name, double bytes) {
     if (!prof) return -1;
     pitt::ProfRec r;
     r.name = name;
+    r.alias.clear();
     r.bytes = bytes;
     for (hipEvent_t* e : {&r.a, &r.b}) {
         if (!event_pool.empty()) {
@@ -120,10 +121,17 @@ int pitt_ctx::prof_collect() {
         (void)hipEventElapsedTime(&ms, r.a, r.b);
         // a scoring chunk with no active frame (its k_score/k_replay launches only retire empty
         // blocks) is accounted apart: the roofline covers the launches that score tiles
-        pitt::ProfTotal& t = totals[r.name == "k_score" && r.bytes == 0.0 ? std::string("k_score:empty") : r.name];
+        const bool empty = r.name == "k_score" && r.bytes == 0.0;
+        pitt::ProfTotal& t = totals[empty ? std::string("k_score:empty") : r.name];
         t.launches += 1;
         t.ms += ms;
         t.bytes += r.bytes;
+        if (!r.alias.empty() && !empty) {
+            pitt::ProfTotal& u = totals[r.alias];
+            u.launches += 1;
+            u.ms += ms;
+            u.bytes += r.bytes;
+        }
         event_pool.push_back(r.a);
         event_pool.push_back(r.b);
     }
@@ -144,7 +152,7 @@ void pitt_sac_params_default(pitt_sac_params* p) {
     p->optimize = 1;             // :55
     p->reduce_order = PITT_REDUCE_SSE2;
     p->div_mode = PITT_DIV_EIGEN32;
-    p->sampler_slack = 64;
+    p->sampler_slack = 1000;     // >= getSamples' 1000-draw limit (sac_model.hpp)
 }
 
 int pitt_create(pitt_ctx** out, int hip_device) {
@@ -188,6 +196,10 @@ void pitt_destroy(pitt_ctx* ctx) {
 
 int pitt_set_stream(pitt_ctx* ctx, void* s) {
     if (!ctx) return PITT_E_INVALID;
+    // a batch in flight was queued on the old stream: finish it there before switching, so that
+    // its results are copied out and its scratch is not reused under it by the next batch
+    const int rc = pitt::finish_batch(ctx);
+    if (rc) return rc;
     ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
     return PITT_OK;
 }

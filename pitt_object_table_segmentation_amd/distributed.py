@@ -69,3 +69,39 @@ def gather_results(results: np.ndarray, frame_start: int, n_frames: int, device=
     dst = torch.empty(world * src.numel(), dtype=torch.uint8, device=src.device)
     dist.all_gather_into_tensor(dst, src)
     return unpack_records(dst.cpu().numpy(), n_frames)
+
+
+def gather_inliers(inliers: np.ndarray, counts: np.ndarray, device=None):
+    """Gather every rank's final inlier lists (optional part of config 4's exchange).
+
+    inliers: this rank's frames' ascending inlier indices, concatenated in frame order (int32);
+    counts:  inliers per frame of this rank (int64).  Returns (all_inliers, all_counts) over the
+    whole batch in frame order.  Two equal-size all_gathers (lengths, then zero-padded lists),
+    since RCCL has no variable-size gather.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    inliers = np.ascontiguousarray(inliers, np.int32)
+    counts = np.ascontiguousarray(counts, np.int64)
+    meta = torch.tensor([len(inliers), len(counts)], dtype=torch.int64, device=device)
+    metas = torch.empty(world * 2, dtype=torch.int64, device=meta.device)
+    dist.all_gather_into_tensor(metas, meta)
+    metas = metas.cpu().numpy().reshape(world, 2)
+    lmax, fmax = int(metas[:, 0].max()), int(metas[:, 1].max())
+    pad_i = np.zeros(max(lmax, 1), np.int32)
+    pad_i[:len(inliers)] = inliers
+    pad_c = np.zeros(max(fmax, 1), np.int64)
+    pad_c[:len(counts)] = counts
+    src_i = torch.from_numpy(pad_i).to(device)
+    src_c = torch.from_numpy(pad_c).to(device)
+    dst_i = torch.empty(world * src_i.numel(), dtype=torch.int32, device=src_i.device)
+    dst_c = torch.empty(world * src_c.numel(), dtype=torch.int64, device=src_c.device)
+    dist.all_gather_into_tensor(dst_i, src_i)
+    dist.all_gather_into_tensor(dst_c, src_c)
+    all_i = dst_i.cpu().numpy().reshape(world, -1)
+    all_c = dst_c.cpu().numpy().reshape(world, -1)
+    out_i = np.concatenate([all_i[r, :metas[r, 0]] for r in range(world)]) if world else np.zeros(0, np.int32)
+    out_c = np.concatenate([all_c[r, :metas[r, 1]] for r in range(world)]) if world else np.zeros(0, np.int64)
+    return out_i, out_c

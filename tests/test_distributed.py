@@ -1,6 +1,6 @@
-"""World-size-2 `gloo` test of the frame-sharded gather (the multi-GPU path's only collective):
-each rank holds the result records of its contiguous shard; after gather_results every rank sees
-all frames in frame order, equal to the single-process list."""
+"""World-size-2 `gloo` tests of the frame-sharded path (config 4).  CPU: the gather of fixed-size
+records and of variable-length inlier lists (the multi-GPU path's only collectives).  GPU: the
+whole shard -> segment -> gather path on the HIP kernels, byte-equal to one single-batch run."""
 import os
 import socket
 
@@ -39,7 +39,12 @@ def _worker(rank, world, port, n_frames, out_q):
         allrec = _records(n_frames)
         s, e = distributed.shard_range(n_frames, world, rank)
         got = distributed.gather_results(allrec[s:e], s, n_frames, device="cpu")
-        out_q.put((rank, got.tobytes() == allrec.tobytes()))
+        rng = np.random.default_rng(7)
+        cnt = rng.integers(0, 50, n_frames)
+        lists = [np.sort(rng.choice(1000, c, replace=False)).astype(np.int32) for c in cnt]
+        gi, gc = distributed.gather_inliers(np.concatenate(lists[s:e] + [np.zeros(0, np.int32)]), cnt[s:e], device="cpu")
+        ok_inl = gi.tobytes() == np.concatenate(lists).tobytes() and np.array_equal(gc, cnt)
+        out_q.put((rank, got.tobytes() == allrec.tobytes() and ok_inl))
     finally:
         dist.destroy_process_group()
 
@@ -57,3 +62,68 @@ def test_gloo_world2_gather(n_frames):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+# ---- config 4 on the HIP path: shard -> segment (own context per rank) -> gather ----------------
+def _sharded_frames(n_frames):
+    frames = []
+    for f in range(n_frames):
+        scene = (pitt.SCENE_TABLE, pitt.SCENE_CLUTTER, pitt.SCENE_TABLE_NAN)[f % 3]
+        w, h = ((320, 240), (160, 120), (640, 480))[f % 3]
+        frames.append(pitt.synth_frame(scene, 2000 + f, w, h))
+    return frames
+
+
+def _hip_worker(rank, world, port, n_frames, out_q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = _sharded_frames(n_frames)
+        s, e = distributed.shard_range(n_frames, world, rank)
+        with pitt.Context(0) as ctx:
+            b = pitt.FrameBatch.from_host(frames[s:e], device="cuda:0")
+            inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+            res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+            inl = inl.cpu().numpy()
+            mine = np.concatenate([inl[o:o + r["n_inliers"]] for o, r in zip(b.offsets, res)] + [np.zeros(0, np.int32)])
+        got = distributed.gather_results(res, s, n_frames, device="cpu")
+        all_inl, all_cnt = distributed.gather_inliers(mine, res["n_inliers"].astype(np.int64), device="cpu")
+        out_q.put((rank, got.tobytes(), all_inl.tobytes(), all_cnt.tobytes()))
+    except Exception as ex:  # report instead of hanging the parent
+        out_q.put((rank, repr(ex), b"", b""))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_config4_sharded_hip_path_equals_single_batch(ctx):
+    """SURVEY s4 / BASELINE config 4 on one GPU: the frame set split by shard_range over a gloo
+    world of 2, each rank segmenting its shard through its own Context on the HIP path, then the
+    per-frame records and the inlier lists gathered -- byte-equal to one plane_segment_batch over
+    every frame (and so to the oracle, which test_plane_gpu pins frame by frame)."""
+    import torch
+    n_frames, world = 7, 2
+    frames = _sharded_frames(n_frames)
+    b = pitt.FrameBatch.from_host(frames, device="cuda:0")
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+    ref = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+    inl = inl.cpu().numpy()
+    ref_inl = np.concatenate([inl[o:o + r["n_inliers"]] for o, r in zip(b.offsets, ref)])
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    port = _free_port()
+    procs = [mctx.Process(target=_hip_worker, args=(r, world, port, n_frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, recs, ginl, gcnt in got:
+        assert isinstance(recs, bytes), recs
+        assert recs == ref.tobytes(), f"rank {rank}: gathered records differ"
+        assert ginl == ref_inl.tobytes(), f"rank {rank}: gathered inlier lists differ"
+        assert gcnt == ref["n_inliers"].astype(np.int64).tobytes()
+    assert sorted(r for r, *_ in got) == [0, 1]

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(header):
 
 
 def test_abi_version():
-    assert _lib.lib.pitt_abi_version() == 1
+    assert _lib.lib.pitt_abi_version() == 2
 
 
 @pytest.mark.parametrize("n", [3, 5, 4800, 307200, 1228800])
@@ -120,4 +120,4 @@ def test_preprocessing_entry_points_reject_null_context():
     assert lib.pitt_deep_filter(None, None, None, None, 0, -1.0, None, None, None, None, None, None, None, None,
                                 None) == L.PITT_E_INVALID
     assert lib.pitt_transform_cloud(None, None, None, None, 0, m, 1, None, None, None) == L.PITT_E_INVALID
-    assert lib.pitt_unpack_pointcloud2(None, None, 0, 0, 16, 0, 0, 4, 8, None, None, None) == L.PITT_E_INVALID
+    assert lib.pitt_unpack_pointcloud2(None, None, 0, 0, 0, 16, 0, 0, 4, 8, None, None, None) == L.PITT_E_INVALID

@@ -165,6 +165,12 @@ def test_unpack_pointcloud2_rejects_bad_layout(ctx):
         ctx.unpack_pointcloud2(buf, 2, 1, 16, 32, (0, 4, 14))   # field past point_step
     with pytest.raises(pitt.PittError):
         ctx.unpack_pointcloud2(buf, 2, 2, 16, 16, (0, 4, 8))    # row_step shorter than a row
+    with pytest.raises(pitt.PittError):
+        ctx.unpack_pointcloud2(buf, 5, 1, 16, 80, (0, 4, 8))    # 5 points need 76 B, the payload has 64
+    with pytest.raises(pitt.PittError):
+        ctx.unpack_pointcloud2(buf, 2, 2, 16, 40, (0, 4, 8))    # second row ends at byte 68
+    x, y, z = ctx.unpack_pointcloud2(buf, 4, 1, 16, 64, (0, 4, 8))  # exactly fits: 60 B needed
+    assert x.numel() == 4
 
 
 def test_preprocessed_frames_through_plane_batch(ctx):

@@ -54,6 +54,22 @@ def test_support_parameter_variants(ctx):
         _compare_supports(dev, orc.find_supports(x, y, z, **kw))
 
 
+def test_find_supports_degenerate_cloud_small_max_iterations(ctx):
+    """A cloud on one exact line: every sample is collinear, getSamples gives up after 1000 draws and
+    RANSAC returns no model, so the support loop ends normally with no support (the sampler table
+    always covers those 1000 draws, even at the support service's max_iterations of 10)."""
+    t = (np.arange(5000) * 0.25).astype(np.float32)
+    x, y, z = t, np.float32(2) * t, np.float32(3) * t
+    for it in (10, 1):
+        dev = ctx.find_supports(x, y, z, pitt.support_params(ransac_max_iterations=it))
+        ref = orc.find_supports(x, y, z, ransac_max_iterations=it)
+        assert len(dev) == len(ref) == 0
+    b = pitt.FrameBatch.from_host([(x, y, z)])
+    res = ctx.plane_segment_batch(b, pitt.sac_params(max_iterations=10))
+    assert res[0]["status"] == pitt.PITT_NO_MODEL and res[0]["n_coeff"] == 0
+    assert res[0]["rejected_samples"] == 1000
+
+
 def _blob(center, n_side, step=0.01):
     g = np.stack(np.meshgrid(*(np.arange(n_side) * step,) * 3), -1).reshape(-1, 3)
     return (g + np.asarray(center)).astype(np.float32)
@@ -64,20 +80,39 @@ def test_clusters_known_layouts(ctx):
     blobs = [_blob(rng.uniform(-1, 1, 3) * 3, int(rng.integers(2, 8))) for _ in range(30)]
     xyz = np.concatenate(blobs)
     xyz = xyz[rng.permutation(len(xyz))]
-    for min_size, max_size in ((1, 10 ** 9), (9, 200), (100, 100)):
+    n = len(xyz)
+    for min_size, max_size in ((1, 10 ** 9), (9, 200), (100, 100), (27, 64), (200, 10 ** 9)):
         dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=min_size, max_size=max_size)
-        n = len(xyz)
-        ref = orc.euclidean_clusters(*xyz.T, min_rate=min_size / n, max_rate=max_size / n, min_input_size=0)
-        # the oracle's rates round back to exactly these sizes only when n divides evenly; compare
-        # the size-filtered components directly
+        # round(n * (m / n)) == m in double for these sizes, so the oracle applies the same filter
+        ref = orc.euclidean_clusters(*xyz.T, min_rate=min_size / n, max_rate=min(max_size, n) / n, min_input_size=0)
+        assert [len(c.indices) for c in dev] == [len(c["inliers"]) for c in ref]
+        for a, b in zip(dev, ref):
+            assert np.array_equal(a.indices, b["inliers"])
+            assert np.array_equal(a.sum_xyz / np.float32(len(a.indices) + 1), b["centroid"])
         sizes = [len(c.indices) for c in dev]
         assert all(min_size <= s <= max_size for s in sizes)
         assert sizes == sorted(sizes, reverse=True)
     dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=1, max_size=10 ** 9)
-    ref = orc.euclidean_clusters(*xyz.T, min_rate=0.0, max_rate=1.0, min_input_size=0)
-    assert len(dev) == len(ref) == 30
-    for a, b in zip(dev, ref):
-        assert np.array_equal(a.indices, b["inliers"])
+    assert len(dev) == 30
+
+
+def test_clusters_nonfinite_points(ctx):
+    """Points with +-inf or NaN coordinates are never indexed (KdTreeFLANN drops them): they are
+    singletons and must not move the grid origin (one -inf would overflow every cell index)."""
+    rng = np.random.default_rng(9)
+    blobs = [_blob(rng.uniform(-1, 1, 3), int(rng.integers(2, 6))) for _ in range(12)]
+    xyz = np.concatenate(blobs)
+    bad = np.array([[-np.inf, 0, 0], [0, np.inf, 0], [0, 0, -np.inf], [np.nan, 1, 1], [np.inf, -np.inf, np.nan],
+                    [-np.inf, -np.inf, -np.inf]], np.float32)
+    pos = np.sort(rng.choice(len(xyz) + len(bad), len(bad), replace=False))
+    xyz = np.insert(xyz, pos - np.arange(len(bad)), bad, axis=0)
+    n = len(xyz)
+    for min_size in (1, 2):
+        dev = ctx.euclidean_clusters(*xyz.T, tolerance=0.03, min_size=min_size, max_size=10 ** 9)
+        ref = orc.euclidean_clusters(*xyz.T, min_rate=min_size / n, max_rate=1.0, min_input_size=0)
+        assert [list(c.indices) for c in dev] == [list(c["inliers"]) for c in ref]
+        if min_size == 2:
+            assert len(dev) == 12
 
 
 def test_clusters_ties_many_equal_sizes(ctx):

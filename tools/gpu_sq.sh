@@ -18,3 +18,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_I
     SQ_BUSY_CYCLES SQ_INST_CYCLES_SALU --kernel-include-regex "$KRE" \
     -d "$OUT/sq_${TAG}_b" -o b -f csv -- python3 $BENCH > "$OUT/sq_${TAG}_b.log" 2>&1 || exit $?
 echo done > "$OUT/sq_${TAG}_done"
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH \
+    SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --kernel-include-regex "$KRE" \
+    -d "$OUT/sq_${TAG}_c" -o c -f csv -- python3 $BENCH > "$OUT/sq_${TAG}_c.log" 2>&1 || exit $?
+echo done > "$OUT/sq_${TAG}_done"
