@@ -226,6 +226,10 @@ constexpr int kWaves = kBlock / 64;
 #endif
 constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score block
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
+#ifndef PITT_SCORE_GRID_CAP
+#define PITT_SCORE_GRID_CAP (256 * 32)
+#endif
+constexpr int kScoreGridCap = PITT_SCORE_GRID_CAP;  // blocks of a later chunk's launch (~ resident capacity)
 
 struct SubPts {
     float x[kGPS], y[kGPS], z[kGPS];
@@ -429,25 +433,21 @@ __device__ __forceinline__ void score_list(uint32_t lb, int c, float x, float y,
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
 template <int ORDER, bool BOX>
 __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, SubPts& P, int rem, float tv, int lane,
-                                          int32_t* __restrict__ wc, RowBox& tbox, float* __restrict__ gbox) {
+                                          int32_t* __restrict__ wc, float& tb, float* __restrict__ gbox,
+                                          uint32_t gsrc) {
     if (__builtin_expect(rem < kSub, 0)) {  // frame tail: points past it never count, never widen a box
 #pragma unroll
         for (int g = 0; g < kGPS; ++g)
             if (g * kGrp + lane >= rem) P.x[g] = P.y[g] = P.z[g] = __builtin_nanf("");
     }
     RowBox B;
-    coord_box(P.x[0], P.x[1], P.x[2], P.x[3], B.lo[0], B.hi[0]);
-    coord_box(P.y[0], P.y[1], P.y[2], P.y[3], B.lo[1], B.hi[1]);
-    coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
-    row_reduce(B);
     if constexpr (BOX) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            tbox.lo[k] = vmin(tbox.lo[k], B.lo[k]);
-            tbox.hi[k] = vmax(tbox.hi[k], B.hi[k]);
-        }
-        // the four groups' boxes for the final selection's group skipping: lane 16 g + i (i < 6)
-        // stores value i of group g (one masked store per sub-step)
+        coord_box(P.x[0], P.x[1], P.x[2], P.x[3], B.lo[0], B.hi[0]);
+        coord_box(P.y[0], P.y[1], P.y[2], P.y[3], B.lo[1], B.hi[1]);
+        coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
+        row_reduce(B);
+        // the four groups' boxes, for the later chunks and the final selection: lane 16 g + i (i < 6)
+        // holds value i of group g, stores it, and folds it into the tile box (min for lo, max for hi)
         const int i = lane & 15;
         float v = B.lo[0];
         v = i == 1 ? B.lo[1] : v;
@@ -456,6 +456,20 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         v = i == 4 ? B.hi[1] : v;
         v = i == 5 ? B.hi[2] : v;
         if (i < 6) gbox[(lane >> 4) * 8 + i] = v;
+        tb = i < 3 ? vmin(tb, v) : vmax(tb, v);
+    } else {
+        // later chunks: the boxes the first chunk stored, staged in LDS at the item's start (row g of
+        // the row layout = group g: a broadcast read per row, no reduction)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const uint32_t a = gsrc + 32u * (uint32_t)(lane >> 4);
+        const f4v q = *(const __attribute__((address_space(3))) f4v*)(uintptr_t)a;
+        const f2v r = *(const __attribute__((address_space(3))) f2v*)(uintptr_t)(a + 16u);
+        B.lo[0] = q.x;
+        B.lo[1] = q.y;
+        B.lo[2] = q.z;
+        B.hi[0] = q.w;
+        B.hi[1] = r.x;
+        B.hi[2] = r.y;
     }
     const RowGeo G = row_geo(B);
     const int rounds = (Hf + kRnd - 1) / kRnd;
@@ -509,39 +523,43 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     float* __restrict__ group_box) {
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
     __shared__ float4 wlist[kScoreWaves][64];  // four 16-entry survivor lists, one per group
+    __shared__ float4 wbox[kScoreWaves][BOX ? 1 : 64];  // later chunks: the item's 32 group boxes
     __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
-    const int it = blockIdx.x * kScoreWaves + w;
-    if (it >= items) return;
     float4* cl = wcoef[w];
     float4* wl = wlist[w];
     int32_t* wc = wcnt[w];
     float tv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));  // threshold in a VGPR (full-rate v_cmp)
+    // items strided over the grid: the grid is sized for the whole batch but capped near the chip's
+    // resident capacity, so a later chunk with few active frames (or none) retires quickly
+    for (int it = blockIdx.x * kScoreWaves + w; it < items; it += gridDim.x * kScoreWaves) {
     const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H);
     const int Hf = cur.h;
-    if (Hf <= 0) return;  // an empty item, or a frame that needs none of this chunk
+    if (Hf <= 0) continue;  // an empty item, or a frame that needs none of this chunk
     const int rounds = (Hf + kRnd - 1) / kRnd;
     SubPts P[2];
     load_sub(X, Y, Z, cur.base, lane, P[0]);
     put_coefs<NST>(cl, hyp_coef + (int64_t)cur.f * hcap + h0, Hf, lane);
     for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
-    float* gb = group_box + ((int64_t)cur.f * tiles_max + cur.t) * (kTile / kGrp) * 8;  // BOX only
-    RowBox tbox;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        tbox.lo[k] = __builtin_inff();
-        tbox.hi[k] = -__builtin_inff();
+    float* gb = group_box + ((int64_t)cur.f * tiles_max + cur.t) * (kTile / kGrp) * 8;
+    if constexpr (!BOX) {  // the tile's 32 group boxes (1 KB, written by the first chunk) into LDS
+        const float4 q = reinterpret_cast<const float4*>(gb)[lane];
+        wbox[w][lane] = q;
     }
+    const uint32_t gsrc = (uint32_t)(uintptr_t)wbox[w];
+    float tb = (lane & 15) < 3 ? __builtin_inff() : -__builtin_inff();  // BOX: this lane's tile-box value
     // sub-steps in pairs: the next sub-step loads into the other register set while this one is
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
-        score_sub<ORDER, BOX>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tbox, gb + s * kGPS * 8);
+        score_sub<ORDER, BOX>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
+                              gsrc + 128u * s);
         if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
-        score_sub<ORDER, BOX>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tbox, gb + (s + 1) * kGPS * 8);
+        score_sub<ORDER, BOX>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
+                              gsrc + 128u * (s + 1));
     }
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
     asm volatile("" ::: "memory");
@@ -555,19 +573,14 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
         }
     }
     if constexpr (BOX) {
-        // rows -> tile: the four rows' boxes combined (xor 16, xor 32 through ds_bpermute)
-        float v[6] = {tbox.lo[0], tbox.lo[1], tbox.lo[2], tbox.hi[0], tbox.hi[1], tbox.hi[2]};
+        // rows -> tile: value i of the four rows combined (xor 16, xor 32)
 #pragma unroll
-        for (int off = 16; off <= 32; off <<= 1)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const float o = __shfl_xor(v[k], off, 64);
-                v[k] = k < 3 ? vmin(v[k], o) : vmax(v[k], o);
-            }
-        float b = v[0];
-#pragma unroll
-        for (int k = 1; k < 6; ++k) b = lane == k ? v[k] : b;
-        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = b;
+        for (int off = 16; off <= 32; off <<= 1) {
+            const float o = __shfl_xor(tb, off, 64);
+            tb = (lane & 15) < 3 ? vmin(tb, o) : vmax(tb, o);
+        }
+        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = tb;
+    }
     }
 }
 
@@ -1349,7 +1362,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         score_recs.push_back(rec);
         auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
                            : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
-        const int score_blocks = (int)(((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves);
+        // the first chunk scores every frame (one item per wave); later ones stride over a capped grid
+        const int64_t all_blocks = ((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves;
+        const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
                            tile_box, group_box);
