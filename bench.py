@@ -3,19 +3,30 @@
 One step = one batch of synthetic 640x480 table-scene clouds per GPU (256 by default, BASELINE
 config 3) through pitt_plane_segment_batch: hypotheses, adaptive RANSAC scoring, refinement and
 the final ascending inlier list, results on the host; with N > 1 ranks the per-frame result
-records are gathered over RCCL (config 4).  Inputs are resident in HBM before the timed region.
+records are gathered over RCCL (config 4).  Inputs are resident in HBM before the timed region;
+each in-flight context segments its own batch (distinct frames, no cross-batch cache reuse).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.  Roofline figures are for the dominant kernel (k_score, the
-inlier-scoring kernel): algorithmic bytes = 12 B per point of every (active frame, tile) a launch
-reads, divided by its average launch time measured with HIP events on its stream.
+Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, N = 1):
+  roofline      k_score, the inlier-scoring kernel: algorithmic bytes (12 B per point of every
+                (active frame, tile) a launch reads) / its average launch time, HIP events on its
+                stream over a pass with one batch in flight
+  kernels       every kernel of the batch with the bytes it actually moved (device-counted for
+                the data-dependent ones) and its launch time
+  clutter       a clutter-scene batch (T = 1001 hypotheses per frame) against the VALU roof
+  pcie_fed      frames/s when every batch starts in pinned host memory (H2D copy in the step)
+  config5       find_supports + euclidean_clusters on the 1.2M-point fused scene, GPU vs oracle
+  cpu_baseline  the oracle (CPU restatement of PCL's path) on the host: frame-parallel on the
+                host's CPU share, and single-core per-frame medians (config 1)
 """
 import argparse
 import concurrent.futures as cf
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -26,23 +37,63 @@ sys.path.insert(0, ROOT)
 
 METRIC = "RANSAC frames/sec on 307k-pt clouds @1/2/4/8 GPU; inlier-kernel HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+# non-FMA f32 VALU ops/s: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz (157.3 TFLOPS counts an FMA as 2)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 W, H = 640, 480
+KERNELS = ("k_hypothesize", "k_score", "k_score.first", "k_score:empty", "k_replay", "k_refine", "k_sel_mark",
+           "k_sel_write")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_frames(ids, threads):
+def host_cpus():
+    """CPUs of this host and the share this process may use: sched affinity, the cgroup CPU quota,
+    and OMP_NUM_THREADS (the GPU box sets it to the box's CPU share)."""
+    info = {"affinity": len(os.sched_getaffinity(0))}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("CPU(s):"):
+                info["lscpu"] = int(ln.split(":")[1])
+            elif ln.startswith("Model name:"):
+                info["model"] = ln.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError, ValueError):
+        pass
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota"] = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    share = info["affinity"]
+    if "cgroup_quota" in info:
+        share = min(share, max(1, math.floor(info["cgroup_quota"])))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    info["share"] = max(1, share)
+    return info
+
+
+def make_frames(ids, threads, scene=None):
     import pitt_object_table_segmentation_amd as pitt
+    scene = pitt.SCENE_TABLE if scene is None else scene
     with cf.ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL
-        return list(ex.map(lambda i: pitt.synth_frame(pitt.SCENE_TABLE, 1000 + int(i), W, H), ids))
+        return list(ex.map(lambda i: pitt.synth_frame(scene, 1000 + int(i), W, H), ids))
 
 
-def cpu_baseline(frames, threads, budget_s):
-    """The oracle (CPU restatement of the reference's PCL path) timed on this host's cores."""
+def oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_binding as orc
+    return orc
+
+
+def cpu_baseline(frames, clutter_frame, cpus, budget_s):
+    """The oracle (CPU restatement of the reference's PCL path): frame-parallel over the host's CPU
+    share for ~budget_s, then single-core per-frame medians of 5 repeats after 1 warm-up."""
+    orc = oracle()
+    threads = cpus["share"]
     done = 0
     t0 = time.perf_counter()
 
@@ -56,10 +107,26 @@ def cpu_baseline(frames, threads, budget_s):
             done += sum(ex.map(one, range(k, k + threads * 4)))
             k += threads * 4
     dt = time.perf_counter() - t0
+
+    def median_ms(fr, reps=5):
+        orc.plane_segment(*fr)
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            o = orc.plane_segment(*fr)
+            ts.append((time.perf_counter() - t) * 1e3)
+        return round(float(np.median(ts)), 2), o.hypotheses
+
+    table_ms, table_t = median_ms(frames[0])
+    clutter_ms, clutter_t = median_ms(clutter_frame)
     return dict(value=round(done / dt, 2), unit="frames/s", cores=threads, kind="port",
                 sample=f"{done} frames cycled over the first {len(frames)} synthetic 640x480 table frames, "
-                       f"{dt:.1f} s wall, frame-parallel over {threads} threads (oracle/pitt_oracle.cpp, "
-                       f"g++ -O2, PCL-equivalent single-threaded segment() per frame)")
+                       f"{dt:.1f} s wall, frame-parallel over {threads} threads = the host's CPU share "
+                       f"(oracle/pitt_oracle.cpp, g++ -O2, PCL-equivalent single-threaded segment() per frame)",
+                single_core={"config1_table_ms_per_frame": table_ms, "table_hypotheses": int(table_t),
+                             "clutter_ms_per_frame": clutter_ms, "clutter_hypotheses": int(clutter_t),
+                             "statistic": "median of 5 after 1 warm-up, one thread"},
+                host=cpus)
 
 
 def pmc_traffic():
@@ -74,6 +141,126 @@ def pmc_traffic():
         return None
 
 
+def kernel_table(ctx, batches):
+    out = {}
+    for k in KERNELS:
+        n, ms, b = ctx.profile_get(k)
+        if n == 0:
+            continue
+        out[k] = {"launches_per_batch": round(n / batches, 2), "us_per_batch": round(ms / batches * 1e3, 1),
+                  "avg_launch_us": round(ms / n * 1e3, 1), "GBps": round(b / max(1e-9, ms) / 1e6, 1)}
+    return out
+
+
+def clutter_pass(pitt, ctx, dev, threads, frames_n=64, steps=3):
+    """BASELINE sec. 3: the clutter scene (table on ~8 % of pixels) runs all 1001 hypotheses per frame;
+    algorithmic VALU work = 1001 x 7 ops (3 mul, 3 add, compare) x 307,200 points per frame."""
+    import torch
+    frames = make_frames(range(frames_n), threads, pitt.SCENE_CLUTTER)
+    b = pitt.FrameBatch.from_host(frames, device=dev)
+    out = torch.empty(b.capacity, dtype=torch.int32, device=dev)
+    p = pitt.sac_params()
+    res = ctx.plane_segment_batch(b, p, out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = ctx.plane_segment_batch(b, p, out)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    hyps = float(np.mean(res["hypotheses"]))
+    ops = hyps * 7 * W * H
+    achieved = ops * frames_n / dt / 1e12
+    return frames, {"frames": frames_n, "frames_per_s": round(frames_n / dt, 1),
+                    "ms_per_batch": round(dt * 1e3, 3), "hypotheses_per_frame_mean": round(hyps, 1),
+                    "valu_roof": {"ops_per_frame": round(ops), "achieved_Tops": round(achieved, 2),
+                                  "peak_Tops": round(VALU_PEAK_TOPS, 1), "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                                  "note": "algorithmic ops (every point x every hypothesis); the kernel culls "
+                                          "(group, hypothesis) pairs by certified box tests, so it executes fewer"}}
+
+
+def pcie_pass(pitt, ctxs, host_batches, dev, params, steps):
+    """Every step's batch starts in pinned host memory: H2D copy on the context's stream, then the
+    batch; the copy of one batch overlaps the kernels of the others."""
+    import torch
+    streams = [torch.cuda.Stream(device=dev) for _ in ctxs]
+    dev_planes = []
+    for hb in host_batches:
+        dev_planes.append([torch.empty_like(t, device=dev) for t in (hb.x, hb.y, hb.z)])
+    outs = [torch.empty(hb.capacity, dtype=torch.int32, device=dev) for hb in host_batches]
+    for c, s in zip(ctxs, streams):
+        c.set_stream(s)
+    pending = [False] * len(ctxs)
+
+    def step(i):
+        j = i % len(ctxs)
+        c, s, hb = ctxs[j], streams[j], host_batches[j]
+        if pending[j]:
+            c.wait()
+        with torch.cuda.stream(s):
+            for d, h in zip(dev_planes[j], (hb.x, hb.y, hb.z)):
+                d.copy_(h, non_blocking=True)
+        b = pitt.FrameBatch(dev_planes[j][0], dev_planes[j][1], dev_planes[j][2], hb.offsets, hb.counts, hb.capacity)
+        c.plane_segment_batch_async(b, params, outs[j])
+        pending[j] = True
+
+    for i in range(len(ctxs)):
+        step(i)
+    for j, c in enumerate(ctxs):
+        c.wait()
+        pending[j] = False
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    for j, c in enumerate(ctxs):
+        if pending[j]:
+            c.wait()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    for c in ctxs:
+        c.set_stream(None)
+    frames = sum(hb.n_frames for hb in host_batches) // len(host_batches)
+    nbytes = sum(t.numel() * 4 for t in (host_batches[0].x, host_batches[0].y, host_batches[0].z))
+    return {"frames_per_s": round(frames * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+            "h2d_bytes_per_batch": nbytes, "h2d_GBps": round(nbytes * steps / dt / 1e9, 1), "steps": steps}
+
+
+def config5_pass(pitt, ctx, threads, reps=5):
+    """BASELINE config 5: find_supports (th 0.02f, 10 iterations) on the 1.2M-point fused scene, then
+    euclidean_clusters (0.03 m, 1 % / 99 %) on every support's on-support cloud; host arrays in and
+    out (the service boundary), GPU median of `reps` vs the oracle once, results compared."""
+    orc = oracle()
+    x, y, z = pitt.synth_fused(1000, 4)
+
+    def gpu_once():
+        sups = ctx.find_supports(x, y, z)
+        cl = []
+        for s in sups:
+            n = len(s.on_support_cloud)
+            cl.append(ctx.euclidean_clusters(*s.on_support_cloud.T, tolerance=0.03,
+                                             min_size=int(np.floor(n * 0.01 + 0.5)),
+                                             max_size=int(np.floor(n * 0.99 + 0.5))) if n >= 30 else [])
+        return sups, cl
+
+    gpu_once()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        sups, cl = gpu_once()
+        ts.append((time.perf_counter() - t) * 1e3)
+    t = time.perf_counter()
+    rs = orc.find_supports(x, y, z)
+    rcl = [orc.euclidean_clusters(*s["on_support_cloud"].T) for s in rs]
+    cpu_ms = (time.perf_counter() - t) * 1e3
+    same = (len(rs) == len(sups) and all(np.array_equal(a.idx_map, b["idx_map"]) for a, b in zip(sups, rs)) and
+            all(len(a) == len(b) and all(np.array_equal(p.indices, q["inliers"]) for p, q in zip(a, b))
+                for a, b in zip(cl, rcl)))
+    return {"points": int(len(x)), "supports": len(sups), "clusters": int(sum(len(c) for c in cl)),
+            "gpu_ms_per_scene": round(float(np.median(ts)), 2), "gpu_statistic": f"median of {reps} after 1 warm-up",
+            "cpu_ms_per_scene": round(cpu_ms, 1), "cpu": "oracle, one thread, O(N) restatement of the loop",
+            "matches_oracle": bool(same)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,9 +269,9 @@ def main():
     ap.add_argument("--frames-per-gpu", type=int, default=256)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the clutter / PCIe / config-5 passes")
     ap.add_argument("--no-inliers", action="store_true", help="skip writing the final inlier lists")
     ap.add_argument("--pipeline", type=int, default=3, help="contexts/streams with batches in flight")
-    ap.add_argument("--torch-streams", action="store_true", help="run contexts on torch streams")
     args = ap.parse_args()
 
     import torch
@@ -97,30 +284,36 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        backend = dist.get_backend()
+        log(f"[rank {rank}] torch.distributed backend {backend} (RCCL), world size {dist.get_world_size()}")
 
     import pitt_object_table_segmentation_amd as pitt
     from pitt_object_table_segmentation_amd import distributed
 
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 8))))
+    cpus = host_cpus()
+    threads = cpus["share"]
     B = args.frames_per_gpu
     total = B * world
     start, end = distributed.shard_range(total, world, rank)
     t_gen = time.perf_counter()
-    frames = make_frames(range(start, end), threads)
-    batch = pitt.FrameBatch.from_host(frames, device=dev)
-    log(f"[rank {rank}] {len(frames)} frames generated + uploaded in {time.perf_counter() - t_gen:.1f} s")
+    # one distinct batch per in-flight context: batch j holds frames start + j * total + [0, B)
+    batches, frames0 = [], None
+    for j in range(args.pipeline):
+        fr = make_frames(range(start + j * total, end + j * total), threads)
+        if j == 0:
+            frames0 = fr
+        batches.append(pitt.FrameBatch.from_host(fr, device=dev))
+    log(f"[rank {rank}] {args.pipeline} x {len(frames0)} frames generated + uploaded in "
+        f"{time.perf_counter() - t_gen:.1f} s")
 
     # Several contexts, each on its own library-created stream (own HW queue): batch i+1 is enqueued
     # before batch i completes, so the latency-bound covariance chain of one batch overlaps the
     # HBM-bound kernels of the next.
     ctxs = [pitt.Context(local) for _ in range(args.pipeline)]
-    streams = [torch.cuda.Stream(device=dev) for _ in ctxs] if args.torch_streams else []
-    for c, s in zip(ctxs, streams):
-        c.set_stream(s)
-    outs = [None if args.no_inliers else torch.empty(batch.capacity, dtype=torch.int32, device=dev)
-            for _ in ctxs]
+    outs = [None if args.no_inliers else torch.empty(b.capacity, dtype=torch.int32, device=dev) for b in batches]
     pending = [None] * len(ctxs)
     torch.cuda.synchronize()
     params = pitt.sac_params()
@@ -134,7 +327,7 @@ def main():
         if pending[i] is not None:
             ctx.wait()
             done = pending[i]
-        pending[i] = ctx.plane_segment_batch_async(batch, params, outs[i])
+        pending[i] = ctx.plane_segment_batch_async(batches[i], params, outs[i])
         if done is not None and world > 1:
             done = distributed.gather_results(done, start, total, device=dev)
         return done
@@ -151,19 +344,17 @@ def main():
         return last
 
     ctx = ctxs[0]
-
     for _ in range(args.warmup):
         step()
-    res = drain()
+    drain()
     # parity spot check outside the timed region (first frame of this rank vs the oracle)
     if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_binding as orc
-        o = orc.plane_segment(*frames[0])
-        ok = (np.array_equal(res[0]["coefficients"], o.coefficients) and res[0]["n_inliers"] == len(o.inliers)
-              and res[0]["hypotheses"] == o.hypotheses)
+        res0 = ctx.plane_segment_batch(batches[0], params, outs[0])
+        o = oracle().plane_segment(*frames0[0])
+        ok = (np.array_equal(res0[0]["coefficients"], o.coefficients) and res0[0]["n_inliers"] == len(o.inliers)
+              and res0[0]["hypotheses"] == o.hypotheses)
         log(f"[rank 0] parity frame 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'} "
-            f"(T={int(res[0]['hypotheses'])}, inliers={int(res[0]['n_inliers'])})")
+            f"(T={int(res0[0]['hypotheses'])}, inliers={int(res0[0]['n_inliers'])})")
 
     # ---- timed throughput pass: K steps, batches overlapped on the contexts' streams ----
     if world > 1:
@@ -182,28 +373,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # ---- roofline pass: the same batches one at a time, HIP events around every launch on the
-    # launch stream (a concurrent batch would share HBM and stretch the kernel's duration) ----
+    # ---- roofline pass: one batch at a time, HIP events around every launch on the launch stream
+    # (a concurrent batch would share HBM and stretch the kernel's duration) ----
     roof_steps = max(1, min(args.steps, 10))
     ctx.profile(True)
     ctx.profile_reset()
-    for _ in range(roof_steps):
-        ctx.plane_segment_batch(batch, params, outs[0])
+    for k in range(roof_steps):
+        ctx.plane_segment_batch(batches[k % len(batches)], params, outs[k % len(batches)])
     launches, ms, nbytes = ctx.profile_get("k_score")
     n_empty, ms_empty, _ = ctx.profile_get("k_score:empty")
+    kernels = kernel_table(ctx, roof_steps)
     if rank == 0:
-        for k in ("k_hypothesize", "k_score", "k_score.first", "k_score:empty", "k_replay", "k_refine", "k_sel_mark",
-                  "k_sel_write"):
-            n_, ms_, b_ = ctx.profile_get(k)
-            log(f"[rank 0] {k:15s} launches {n_:5d}  {ms_ / roof_steps:8.3f} ms/batch  "
-                f"avg {ms_ / max(1, n_) * 1e3:9.1f} us  {b_ / max(1e-9, ms_) / 1e6:8.1f} GB/s")
+        for k, v in kernels.items():
+            log(f"[rank 0] {k:15s} launches/batch {v['launches_per_batch']:5.1f}  {v['us_per_batch']:8.1f} us/batch  "
+                f"avg {v['avg_launch_us']:8.1f} us  {v['GBps']:8.1f} GB/s")
     ctx.profile(False)
     hyps = res["hypotheses"]
 
+    line = None
     if rank == 0:
         avg_ms = ms / max(1, launches)
         achieved = (nbytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if launches else 0.0
-        traffic = pmc_traffic()
         line = {
             "metric": METRIC,
             "value": round(total * args.steps / dt, 2),
@@ -216,7 +406,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic 640x480 organised table-scene clouds, scene_seed = 1000 + frame id",
+            "data": "synthetic 640x480 organised table-scene clouds, scene_seed = 1000 + frame id, "
+                    f"{args.pipeline} distinct batches in flight",
             "config": {
                 "workload": f"batch of {B} synthetic 307k-pt clouds per GPU (BASELINE config 3"
                             f"{'; config 4: frame-sharded, RCCL all_gather of per-frame records' if world > 1 else ''}),"
@@ -225,6 +416,8 @@ def main():
                 "points_per_frame": W * H,
                 "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU",
                 "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
+                "world_size_seen": world,
+                "collective": (f"{backend} all_gather_into_tensor of per-frame records" if world > 1 else None),
             },
             "roofline": {
                 "kernel": "k_score",
@@ -233,7 +426,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": pmc_traffic(),
                 "launches": launches,
                 "measured": f"HIP events on k_score's stream over a separate {roof_steps}-batch pass with one "
                             "batch in flight (the timed pass overlaps batches on several streams); launches "
@@ -243,9 +436,23 @@ def main():
                 "avg_launch_us": round(avg_ms * 1e3, 2),
                 "algorithmic_bytes_per_launch": round(nbytes / max(1, launches), 1),
             },
+            "kernels": kernels,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(frames, threads, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_extras:
+        clutter_frames, line["clutter"] = clutter_pass(pitt, ctx, dev, threads)
+        log(f"[rank 0] clutter: {line['clutter']}")
+        host = [pitt.FrameBatch(b.x.cpu().pin_memory(), b.y.cpu().pin_memory(), b.z.cpu().pin_memory(), b.offsets,
+                                b.counts, b.capacity) for b in batches]
+        line["pcie_fed"] = pcie_pass(pitt, ctxs, host, dev, params, max(3, min(args.steps, 10)))
+        log(f"[rank 0] pcie_fed: {line['pcie_fed']}")
+        line["config5"] = config5_pass(pitt, ctx, threads)
+        log(f"[rank 0] config5: {line['config5']}")
+    else:
+        clutter_frames = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cl = clutter_frames[0] if clutter_frames else make_frames([0], 1, pitt.SCENE_CLUTTER)[0]
+        line["cpu_baseline"] = cpu_baseline(frames0, cl, cpus, args.cpu_budget)
+    if rank == 0:
         print(json.dumps(line), flush=True)
     for c in ctxs:
         c.close()

@@ -5,9 +5,12 @@
 // in float, r^2 = (float)((double)tol_f * tol_f)), seeding clusters in ascending index order.
 // Without duplicate points the clusters are exactly the connected components of that
 // radius graph, and the seed of each is its smallest index.  Here:
-//   k_cells     hashed uniform grid, cell = 1.01 * tolerance (a neighbour is at most one cell away)
-//   k_union     union-find over the 27-cell neighbourhood, smaller root wins (root = min index)
-//   k_flatten / k_sizes / kept-root compaction (ascending seeds = PCL discovery order)
+//   k_cells ... k_scatter   hashed grid of cells of side tol / sqrt(3) (each cell a clique of the
+//               radius graph), points grouped by cell
+//   k_cell_union  union-find over CELLS: a cell pair within the 5x5x5 neighbourhood joins at its
+//               first point pair closer than the radius (early exit), not per point pair
+//   k_cell_roots / k_point_labels   component size and seed (smallest index), per-point labels;
+//               kept-root compaction (ascending seeds = PCL discovery order)
 //   host        std::sort(rbegin, rend, size <) -- the reference's own ordering call, so ties
 //               and > 16 clusters order exactly as libstdc++ does it there
 //   k_keys + bitonic sort of (slot << 32 | index): members ascending inside each cluster
@@ -92,18 +95,23 @@ __global__ __launch_bounds__(64) void k_minxyz_final(const float* __restrict__ p
     if (threadIdx.x == 0) { mn[0] = a; mn[1] = b; mn[2] = c; }
 }
 
-__global__ void k_iota_cl(int32_t* __restrict__ v, int64_t n) {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
-        v[k] = (int32_t)k;
-}
+// ---- cell grid ---------------------------------------------------------------------------------
+// Cells of side tol_f / sqrt(3) shrunk by 1e-4: two finite points in one cell are closer than
+// tol (1 - 1e-4) -- far enough inside the radius that PCL's float test ((dx^2 + dy^2) + dz^2 < r^2)
+// holds too -- so every cell is a clique of the radius graph.  A radius neighbour of a point lies
+// at most two cells away on each axis (tol / cell < 1.7323), so the components of the point graph
+// are the components of the cell graph whose edges are the cell pairs within that 5x5x5
+// neighbourhood holding at least one point pair closer than the radius.
+constexpr double kCellShrink = 1.0 - 1e-4;
+constexpr int kCellBits = 21;
+constexpr int64_t kCellSpan = ((int64_t)1 << kCellBits) - 8;  // grid coordinates (+2 neighbours) per axis
 
 struct Grid {
     const float *x, *y, *z;
     const float* mn;
     double inv_cell;
-    uint64_t* keys;   // [hsize]
-    int32_t* slot;    // [n]
-    int32_t* ccount;  // [hsize]
+    uint64_t* keys;   // [hsize] occupied cells' keys
+    int32_t* hcid;    // [hsize] dense id of the cell in a slot
     uint32_t hmask;
 };
 
@@ -123,10 +131,13 @@ __device__ __forceinline__ int32_t hash_find(const Grid& g, uint64_t key) {
     }
 }
 
-__global__ void k_cells(Grid g, int64_t n) {
+// Occupied cells into the hash; the inserting thread numbers the cell (dense id, any order) and
+// records its key.  pslot[i] = the point's slot, -1 for a non-finite point (never indexed by
+// KdTreeFLANN: a singleton).
+__global__ void k_cells(Grid g, int64_t n, int32_t* __restrict__ pslot, int32_t* __restrict__ ncells,
+                        uint64_t* __restrict__ ckey) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        // a non-finite point has no radius neighbours (FLANN distances are NaN): a singleton
-        if (!finite3(g.x[i], g.y[i], g.z[i])) { g.slot[i] = -1; continue; }
+        if (!finite3(g.x[i], g.y[i], g.z[i])) { pslot[i] = -1; continue; }
         int64_t cx, cy, cz;
         cell_of(g, i, cx, cy, cz);
         const uint64_t key = cell_key(cx, cy, cz);
@@ -134,20 +145,70 @@ __global__ void k_cells(Grid g, int64_t n) {
         while (true) {
             const uint64_t prev = atomicCAS((unsigned long long*)&g.keys[h], (unsigned long long)kEmpty,
                                             (unsigned long long)key);
-            if (prev == kEmpty || prev == key) break;
+            if (prev == kEmpty) {
+                const int32_t c = atomicAdd(ncells, 1);
+                g.hcid[h] = c;
+                ckey[c] = key;
+                break;
+            }
+            if (prev == key) break;
             h = (h + 1) & g.hmask;
         }
-        g.slot[i] = (int32_t)h;
-        atomicAdd(&g.ccount[h], 1);
+        pslot[i] = (int32_t)h;
     }
 }
 
-__global__ void k_scatter(const int32_t* __restrict__ slot, int64_t n, const int32_t* __restrict__ cstart,
+// Per point: its cell id; per cell: point count and smallest point index.
+__global__ void k_cell_count(const int32_t* __restrict__ pslot, int64_t n, const int32_t* __restrict__ hcid,
+                             int32_t* __restrict__ pcid, int32_t* __restrict__ ccnt, int32_t* __restrict__ cmin) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t h = pslot[i];
+        const int32_t c = h < 0 ? -1 : hcid[h];
+        pcid[i] = c;
+        if (c >= 0) {
+            atomicAdd(&ccnt[c], 1);
+            atomicMin(&cmin[c], (int32_t)i);
+        }
+    }
+}
+
+// Exclusive scan of the cells' counts (one 1024-thread block; the cell count is read on the device).
+__global__ __launch_bounds__(1024) void k_cell_scan(const int32_t* __restrict__ ccnt, const int32_t* __restrict__ ncells,
+                                                    int32_t* __restrict__ cstart) {
+    __shared__ int32_t part[16];
+    const int nc = *ncells;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int carry = 0;
+    for (int base = 0; base < nc; base += 1024) {
+        const int t = base + (int)threadIdx.x;
+        const int v = t < nc ? ccnt[t] : 0;
+        int inc = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) part[w] = inc;
+        __syncthreads();
+        int pre = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            pre += k < w ? part[k] : 0;
+            tot += part[k];
+        }
+        if (t < nc) cstart[t] = carry + pre + inc - v;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cstart[nc] = carry;
+}
+
+__global__ void k_scatter(const int32_t* __restrict__ pcid, int64_t n, const int32_t* __restrict__ cstart,
                           int32_t* __restrict__ cursor, int32_t* __restrict__ cpts) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t s = slot[i];
-        if (s < 0) continue;
-        cpts[cstart[s] + atomicAdd(&cursor[s], 1)] = (int32_t)i;
+        const int32_t c = pcid[i];
+        if (c < 0) continue;
+        cpts[cstart[c] + atomicAdd(&cursor[c], 1)] = (int32_t)i;
     }
 }
 
@@ -168,44 +229,93 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int32_t a, int32_t b) 
         b = uf_find(parent, b);
         if (a == b) return;
         if (a > b) { const int32_t t = a; a = b; b = t; }
-        // hook the larger root under the smaller one: roots end up as component minima
-        if (atomicCAS(&parent[b], b, a) == b) return;
+        if (atomicCAS(&parent[b], b, a) == b) return;  // the larger root hooks under the smaller
     }
 }
 
-__global__ void k_union(Grid g, int64_t n, const int32_t* __restrict__ cstart, const int32_t* __restrict__ cpts,
-                        float r2, int32_t* __restrict__ parent) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float qx = g.x[i], qy = g.y[i], qz = g.z[i];
-        if (!finite3(qx, qy, qz)) continue;
-        int64_t cx, cy, cz;
-        cell_of(g, i, cx, cy, cz);
-        for (int dx = -1; dx <= 1; ++dx)
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dz = -1; dz <= 1; ++dz) {
-                    const int32_t h = hash_find(g, cell_key(cx + dx, cy + dy, cz + dz));
-                    if (h < 0) continue;
-                    for (int32_t k = cstart[h]; k < cstart[h + 1]; ++k) {
-                        const int32_t j = cpts[k];
-                        if (j <= i) continue;
-                        const float ex = qx - g.x[j], ey = qy - g.y[j], ez = qz - g.z[j];
-                        const float d = ex * ex + ey * ey + ez * ez;  // FLANN L2_Simple order
-                        if (d < r2) uf_union(parent, (int32_t)i, j);
+__global__ void k_cell_iota(int32_t* __restrict__ parent, const int32_t* __restrict__ ncells) {
+    const int nc = *ncells;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += gridDim.x * blockDim.x) parent[c] = c;
+}
+
+// One wave per cell: against each of the 62 cells after it in the 5x5x5 neighbourhood (the other 62
+// see it from their side), unless the two are already joined, look for one point pair closer than
+// the radius (PCL's float order) -- lanes hold the cell's points, the neighbour's points are walked
+// one by one -- and join the cells at the first such pair.
+__global__ __launch_bounds__(256) void k_cell_union(Grid g, const int32_t* __restrict__ ncells,
+                                                    const uint64_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
+                                                    const int32_t* __restrict__ cpts, float r2,
+                                                    int32_t* __restrict__ parent) {
+    const int nc = *ncells;
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * 4;
+    for (int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6))); c < nc; c += nw) {
+        const uint64_t key = ckey[c];
+        const int64_t cx = (int64_t)(key & 0x1FFFFF), cy = (int64_t)((key >> 21) & 0x1FFFFF), cz = (int64_t)(key >> 42);
+        const int b0 = cstart[c], e0 = cstart[c + 1];
+        for (int o = 63; o < 125; ++o) {  // offsets after (0, 0, 0) in this order; the rest is the neighbours' half
+            const int dx = o / 25 - 2, dy = (o / 5) % 5 - 2, dz = o % 5 - 2;
+            if (cx + dx < 0 || cy + dy < 0 || cz + dz < 0) continue;
+            const int32_t h = hash_find(g, cell_key(cx + dx, cy + dy, cz + dz));
+            if (h < 0) continue;
+            const int32_t d = g.hcid[h];
+            if (uf_find(parent, c) == uf_find(parent, d)) continue;
+            const int b1 = cstart[d], e1 = cstart[d + 1];
+            bool hit = false;
+            for (int p0 = b0; p0 < e0 && !hit; p0 += 64) {
+                const int pk = p0 + lane;
+                float px = __builtin_nanf(""), py = px, pz = px;
+                if (pk < e0) {
+                    const int32_t i = cpts[pk];
+                    px = g.x[i];
+                    py = g.y[i];
+                    pz = g.z[i];
+                }
+                for (int q = b1; q < e1; ++q) {
+                    const int32_t j = __builtin_amdgcn_readfirstlane(cpts[q]);
+                    const float ex = px - g.x[j], ey = py - g.y[j], ez = pz - g.z[j];
+                    const float dd = ex * ex + ey * ey + ez * ez;  // FLANN L2_Simple order
+                    if (__builtin_amdgcn_ballot_w64(dd < r2)) {
+                        hit = true;
+                        break;
                     }
                 }
+            }
+            if (hit && lane == 0) uf_union(parent, c, d);
+        }
     }
 }
 
-__global__ void k_flatten_sizes(int32_t* __restrict__ parent, int64_t n, int32_t* __restrict__ size) {
+// Components: per cell its root; per root the size (sum of its cells' counts) and the seed (the
+// smallest point index -- PCL's BFS discovers components in ascending seed order).
+__global__ void k_cell_roots(int32_t* __restrict__ parent, const int32_t* __restrict__ ncells,
+                             const int32_t* __restrict__ ccnt, const int32_t* __restrict__ cmin,
+                             int32_t* __restrict__ csize, int32_t* __restrict__ cseed) {
+    const int nc = *ncells;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += gridDim.x * blockDim.x) {
+        const int32_t r = uf_find(parent, c);
+        atomicAdd(&csize[r], ccnt[c]);
+        atomicMin(&cseed[r], cmin[c]);
+    }
+}
+
+// Per point: label = its component's seed (a non-finite point is its own singleton); at a seed the
+// component size.
+__global__ void k_point_labels(const int32_t* __restrict__ pcid, int64_t n, int32_t* __restrict__ parent,
+                               const int32_t* __restrict__ csize, const int32_t* __restrict__ cseed,
+                               int32_t* __restrict__ label, int32_t* __restrict__ size) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t r = uf_find(parent, (int32_t)i);
-        atomicAdd(&size[r], 1);
+        const int32_t c = pcid[i];
+        if (c < 0) {
+            label[i] = (int32_t)i;
+            size[i] = 1;
+            continue;
+        }
+        const int32_t r = uf_find(parent, c);
+        const int32_t sd = cseed[r];
+        label[i] = sd;
+        if (sd == (int32_t)i) size[i] = csize[r];
     }
-}
-
-__global__ void k_labels(int32_t* __restrict__ parent, int64_t n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        parent[i] = uf_find(parent, (int32_t)i);
 }
 
 struct KeptRoot {
@@ -299,32 +409,51 @@ __global__ void k_members(const uint64_t* __restrict__ keys, int64_t m, const fl
     }
 }
 
-// Float sums in index order (cluster_segmentation_srv.cpp:88-90): one block per cluster stages
-// coordinates through LDS; lanes 0..2 run the three serial chains.
+// Float sums in index order (cluster_segmentation_srv.cpp:88-90): one block per cluster.  Waves
+// 1-3 stage 2048-element slices of x, y, z into a double-buffered LDS ring while lanes 0..2 of
+// wave 0 run the three serial chains over the previous slice, 16 elements per unrolled step read
+// as four float4 (the adds stay in index order: no reassociation).
+constexpr int kSumChunk = 2048;
+
 __global__ __launch_bounds__(256) void k_sums(const int64_t* __restrict__ coff, int32_t k, const float* __restrict__ cx,
                                               const float* __restrict__ cy, const float* __restrict__ cz,
                                               float* __restrict__ sums) {
-    __shared__ float buf[3][1024];
+    __shared__ float4 buf[2][3][kSumChunk / 4];
     const int c = blockIdx.x;
     if (c >= k) return;
     const int64_t b = coff[c], e = coff[c + 1];
+    const int64_t nch = (e - b + kSumChunk - 1) / kSumChunk;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float s = 0.0f;
-    const int lane = threadIdx.x;
-    for (int64_t i0 = b; i0 < e; i0 += 1024) {
-        for (int t = lane; t < 1024; t += 256) {
-            const int64_t i = i0 + t;
-            buf[0][t] = i < e ? cx[i] : 0.0f;
-            buf[1][t] = i < e ? cy[i] : 0.0f;
-            buf[2][t] = i < e ? cz[i] : 0.0f;
+    for (int64_t i = 0; i <= nch; ++i) {
+        if (w > 0 && i < nch) {  // stage slice i
+            float* f = reinterpret_cast<float*>(buf[i & 1]);
+            const int64_t i0 = b + i * kSumChunk;
+            for (int t = (int)threadIdx.x - 64; t < kSumChunk; t += 192) {
+                const int64_t j = i0 + t;
+                const bool in = j < e;
+                f[t] = in ? cx[j] : 0.0f;
+                f[kSumChunk + t] = in ? cy[j] : 0.0f;
+                f[2 * kSumChunk + t] = in ? cz[j] : 0.0f;
+            }
         }
-        __syncthreads();
-        if (lane < 3) {
-            const int64_t cnt = min((int64_t)1024, e - i0);
-            for (int t = 0; t < cnt; ++t) s += buf[lane][t];
+        if (w == 0 && lane < 3 && i > 0) {  // sum slice i - 1
+            const float4* q = buf[(i - 1) & 1][lane];
+            const int cnt = (int)min((int64_t)kSumChunk, e - (b + (i - 1) * kSumChunk));
+            int t = 0;
+            for (; t + 16 <= cnt; t += 16) {
+                const float4 a0 = q[t / 4], a1 = q[t / 4 + 1], a2 = q[t / 4 + 2], a3 = q[t / 4 + 3];
+                s = s + a0.x; s = s + a0.y; s = s + a0.z; s = s + a0.w;
+                s = s + a1.x; s = s + a1.y; s = s + a1.z; s = s + a1.w;
+                s = s + a2.x; s = s + a2.y; s = s + a2.z; s = s + a2.w;
+                s = s + a3.x; s = s + a3.y; s = s + a3.z; s = s + a3.w;
+            }
+            const float* r = reinterpret_cast<const float*>(q);
+            for (; t < cnt; ++t) s = s + r[t];
         }
         __syncthreads();
     }
-    if (lane < 3) sums[3 * c + lane] = s;
+    if (w == 0 && lane < 3) sums[3 * c + lane] = s;
 }
 
 static inline int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
@@ -359,7 +488,7 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     // KdTreeFLANN::radiusSearch: r^2 = (float)(radius * radius) with radius = (double)(float)tol
     const float tol_f = (float)tolerance;
     const float r2 = (float)((double)tol_f * (double)tol_f);
-    const double cell = (double)tol_f * 1.01;
+    const double cell = (double)tol_f * (1.0 / std::sqrt(3.0)) * kCellShrink;
     if (!(cell > 0.0) || !std::isfinite(cell)) return ctx->fail(PITT_E_INVALID, "tolerance must be > 0");
     uint32_t hsize = 1024;
     while ((int64_t)hsize < 2 * n) hsize <<= 1;
@@ -367,26 +496,38 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     float* X = (float*)ctx->buf("cl_xyz", N * 3 * 4);
     float* MN = (float*)ctx->buf("cl_min", 64);
     uint64_t* KEYS = (uint64_t*)ctx->buf("cl_hkeys", (size_t)hsize * 8);
-    int32_t* SLOT = (int32_t*)ctx->buf("cl_slot", N * 4);
-    int32_t* CCNT = (int32_t*)ctx->buf("cl_ccnt", ((size_t)hsize + 1) * 4);
-    int32_t* CSTART = (int32_t*)ctx->buf("cl_cstart", ((size_t)hsize + 1) * 4);
-    int32_t* CUR = (int32_t*)ctx->buf("cl_cursor", (size_t)hsize * 4);
+    int32_t* HCID = (int32_t*)ctx->buf("cl_hcid", (size_t)hsize * 4);
+    uint64_t* CKEY = (uint64_t*)ctx->buf("cl_ckey", N * 8);
+    int32_t* PSLOT = (int32_t*)ctx->buf("cl_pslot", N * 4);
+    int32_t* PCID = (int32_t*)ctx->buf("cl_pcid", N * 4);
+    // per-cell arrays (cells <= points): count, min index, start (+1), cursor, parent, size, seed
+    int32_t* CELLS = (int32_t*)ctx->buf("cl_cells", (N * 7 + 16) * 4);
     int32_t* CPTS = (int32_t*)ctx->buf("cl_cpts", N * 4);
-    int32_t* PAR = (int32_t*)ctx->buf("cl_parent", N * 4);
+    int32_t* LABEL = (int32_t*)ctx->buf("cl_label", N * 4);
     int32_t* SIZE = (int32_t*)ctx->buf("cl_size", N * 4);
     int32_t* ROOTS = (int32_t*)ctx->buf("cl_roots", N * 4);
     int32_t* RSIZES = (int32_t*)ctx->buf("cl_rsizes", N * 4);
     int32_t* RSLOT = (int32_t*)ctx->buf("cl_rootslot", N * 4);
-    if (!X || !MN || !KEYS || !SLOT || !CCNT || !CSTART || !CUR || !CPTS || !PAR || !SIZE || !ROOTS || !RSIZES || !RSLOT)
+    if (!X || !MN || !KEYS || !HCID || !CKEY || !PSLOT || !PCID || !CELLS || !CPTS || !LABEL || !SIZE || !ROOTS ||
+        !RSIZES || !RSLOT)
         return ctx->fail(PITT_E_NOMEM, "cluster scratch");
+    int32_t* NCELLS = CELLS;                 // [1] (+ padding)
+    int32_t* CCNT = CELLS + 16;              // [N]
+    int32_t* CMIN = CCNT + N;                // [N]
+    int32_t* CCUR = CMIN + N;                // [N]
+    int32_t* CSIZE = CCUR + N;               // [N]
+    int32_t* CSEED = CSIZE + N;              // [N]
+    int32_t* CPAR = CSEED + N;               // [N]
+    int32_t* CSTART = (int32_t*)ctx->buf("cl_cstart", (N + 1) * 4);
+    if (!CSTART) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
     float *Y = X + N, *Z = X + 2 * N;
     PITT_HIP_TRY(hipMemcpyAsync(X, hx, N * 4, hipMemcpyHostToDevice, s));
     PITT_HIP_TRY(hipMemcpyAsync(Y, hy, N * 4, hipMemcpyHostToDevice, s));
     PITT_HIP_TRY(hipMemcpyAsync(Z, hz, N * 4, hipMemcpyHostToDevice, s));
     PITT_HIP_TRY(hipMemsetAsync(KEYS, 0xFF, (size_t)hsize * 8, s));
-    PITT_HIP_TRY(hipMemsetAsync(CCNT, 0, ((size_t)hsize + 1) * 4, s));
-    PITT_HIP_TRY(hipMemsetAsync(CUR, 0, (size_t)hsize * 4, s));
-    PITT_HIP_TRY(hipMemsetAsync(SIZE, 0, N * 4, s));
+    PITT_HIP_TRY(hipMemsetAsync(CELLS, 0, (N * 7 + 16) * 4, s));
+    PITT_HIP_TRY(hipMemsetAsync(CMIN, 0x7F, N * 4, s));   // INT_MAX-ish: atomicMin seeds
+    PITT_HIP_TRY(hipMemsetAsync(CSEED, 0x7F, N * 4, s));
     {
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMinBlocks));
         float* PART = (float*)ctx->buf("cl_minpart", (size_t)kMinBlocks * 3 * sizeof(float));
@@ -394,16 +535,32 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
         hipLaunchKernelGGL(k_minxyz, dim3(nb), dim3(kBlock), 0, s, X, Y, Z, n, PART);
         hipLaunchKernelGGL(k_minxyz_final, dim3(1), dim3(64), 0, s, PART, nb, MN);
     }
-    hipLaunchKernelGGL(k_iota_cl, dim3(ew(n)), dim3(256), 0, s, PAR, n);
-    Grid g{X, Y, Z, MN, 1.0 / cell, KEYS, SLOT, CCNT, hsize - 1};
-    hipLaunchKernelGGL(k_cells, dim3(ew(n)), dim3(256), 0, s, g, n);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, CCNT, (int64_t)hsize, CSTART);
-    hipLaunchKernelGGL(k_scatter, dim3(ew(n)), dim3(256), 0, s, SLOT, n, CSTART, CUR, CPTS);
-    hipLaunchKernelGGL(k_union, dim3(ew(n)), dim3(256), 0, s, g, n, CSTART, CPTS, r2, PAR);
-    hipLaunchKernelGGL(k_flatten_sizes, dim3(ew(n)), dim3(256), 0, s, PAR, n, SIZE);
-    hipLaunchKernelGGL(k_labels, dim3(ew(n)), dim3(256), 0, s, PAR, n);
+    // the grid's extent must fit the 21-bit cell coordinates (else distinct cells would alias)
+    {
+        float mxh[3] = {-INFINITY, -INFINITY, -INFINITY}, mnh[3];
+        for (int64_t i = 0; i < n; ++i) {
+            if (!(std::isfinite(hx[i]) && std::isfinite(hy[i]) && std::isfinite(hz[i]))) continue;
+            mxh[0] = std::max(mxh[0], hx[i]);
+            mxh[1] = std::max(mxh[1], hy[i]);
+            mxh[2] = std::max(mxh[2], hz[i]);
+        }
+        PITT_HIP_TRY(hipMemcpyAsync(mnh, MN, 12, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        for (int k = 0; k < 3; ++k)
+            if (std::isfinite(mnh[k]) && ((double)mxh[k] - (double)mnh[k]) / cell >= (double)kCellSpan)
+                return ctx->fail(PITT_E_INVALID, "cloud extent exceeds 2^21 cells of tolerance / sqrt(3)");
+    }
+    Grid g{X, Y, Z, MN, 1.0 / cell, KEYS, HCID, hsize - 1};
+    hipLaunchKernelGGL(k_cells, dim3(ew(n)), dim3(256), 0, s, g, n, PSLOT, NCELLS, CKEY);
+    hipLaunchKernelGGL(k_cell_count, dim3(ew(n)), dim3(256), 0, s, PSLOT, n, HCID, PCID, CCNT, CMIN);
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, CCNT, NCELLS, CSTART);
+    hipLaunchKernelGGL(k_scatter, dim3(ew(n)), dim3(256), 0, s, PCID, n, CSTART, CCUR, CPTS);
+    hipLaunchKernelGGL(k_cell_iota, dim3(ew(n)), dim3(256), 0, s, CPAR, NCELLS);
+    hipLaunchKernelGGL(k_cell_union, dim3(ew(n)), dim3(256), 0, s, g, NCELLS, CKEY, CSTART, CPTS, r2, CPAR);
+    hipLaunchKernelGGL(k_cell_roots, dim3(ew(n)), dim3(256), 0, s, CPAR, NCELLS, CCNT, CMIN, CSIZE, CSEED);
+    hipLaunchKernelGGL(k_point_labels, dim3(ew(n)), dim3(256), 0, s, PCID, n, CPAR, CSIZE, CSEED, LABEL, SIZE);
     int64_t K = 0;
-    int rc = compact(ctx, n, KeptRoot{PAR, SIZE, (uint64_t)(int64_t)min_size, (uint64_t)(int64_t)max_size},
+    int rc = compact(ctx, n, KeptRoot{LABEL, SIZE, (uint64_t)(int64_t)min_size, (uint64_t)(int64_t)max_size},
                      WriteRoot{SIZE, ROOTS, RSIZES}, &K);
     if (rc) return rc;
     if (K == 0) return PITT_OK;
@@ -441,7 +598,7 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     PITT_HIP_TRY(hipMemsetAsync(SK, 0xFF, (size_t)Mp * 8, s));
     hipLaunchKernelGGL(k_set_slots, dim3(ew(K)), dim3(256), 0, s, SROOT, SROOT + K, (int32_t)K, RSLOT);
     int64_t M2 = 0;
-    rc = compact(ctx, n, KeptPoint{PAR, RSLOT}, WriteKey{PAR, RSLOT, SK}, &M2);
+    rc = compact(ctx, n, KeptPoint{LABEL, RSLOT}, WriteKey{LABEL, RSLOT, SK}, &M2);
     if (rc) return rc;
     if (M2 != M) return ctx->fail(PITT_E_INVALID, "cluster member count mismatch");
     // bitonic sort of Mp keys

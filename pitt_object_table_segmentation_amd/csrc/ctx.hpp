@@ -72,6 +72,12 @@ struct pitt_ctx {
     std::vector<std::pair<int64_t, int64_t>> inflight_stat;
     std::vector<int> inflight_score_recs;
     std::vector<int> inflight_chunks;
+    void* inflight_acct = nullptr;        // pinned copy of the device byte counters (profiling)
+    std::vector<int> inflight_acct_recs;  // profiler record per counted kernel (-1: none)
+    int64_t inflight_acct_tiles = 0;      // per-tile byte words following the counters
+
+    // support loop: z sums that could not be certified and ran the sequential loop (diagnostic)
+    int64_t zsum_sequential = 0;
 
     // last batch (debug / parity hooks)
     int32_t last_hcap = 0;

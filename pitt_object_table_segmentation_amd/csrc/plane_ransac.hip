@@ -56,6 +56,14 @@ struct ChunkStat {
     int64_t points;
 };
 
+// Bytes a data-dependent kernel actually moved, counted on the device only while profiling (acct
+// non-null): kAcShards slots per kernel so that concurrent waves rarely hit the same address.
+enum { kAcHyp = 0, kAcReplay = 1, kAcRefine = 2, kAcSelMark = 3, kAcSelWrite = 4, kAcKernels = 5 };
+constexpr int kAcShards = 64;
+__device__ __forceinline__ void acct_add(unsigned long long* acct, int k, unsigned long long bytes) {
+    if (acct && bytes) atomicAdd(&acct[k * kAcShards + (blockIdx.x & (kAcShards - 1))], bytes);
+}
+
 // ------------------------------------------------------------------------------------------
 // Hypotheses, generated lazily in windows of kBlock sampler-table attempts.  Attempt a uses table
 // triple a (the sampler's draws depend only on (n, seed) until a sample is rejected; rejected
@@ -151,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
     const FrameMeta* __restrict__ meta, const int32_t* __restrict__ tables, int A, int hcap, int target,
     int runnable_all, float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt,
     FrameState* __restrict__ st, int32_t* __restrict__ list0, int32_t* __restrict__ cnt0,
-    ChunkStat* __restrict__ stat0) {
+    ChunkStat* __restrict__ stat0, unsigned long long* __restrict__ acct) {
     __shared__ GenLds G;
     const int f = blockIdx.x;
     const FrameMeta m = meta[f];
@@ -192,6 +200,8 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
             atomicAdd(&stat0->tiles, m.tiles);
             atomicAdd((unsigned long long*)&stat0->points, (unsigned long long)m.n);
         }
+        // attempts examined: 3 table indices + 3 gathered points; hypotheses written: 16 + 4 B
+        acct_add(acct, kAcHyp, (unsigned long long)s.gen_att * 48ull + (unsigned long long)s.n_avail * 20ull);
     }
 }
 
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
     ChunkStat* __restrict__ next_stat, const float* __restrict__ X, const float* __restrict__ Y,
     const float* __restrict__ Z, const int32_t* __restrict__ tables, int A, int target_next,
-    float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt) {
+    float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt, unsigned long long* __restrict__ acct) {
     __shared__ GenLds G;
     __shared__ int32_t part[kBlock / 64][kMaxChunk];
     __shared__ int32_t tot[kMaxChunk];
@@ -628,6 +638,7 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     __syncthreads();
     if (threadIdx.x == 0) G.s = st[f];
     __syncthreads();
+    const int att0 = G.s.gen_att, avail0 = G.s.n_avail;
     if (threadIdx.x != 0) goto extend;
     {
     FrameState& s = G.s;
@@ -677,6 +688,10 @@ extend:
             atomicAdd(&next_stat->tiles, m.tiles);
             atomicAdd((unsigned long long*)&next_stat->points, (unsigned long long)m.n);
         }
+        // count rows read, totals written, and the next chunk's hypotheses generated
+        acct_add(acct, kAcReplay, (unsigned long long)Hn * (unsigned long long)m.tiles * 4ull + (unsigned long long)Hn * 4ull +
+                                      (unsigned long long)(s.gen_att - att0) * 48ull +
+                                      (unsigned long long)(s.n_avail - avail0) * 20ull);
     }
 }
 
@@ -1074,7 +1089,7 @@ __global__ __launch_bounds__(192) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
-    int tiles_max, float4* __restrict__ final_coef) {
+    int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct) {
     __shared__ RefineLds L;
     const int f = blockIdx.x;
     const FrameState s = st[f];
@@ -1099,6 +1114,9 @@ __global__ __launch_bounds__(192) void k_refine(
                                       hstride);
         const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
         const int total = refine_stream<ORDER, kRDepth>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane, nact, 0, nsteps);
+        // the listed tiles' points, their count words, the plane in and out
+        if (lane == 0)
+            acct_add(acct, kAcRefine, (unsigned long long)nsteps * kRChunk * 12ull + (unsigned long long)m.tiles * 4ull + 32ull);
         if (lane == 0) {
             L.total = total;
             lds_release(&L.done, 1);
@@ -1136,7 +1154,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ final_coef,
     float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, const float* __restrict__ group_box,
-    uint32_t* __restrict__ sel_bits, int32_t* __restrict__ sel_cnt) {
+    uint32_t* __restrict__ sel_bits, int32_t* __restrict__ sel_cnt, uint32_t* __restrict__ acct_tile) {
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -1146,6 +1164,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     const float4 c = final_coef[f];
     const int64_t row = (int64_t)f * tiles_max + t;
     uint32_t word = 0;
+    unsigned long long moved = 32ull + 256ull + 4ull;  // tile box in; predicate bits and count out
     if (!box_misses_slab(tile_box + row * 8, c, thf)) {
         const int rem = (int)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
         const int64_t p0 = m.off + (int64_t)t * kTile + lane;
@@ -1154,6 +1173,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
         // groups whose box certainly misses the slab hold no inlier: not read (lane g tests group g)
         const bool gact = lane < kSelGroups && !box_misses_slab(group_box + (row * kSelGroups + lane) * 8, c, thf);
         const uint32_t gm = (uint32_t)__builtin_amdgcn_ballot_w64(gact);
+        moved += 32ull * kSelGroups + 12ull * 64ull * (unsigned long long)__builtin_popcount(gm);
         float px[kSelGroups], py[kSelGroups], pz[kSelGroups];  // the tile's live groups in flight
 #pragma unroll
         for (int g = 0; g < kSelGroups; ++g) {
@@ -1172,13 +1192,16 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     }
     sel_bits[row * 64 + lane] = word;
     const int n = wave_sum(__builtin_popcount(word));
-    if (lane == 0) sel_cnt[row] = n;
+    if (lane == 0) {
+        sel_cnt[row] = n;
+        if (acct_tile) acct_tile[row] = (uint32_t)moved;  // profiling: a plain store per tile, no atomics
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_sel_write(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, int n_frames, int tiles_max,
     const uint32_t* __restrict__ sel_bits, const int32_t* __restrict__ sel_cnt, int32_t* __restrict__ inliers,
-    int32_t* __restrict__ n_final) {
+    int32_t* __restrict__ n_final, uint32_t* __restrict__ acct_tile) {
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -1191,6 +1214,9 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
     pre = __builtin_amdgcn_readfirstlane(wave_sum(pre));
     const int mine = cnt[t];
     if (t == m.tiles - 1 && lane == 0) n_final[f] = pre + mine;
+    // the earlier tiles' counts, then the tile's bits and its indices
+    if (lane == 0 && acct_tile)
+        acct_tile[(int64_t)f * tiles_max + t] = 4u * (uint32_t)(t + 1) + (inliers && mine ? 256u + 4u * (uint32_t)mine : 0u);
     if (!inliers || mine == 0) return;
     const uint32_t word = sel_bits[((int64_t)f * tiles_max + t) * 64 + lane];
     int32_t* out = inliers + m.off + pre;
@@ -1250,11 +1276,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     hipStream_t sm = ctx->stream;
     // --- sizes ---
     int tiles_max = 1;
-    int64_t total_pts = 0;
-    for (int f = 0; f < nf; ++f) {
-        tiles_max = std::max<int>(tiles_max, (int)((fr->counts[f] + kTile - 1) / kTile));
-        total_pts += fr->counts[f];
-    }
+    for (int f = 0; f < nf; ++f) tiles_max = std::max<int>(tiles_max, (int)((fr->counts[f] + kTile - 1) / kTile));
     const int max_iter = p->max_iterations;
     const int hcap = max_iter >= 0 ? max_iter + 1 : 1;
     const int runnable_all = ((unsigned)max_iter * 10u) != 0u ? 1 : 0;
@@ -1331,10 +1353,22 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     // counters + chunk stats in one zeroed block
     const size_t cnt_bytes = (size_t)(nchunks + 1) * 4;
     const size_t stat_off = (cnt_bytes + 15) & ~(size_t)15;
-    const size_t zero_bytes = stat_off + (size_t)(nchunks + 1) * sizeof(ChunkStat);
+    const size_t acct_off = stat_off + (size_t)(nchunks + 1) * sizeof(ChunkStat);
+    const size_t acct_bytes = (size_t)kAcKernels * kAcShards * sizeof(unsigned long long);
+    const size_t zero_bytes = acct_off + acct_bytes;
     char* zblock = as<char>(ctx->buf("zblock", zero_bytes));
     int32_t* counters = as<int32_t>(zblock);
     ChunkStat* cstat = as<ChunkStat>(zblock + stat_off);
+    // per-kernel byte accounting, only while profiling (the kernels skip the atomics otherwise)
+    unsigned long long* acct = ctx->prof ? as<unsigned long long>(zblock + acct_off) : nullptr;
+    // the per-tile kernels store their bytes per tile instead (two arrays of nf x tiles_max words)
+    const size_t tile_words = (size_t)nf * tiles_max;
+    uint32_t* acct_tiles = nullptr;
+    if (ctx->prof) {
+        acct_tiles = as<uint32_t>(ctx->buf("acct_tiles", tile_words * 2 * 4));
+        if (!acct_tiles) return ctx->fail(PITT_E_NOMEM, "profiling scratch");
+        PITT_HIP_TRY(hipMemsetAsync(acct_tiles, 0, tile_words * 2 * 4, sm));
+    }
     float4* best_coef = as<float4>(ctx->buf("best_coef", (size_t)nf * sizeof(float4)));
     float4* final_coef = as<float4>(ctx->buf("final_coef", (size_t)nf * sizeof(float4)));
     int32_t* n_final = as<int32_t>(ctx->buf("n_final", (size_t)nf * 4));
@@ -1348,10 +1382,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
     int rec;
-    rec = ctx->prof_begin("k_hypothesize", (double)nf * A * 48.0);
+    std::vector<int> acct_recs((size_t)kAcKernels, -1);
+    rec = ctx->prof_begin("k_hypothesize", 0.0);
+    acct_recs[kAcHyp] = rec;
     hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta,
                        tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
-                       counters, cstat);
+                       counters, cstat, acct);
     ctx->prof_end(rec);
     const double log_prob = std::log(1.0 - p->probability);
     std::vector<int> score_recs;
@@ -1370,28 +1406,32 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            tile_box, group_box);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
+        if (c == 0) acct_recs[kAcReplay] = rec;  // every replay launch's bytes are counted in this one
         const int target_next = c + 1 < nchunks ? std::min(h0 + H + chunks[(size_t)c + 1], hcap) : 0;
         hipLaunchKernelGGL((k_replay<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride,
                            tiles_max, h0, H, max_iter, log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf,
                            counters + c + 1, cstat + c + 1, fr->x, fr->y, fr->z, tables, A, target_next, hyp_coef,
-                           hyp_attempt);
+                           hyp_attempt, acct);
         ctx->prof_end(rec);
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        p->optimize ? 1 : 0, best_coef, final_coef);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
-    rec = ctx->prof_begin("k_refine", (double)total_pts * 12.0);
+    rec = ctx->prof_begin("k_refine", 0.0);
+    acct_recs[kAcRefine] = rec;
     hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(192), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                       thf, tile_counts, hstride, tiles_max, final_coef);
+                       thf, tile_counts, hstride, tiles_max, final_coef, acct);
     ctx->prof_end(rec);
     const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
-    rec = ctx->prof_begin("k_sel_mark", (double)total_pts * 12.0);
+    rec = ctx->prof_begin("k_sel_mark", 0.0);
+    acct_recs[kAcSelMark] = rec;
     hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
-                       final_coef, thf, nf, tiles_max, tile_box, group_box, sel_bits, sel_cnt);
+                       final_coef, thf, nf, tiles_max, tile_box, group_box, sel_bits, sel_cnt, acct_tiles);
     ctx->prof_end(rec);
     rec = ctx->prof_begin("k_sel_write", 0.0);
+    acct_recs[kAcSelWrite] = rec;
     hipLaunchKernelGGL(k_sel_write, dim3(sel_blocks), dim3(kBlock), 0, sm, meta, st, nf, tiles_max, sel_bits, sel_cnt,
-                       inliers_dev, n_final);
+                       inliers_dev, n_final, acct_tiles ? acct_tiles + tile_words : nullptr);
     ctx->prof_end(rec);
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
@@ -1400,6 +1440,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
+    void* hacct = nullptr;
+    if (acct) {
+        hacct = ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4);
+        PITT_HIP_TRY(hipMemcpyAsync(hacct, acct, acct_bytes, hipMemcpyDeviceToHost, sm));
+        PITT_HIP_TRY(hipMemcpyAsync((char*)hacct + acct_bytes, acct_tiles, tile_words * 2 * 4, hipMemcpyDeviceToHost, sm));
+    }
     // completion (pitt_wait): copy results out, price the score launches
     ctx->inflight = true;
     ctx->inflight_results = results;
@@ -1409,6 +1455,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ctx->inflight_score_recs = score_recs;
     ctx->inflight_chunks = chunks;
     ctx->inflight_hstat = hstat;
+    ctx->inflight_acct = hacct;
+    ctx->inflight_acct_tiles = (int64_t)tile_words;
+    ctx->inflight_acct_recs = acct_recs;
     ctx->last_hcap = hcap;
     ctx->last_frames = nf;
     return PITT_OK;
@@ -1426,6 +1475,22 @@ int finish_batch(pitt_ctx* ctx) {
     for (size_t c = 0; c < ctx->inflight_score_recs.size(); ++c)
         ctx->prof_set_bytes(ctx->inflight_score_recs[c],
                             (double)hstat[c].tiles * kTile * 12.0 + (double)hstat[c].tiles * ctx->inflight_chunks[c] * 4.0);
+    if (ctx->inflight_acct) {  // the data-dependent kernels: bytes they actually moved
+        const unsigned long long* a = (const unsigned long long*)ctx->inflight_acct;
+        const uint32_t* tw = (const uint32_t*)(a + kAcKernels * kAcShards);
+        const int64_t nt = ctx->inflight_acct_tiles;
+        for (int k = 0; k < kAcKernels; ++k) {
+            double b = 0;
+            if (k == kAcSelMark || k == kAcSelWrite) {
+                const uint32_t* v = tw + (k == kAcSelMark ? 0 : nt);
+                for (int64_t i = 0; i < nt; ++i) b += (double)v[i];
+            } else {
+                for (int j = 0; j < kAcShards; ++j) b += (double)a[k * kAcShards + j];
+            }
+            ctx->prof_set_bytes(ctx->inflight_acct_recs[(size_t)k], b);
+        }
+        ctx->inflight_acct = nullptr;
+    }
     return PITT_OK;
 }
 

@@ -239,9 +239,10 @@ __global__ __launch_bounds__(kBlock) void k_bbox_tilemin(const float* __restrict
     }
 }
 
-// out[0..7]: xMax, xMin, yMax, yMin, zsum, zabs, q, exact(1/0)
-__global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, const float* __restrict__ z, int64_t n,
-                             double* __restrict__ out) {
+// out[0..7]: xMax, xMin, yMax, yMin, zsum (tile partials in tile order), zabs, q, exact(1/0).  The
+// host turns zsum into zMed and certifies it (zmed_certified); only an uncertifiable sum pays the
+// reference's sequential double loop (k_zsum_seq).
+__global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, double* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     float mx = -INFINITY, my = -INFINITY, cx = INFINITY, cy = INFINITY;
     double zs = 0.0, za = 0.0;
@@ -256,12 +257,34 @@ __global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, con
         q = min(q, tiles[t].q);
     }
     const bool exact = (q == (1 << 30)) || (za <= ldexp(1.0, 52 + q));
-    if (!exact) {  // fall back to the reference's sequential double sum
-        zs = 0.0;
-        for (int64_t i = 0; i < n; ++i) zs += (double)z[i];
-    }
     out[0] = mx; out[1] = cx; out[2] = my; out[3] = cy;
     out[4] = zs; out[5] = za; out[6] = q; out[7] = exact ? 1.0 : 0.0;
+}
+
+// supports_segmentation_srv.cpp:207,217: the reference's sequential double sum of z.
+__global__ void k_zsum_seq(const float* __restrict__ z, int64_t n, double* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double zs = 0.0;
+    for (int64_t i = 0; i < n; ++i) zs += (double)z[i];
+    *out = zs;
+}
+
+// zMed = zsum / n + off computed from a sum in another association: the sequential sum differs by
+// at most 2 (n - 1) u sum|z| (u = 2^-53, both sums' error bounds), the division and the addition
+// add a few ulps.  If no float lies within that bound of zMed, every `(double)z > zMed` test of
+// the on-support filter decides the same way for the sequential value: returns true and zMed.
+static bool zmed_certified(double zsum, double zabs, int64_t n, double off, double* zmed) {
+    const double u = std::ldexp(1.0, -53);
+    const double m = zsum / (double)n + off;
+    const double b = 2.0000001 * (double)(n - 1) * u * zabs / (double)n * (1.0 + 4.0 * u) +
+                     8.0 * u * (std::fabs(zsum) / (double)n + std::fabs(off) + std::fabs(m)) + 1e-300;
+    const double lo = m - b, hi = m + b;
+    if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
+    float f = (float)hi;                    // the largest float <= hi
+    if ((double)f > hi) f = std::nextafter(f, -INFINITY);
+    if ((double)f >= lo) return false;      // a float inside [lo, hi]: the sums' rounding could matter
+    *zmed = m;
+    return true;
 }
 
 struct OnSupport {
@@ -429,16 +452,25 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
             hipLaunchKernelGGL(k_bbox_tilescan, dim3(1), dim3(64), 0, s, BT, nt, PRE);
             hipLaunchKernelGGL(k_bbox_tilemin, dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, S, S + cap, S + 2 * cap,
                                n_inl, PRE, BT);
-            hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, BT, nt, S + 2 * cap, n_inl, BB);
+            hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, BT, nt, BB);
             double* hb = (double*)ctx->pinned("sup_bb_h", 8 * sizeof(double));
             PITT_HIP_TRY(hipMemcpyAsync(hb, BB, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
             PITT_HIP_TRY(hipStreamSynchronize(s));
-            double xMax = hb[0], xMin = hb[1], yMax = hb[2], yMin = hb[3], zMed = hb[4];
+            double xMax = hb[0], xMin = hb[1], yMax = hb[2], yMin = hb[3], zMed = 0.0;
             xMax -= sp->edge_remove_offset[0];
             xMin += sp->edge_remove_offset[0];
             yMax -= sp->edge_remove_offset[1];
             yMin += sp->edge_remove_offset[1];
-            zMed = zMed / (double)n_inl + sp->edge_remove_offset[2];
+            const double off_z = sp->edge_remove_offset[2];
+            if (hb[7] != 0.0) {  // every partial sum exact: any association gives the sequential value
+                zMed = hb[4] / (double)n_inl + off_z;
+            } else if (!zmed_certified(hb[4], hb[5], n_inl, off_z, &zMed)) {
+                hipLaunchKernelGGL(k_zsum_seq, dim3(1), dim3(64), 0, s, S + 2 * cap, n_inl, BB + 4);
+                PITT_HIP_TRY(hipMemcpyAsync(hb, BB, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+                PITT_HIP_TRY(hipStreamSynchronize(s));
+                zMed = hb[4] / (double)n_inl + off_z;
+                ++ctx->zsum_sequential;
+            }
             int64_t n_on = 0;
             rc = run_compact(ctx, N,
                              OnSupport{O, O + cap, O + 2 * cap, MAP[mcur ^ 1], lv, xMin, xMax, yMin, yMax, zMed},
