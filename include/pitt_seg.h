@@ -20,6 +20,8 @@
  *        src/obj_segmentation.cpp:248
  *   pitt_unpack_pointcloud2       replaces  fromROSMsg (PointCloud2 -> PointCloud<PointXYZ>)
  *        src/point_cloud_library/pc_manager.cpp:94-104
+ *   pitt_voxel_grid               replaces  VoxelGrid<PointXYZ>::filter (PCManager::downSampling)
+ *        src/point_cloud_library/pc_manager.cpp:55-67, src/obj_segmentation.cpp:238
  *
  * Conventions: plain pointers and sizes, no C++ types, no exceptions.  Every call returns an
  * int status (PITT_OK, PITT_NO_MODEL, or a negative PITT_E_*).  A context is not thread-safe;
@@ -227,6 +229,20 @@ int pitt_transform_cloud(pitt_ctx* ctx, const float* x, const float* y, const fl
 int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes, int32_t width, int32_t height,
                             int32_t point_step, int64_t row_step, int32_t off_x, int32_t off_y, int32_t off_z,
                             float* x, float* y, float* z);
+
+/* pcl::VoxelGrid<PointXYZ> downsampling as called by PCManager::downSampling,
+ * src/point_cloud_library/pc_manager.cpp:55-67 (leaf 0.01 m, :19; called at obj_segmentation.cpp:238).
+ * PCL 1.7 applyFilter: one output point per occupied leaf, in ascending leaf index
+ * (i + j div_x + k div_x div_y); its value is the float mean of the leaf's finite points (sum, then
+ * times 1/n).  Non-finite points never count.  When the grid would overflow int32 PCL warns and
+ * returns the input unchanged: then out = in, *n_out = n and *flags |= PITT_VOXEL_OVERFLOW_COPY.
+ * The points inside a leaf are summed in ascending point order (PCL's std::sort leaves them in
+ * libstdc++'s introsort order), so a centroid may differ from PCL's in its last bits.
+ * Device SoA in; device SoA out of capacity n.  Leaf sizes must be > 0. */
+#define PITT_VOXEL_OVERFLOW_COPY 1
+int pitt_voxel_grid(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                    float leaf_x, float leaf_y, float leaf_z, float* out_x, float* out_y, float* out_z,
+                    int64_t* n_out, int32_t* flags);
 
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };

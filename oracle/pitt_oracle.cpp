@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -749,6 +750,92 @@ int orc_transform_cloud(const float* x, const float* y, const float* z, int64_t 
         oy[i] = m[4] * px + m[5] * py + m[6] * pz + m[7];
         oz[i] = m[8] * px + m[9] * py + m[10] * pz + m[11];
     }
+    return 0;
+}
+
+// pcl::VoxelGrid<PointXYZ>::applyFilter (PCL 1.7 filters/impl/voxel_grid.hpp, absent here) as used by
+// PCManager::downSampling (pc_manager.cpp:61-67, leaf 0.01 m from :19; called at
+// obj_segmentation.cpp:238).  Defaults: no filter field, downsample_all_data_ = true (x, y, z are the
+// PointXYZ fields), min_points_per_voxel_ = 0.
+//   * getMinMax3D over the finite points (Array4f min/max in float);
+//   * dx = (int64)((max - min) * inv) + 1 per axis, inv = 1.0f / leaf; dx*dy*dz > INT32_MAX: the
+//     filter warns and outputs the input cloud unchanged (return 1);
+//   * min_b = (int)floor(min * inv); div_b = max_b - min_b + 1; divb_mul = (1, div_b0, div_b0*div_b1);
+//   * per finite point (in input order): ijk = (int)(floor(p * inv) - (float)min_b),
+//     idx = ijk0 + ijk1 * divb_mul1 + ijk2 * divb_mul2;
+//   * std::sort of (idx, point index) pairs by idx only -- NOT stable: the order inside a voxel is
+//     libstdc++'s introsort permutation (this build's libstdc++; assumption A10).  sort_mode 1 uses
+//     std::stable_sort instead (ascending point index inside a voxel);
+//   * per voxel, ascending idx: centroid = first point, += the others in sorted order (float),
+//     then `centroid /= n` -- Eigen 3.2 multiplies by 1.0f / n (A9).
+// Non-finite points never enter (the is_dense == false path; a dense cloud has none).
+struct VoxPair {
+    uint32_t idx, cloud_point_index;
+    bool operator<(const VoxPair& o) const { return idx < o.idx; }
+};
+
+int orc_voxel_grid(const float* x, const float* y, const float* z, int64_t n, float lx, float ly, float lz,
+                   int32_t sort_mode, float* ox, float* oy, float* oz, int64_t* n_out) {
+    const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    const float* c[3] = {x, y, z};
+    int64_t finite = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!(std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]))) continue;
+        ++finite;
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = c[k][i] < mn[k] ? c[k][i] : mn[k];  // Eigen cwiseMin: std::min(a, b)
+            mx[k] = mx[k] < c[k][i] ? c[k][i] : mx[k];
+        }
+    }
+    *n_out = 0;
+    if (finite == 0) return 0;
+    int64_t d[3];
+    for (int k = 0; k < 3; ++k) d[k] = (int64_t)((mx[k] - mn[k]) * inv[k]) + 1;
+    if (d[0] * d[1] * d[2] > (int64_t)INT32_MAX) {
+        for (int64_t i = 0; i < n; ++i) {
+            ox[i] = x[i];
+            oy[i] = y[i];
+            oz[i] = z[i];
+        }
+        *n_out = n;
+        return 1;
+    }
+    int min_b[3], max_b[3], div_b[3];
+    for (int k = 0; k < 3; ++k) {
+        min_b[k] = (int)std::floor(mn[k] * inv[k]);
+        max_b[k] = (int)std::floor(mx[k] * inv[k]);
+        div_b[k] = max_b[k] - min_b[k] + 1;
+    }
+    const int mul[3] = {1, div_b[0], div_b[0] * div_b[1]};
+    std::vector<VoxPair> v;
+    v.reserve((size_t)finite);
+    for (int64_t i = 0; i < n; ++i) {
+        if (!(std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]))) continue;
+        int idx = 0;
+        for (int k = 0; k < 3; ++k) idx += (int)(std::floor(c[k][i] * inv[k]) - (float)min_b[k]) * mul[k];
+        v.push_back({(uint32_t)idx, (uint32_t)i});
+    }
+    if (sort_mode == 1) std::stable_sort(v.begin(), v.end());
+    else std::sort(v.begin(), v.end());
+    int64_t out = 0;
+    for (size_t a = 0; a < v.size();) {
+        size_t b = a + 1;
+        while (b < v.size() && v[b].idx == v[a].idx) ++b;
+        float s[3] = {x[v[a].cloud_point_index], y[v[a].cloud_point_index], z[v[a].cloud_point_index]};
+        for (size_t j = a + 1; j < b; ++j) {
+            s[0] += x[v[j].cloud_point_index];
+            s[1] += y[v[j].cloud_point_index];
+            s[2] += z[v[j].cloud_point_index];
+        }
+        const float r = 1.0f / (float)(b - a);
+        ox[out] = s[0] * r;
+        oy[out] = s[1] * r;
+        oz[out] = s[2] * r;
+        ++out;
+        a = b;
+    }
+    *n_out = out;
     return 0;
 }
 

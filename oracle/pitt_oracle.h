@@ -118,6 +118,10 @@ int     orc_unpack_pointcloud2(const uint8_t* data, int32_t width, int32_t heigh
                                float* x, float* y, float* z);
 int     orc_transform_cloud(const float* x, const float* y, const float* z, int64_t n, const float m[16],
                             int32_t dense, float* ox, float* oy, float* oz);
+// VoxelGrid<PointXYZ>::applyFilter (pc_manager.cpp:61-67); sort_mode 0 = std::sort (PCL), 1 = stable.
+// Returns 1 when the grid would overflow int32 (the output is then the input, n_out = n).
+int     orc_voxel_grid(const float* x, const float* y, const float* z, int64_t n, float lx, float ly, float lz,
+                       int32_t sort_mode, float* ox, float* oy, float* oz, int64_t* n_out);
 
 #ifdef __cplusplus
 }

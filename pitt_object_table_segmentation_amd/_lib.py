@@ -21,6 +21,7 @@ PITT_E_SAMPLER = -4
 PITT_E_NODEVICE = -5
 PITT_TILE_POINTS = 2048
 PITT_FLAG_K_NEAR_INTEGER = 1
+PITT_VOXEL_OVERFLOW_COPY = 1
 
 REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
 DIV_EIGEN32, DIV_TRUE = 0, 1
@@ -144,6 +145,8 @@ SIGNATURES = {
                                 _i64p, _f32p]),
     "pitt_transform_cloud": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp]),
     "pitt_unpack_pointcloud2": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
+                               _vp, _i64p, _i32p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
     "pitt_find_supports": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.POINTER(SupportParams),
                                   ctypes.POINTER(SupportList)]),

@@ -324,6 +324,19 @@ class Context:
                                                 z.data_ptr()), "pitt_unpack_pointcloud2")
         return x[:n], y[:n], z[:n]
 
+    def voxel_grid(self, x, y, z, leaf=(0.01, 0.01, 0.01)):
+        """VoxelGrid<PointXYZ> downsampling (pc_manager.cpp:55-67) on device tensors: returns device
+        (x, y, z) of the leaf centroids in ascending leaf index, and the flags (PITT_VOXEL_OVERFLOW_COPY)."""
+        import torch
+        n = x.numel()
+        ox, oy, oz = (torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(3))
+        m, fl = ctypes.c_int64(), ctypes.c_int32()
+        self._check(lib.pitt_voxel_grid(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, float(leaf[0]),
+                                        float(leaf[1]), float(leaf[2]), ox.data_ptr(), oy.data_ptr(), oz.data_ptr(),
+                                        ctypes.byref(m), ctypes.byref(fl)), "pitt_voxel_grid")
+        k = m.value
+        return (ox[:k], oy[:k], oz[:k]), fl.value
+
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
         x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))

@@ -226,3 +226,19 @@ def unpack_pointcloud2(data: np.ndarray, width, height, point_step, row_step, of
     O.orc_unpack_pointcloud2(data.ctypes.data, width, height, point_step, row_step, *offsets,
                              _fp(o[0]), _fp(o[1]), _fp(o[2]))
     return o[:, :n].T.copy()
+
+
+O.orc_voxel_grid.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                     ctypes.c_int32] + [ctypes.c_void_p] * 4
+SORT_PCL, SORT_STABLE = 0, 1
+
+
+def voxel_grid(x, y, z, leaf=(0.01, 0.01, 0.01), sort_mode=SORT_PCL):
+    """VoxelGrid<PointXYZ>::applyFilter restated (pc_manager.cpp:61-67): (Nx3 centroids, overflow flag)."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    o = np.empty((3, max(n, 1)), np.float32)
+    m = ctypes.c_int64()
+    rc = O.orc_voxel_grid(_fp(x), _fp(y), _fp(z), n, *leaf, sort_mode, _fp(o[0]), _fp(o[1]), _fp(o[2]),
+                          ctypes.byref(m))
+    return o[:, :m.value].T.copy(), rc

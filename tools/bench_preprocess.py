@@ -67,6 +67,26 @@ def main():
             res[k] = {"avg_us": round(per, 1), "algorithmic_bytes": byts,
                       "GB_s": round(byts / per / 1e3, 1), "frac": round(byts / per / 1e3 / PEAK, 3)}
         ctx.profile(False)
+        # VoxelGrid 1 cm, one 640x480 frame per call as downSampling runs it (16 distinct frames)
+        frames = [tuple(t[f * n1:(f + 1) * n1] for t in (dx, dy, dz)) for f in range(min(16, args.frames))]
+        for fr in frames:
+            ctx.voxel_grid(*fr)
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        t0 = time.perf_counter()
+        vox_reps = 4
+        for _ in range(vox_reps):
+            for fr in frames:
+                (vx, _, _), _ = ctx.voxel_grid(*fr)
+        torch.cuda.synchronize()
+        vox_ms = (time.perf_counter() - t0) * 1e3 / (vox_reps * len(frames))
+        vox = {"ms_per_frame_wall": round(vox_ms, 4), "leaves_last_frame": int(vx.numel()), "kernels": {}}
+        for k in ("k_vox_minmax", "k_vox_keys", "vox_radix_sort", "k_vox_runs", "k_vox_centroid"):
+            launches, ms, algo = ctx.profile_get(k)
+            if launches:
+                vox["kernels"][k] = {"avg_us": round(ms / launches * 1e3, 1)}
+        ctx.profile(False)
     import oracle_binding as orc
     t0 = time.perf_counter()
     k = 0
@@ -76,9 +96,13 @@ def main():
         orc.transform_cloud(*rc.T, m)
         k += 1
     cpu = k * n1 / (time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    for f in range(4):
+        orc.voxel_grid(*(a[f * n1:(f + 1) * n1] for a in (x, y, z)))
+    vox["cpu_oracle_ms_per_frame_1thread"] = round((time.perf_counter() - t0) * 1e3 / 4, 2)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
                                   f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
-                      "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu),
+                      "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox,
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
 
