@@ -124,3 +124,27 @@ def test_preprocessing_entry_points_reject_null_context():
     n, fl = ctypes.c_int64(), ctypes.c_int32()
     assert lib.pitt_voxel_grid(None, None, None, None, 0, 0.01, 0.01, 0.01, None, None, None, ctypes.byref(n),
                                ctypes.byref(fl)) == L.PITT_E_INVALID
+
+
+def test_ros_adapters_use_only_declared_abi():
+    """adapters/ros/ (compiled only where ROS and pitt_msgs exist) calls nothing but the C ABI that
+    include/*.h declares, and advertises the reference's service names (srv_manager.h:25-32)."""
+    import glob
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    declared = set()
+    for h in glob.glob(os.path.join(root, "include", "*.h")):
+        declared |= set(re.findall(r"\b(pitt_\w+)\s*\(", open(h).read()))
+    srcs = glob.glob(os.path.join(root, "adapters", "ros", "*.cpp")) + \
+        glob.glob(os.path.join(root, "adapters", "ros", "*.hpp"))
+    assert len(srcs) == 5
+    used = set()
+    for s in srcs:
+        used |= set(re.findall(r"\b(pitt_(?!ros\b)\w+)\s*\(", open(s).read()))
+    assert used and used <= declared, sorted(used - declared)
+    names = {"plane_segmentation_node.cpp": "plane_segmentation_srv", "deep_filter_node.cpp": "deep_filter_srv",
+             "supports_segmentation_node.cpp": "support_segmentation_srv",
+             "cluster_segmentation_node.cpp": "cluster_Segmentation_srv"}
+    for f, name in names.items():
+        assert f'advertiseService("{name}"' in open(os.path.join(root, "adapters", "ros", f)).read(), f
