@@ -10,7 +10,8 @@ import importlib.util
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpitt_seg.so")
+# PITT_LIB_PATH: an alternative build of the same library (A/B experiments, tools/ only)
+LIB_PATH = os.environ.get("PITT_LIB_PATH") or os.path.join(_HERE, "libpitt_seg.so")
 
 PITT_OK = 0
 PITT_NO_MODEL = 1
