@@ -22,6 +22,8 @@
  *        src/point_cloud_library/pc_manager.cpp:94-104
  *   pitt_voxel_grid               replaces  VoxelGrid<PointXYZ>::filter (PCManager::downSampling)
  *        src/point_cloud_library/pc_manager.cpp:55-67, src/obj_segmentation.cpp:238
+ *   pitt_normal_estimation        replaces  NormalEstimation<PointXYZ, Normal>::compute (estimateNormal)
+ *        src/point_cloud_library/pc_manager.cpp:68-78
  *
  * Conventions: plain pointers and sizes, no C++ types, no exceptions.  Every call returns an
  * int status (PITT_OK, PITT_NO_MODEL, or a negative PITT_E_*).  A context is not thread-safe;
@@ -243,6 +245,18 @@ int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes,
 int pitt_voxel_grid(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                     float leaf_x, float leaf_y, float leaf_z, float* out_x, float* out_y, float* out_z,
                     int64_t* n_out, int32_t* flags);
+
+/* pcl::NormalEstimation<PointXYZ, Normal> with a search::KdTree and setKSearch(k), as called by
+ * PCManager::estimateNormal, src/point_cloud_library/pc_manager.cpp:68-78 (k = 50, :18; called at
+ * obj_segmentation.cpp:253 and ransac_segmentation.cpp:233).  Per point: the k nearest finite points
+ * (exact; k clamped to the finite count) in ascending float distance (dx*dx + dy*dy) + dz*dz, ties by
+ * point index; the float covariance over them in that order, eigen33, curvature |l_min / trace|, the
+ * normal flipped towards `viewpoint` (NULL = origin, PCL's default).  A non-finite point or fewer than
+ * 3 neighbours gives NaN.  Device SoA in; device outputs of n floats each.  neighbours (n * k int32) and
+ * neighbour_count (n) are optional device outputs (the lists in summation order).  k in [1, 64]. */
+int pitt_normal_estimation(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                           int32_t k, const float viewpoint[3], float* nx, float* ny, float* nz,
+                           float* curvature, int32_t* neighbours, int32_t* neighbour_count);
 
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };

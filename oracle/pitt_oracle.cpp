@@ -839,4 +839,134 @@ int orc_voxel_grid(const float* x, const float* y, const float* z, int64_t n, fl
     return 0;
 }
 
+// pcl::NormalEstimation<PointXYZ, Normal>::compute with a search::KdTree and setKSearch(k), as
+// PCManager::estimateNormal (pc_manager.cpp:68-78, k = 50 from :18; called at obj_segmentation.cpp:253
+// and ransac_segmentation.cpp:233).  PCL 1.7 features/impl/normal_3d.hpp + feature.h:
+//   * neighbours: KdTreeFLANN::nearestKSearch(point, k) -- exact (eps 0), k clamped to the number of
+//     indexed (finite) points, results ascending by FLANN's L2_Simple float distance
+//     ((dx*dx + dy*dy) + dz*dz, dx = query - point); equal distances in ascending point index here
+//     (FLANN keeps its traversal order: assumption A11, exact ties only between duplicate points);
+//   * computePointNormal: < 3 neighbours -> NaN; else computeMeanAndCovarianceMatrix over the
+//     neighbours in that order (the nine float accumulators, `accu /= n` as x * (1/n), A6/A9), then
+//     solvePlaneParameters: eigen33 -> (nx, ny, nz), curvature = |l_min / (c00 + c11 + c22)| (0 when
+//     the trace is 0);
+//   * flipNormalTowardsViewpoint: (vp - p) . n = ((vx*nx + vy*ny) + vz*nz) < 0 -> negate;
+//   * a non-finite query point (is_dense == false) gets NaN normal and curvature.
+// Exact kNN by rings of a uniform grid (the ring is grown until the k-th distance is certainly
+// below the distance of every point outside it).
+int orc_normal_estimation(const float* x, const float* y, const float* z, int64_t n, int32_t k, const float vp[3],
+                          float* nx, float* ny, float* nz, float* curv, int32_t* nn_out, int32_t* nn_cnt) {
+    const float qnan = std::numeric_limits<float>::quiet_NaN();
+    auto fin = [&](int64_t i) { return std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]); };
+    std::vector<int32_t> pts;
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    for (int64_t i = 0; i < n; ++i) {
+        if (!fin(i)) continue;
+        pts.push_back((int32_t)i);
+        const double p[3] = {x[i], y[i], z[i]};
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = std::min(mn[a], p[a]);
+            mx[a] = std::max(mx[a], p[a]);
+        }
+    }
+    const int64_t nf = (int64_t)pts.size();
+    const int kk = (int)std::min<int64_t>(k, nf);
+    double h = 0.05;
+    if (nf > 0) {  // ~16 points per occupied cell on a surface-like cloud
+        double ext = std::max(mx[0] - mn[0], std::max(mx[1] - mn[1], mx[2] - mn[2]));
+        h = std::max(ext / 64.0, 1e-6);
+        for (int it = 0; it < 2; ++it) {
+            std::unordered_map<uint64_t, int> occ;
+            for (int32_t i : pts) {
+                const int64_t c[3] = {(int64_t)((x[i] - mn[0]) / h), (int64_t)((y[i] - mn[1]) / h),
+                                      (int64_t)((z[i] - mn[2]) / h)};
+                ++occ[(uint64_t)c[0] | ((uint64_t)c[1] << 21) | ((uint64_t)c[2] << 42)];
+            }
+            const double per = (double)nf / (double)occ.size();
+            h = std::max(h * std::sqrt(16.0 / per), 1e-6);
+        }
+    }
+    int64_t dim[3];
+    for (int a = 0; a < 3; ++a) dim[a] = nf ? (int64_t)((mx[a] - mn[a]) / h) + 1 : 1;
+    std::unordered_map<uint64_t, std::vector<int32_t>> grid;
+    auto key = [](int64_t a, int64_t b, int64_t c) { return (uint64_t)a | ((uint64_t)b << 21) | ((uint64_t)c << 42); };
+    std::vector<int64_t> cell((size_t)n * 3, 0);
+    for (int32_t i : pts) {
+        cell[3 * i] = (int64_t)((x[i] - mn[0]) / h);
+        cell[3 * i + 1] = (int64_t)((y[i] - mn[1]) / h);
+        cell[3 * i + 2] = (int64_t)((z[i] - mn[2]) / h);
+        grid[key(cell[3 * i], cell[3 * i + 1], cell[3 * i + 2])].push_back(i);
+    }
+    const int64_t rmax = std::max(dim[0], std::max(dim[1], dim[2]));
+    std::vector<std::pair<float, int32_t>> cand;
+    for (int64_t q = 0; q < n; ++q) {
+        if (nn_cnt) nn_cnt[q] = 0;
+        if (!fin(q) || kk < 3) {  // no normal: no neighbour list is summed (count 0)
+            nx[q] = ny[q] = nz[q] = curv[q] = qnan;
+            continue;
+        }
+        for (int64_t r = 1;; ++r) {
+            cand.clear();
+            for (int64_t a = cell[3 * q] - r; a <= cell[3 * q] + r; ++a)
+                for (int64_t b = cell[3 * q + 1] - r; b <= cell[3 * q + 1] + r; ++b)
+                    for (int64_t c = cell[3 * q + 2] - r; c <= cell[3 * q + 2] + r; ++c) {
+                        if (a < 0 || b < 0 || c < 0 || a >= dim[0] || b >= dim[1] || c >= dim[2]) continue;
+                        auto it = grid.find(key(a, b, c));
+                        if (it == grid.end()) continue;
+                        for (int32_t j : it->second) {
+                            const float dx = x[q] - x[j], dy = y[q] - y[j], dz = z[q] - z[j];
+                            cand.emplace_back(dx * dx + dy * dy + dz * dz, j);
+                        }
+                    }
+            if ((int)cand.size() < kk && r < rmax) continue;
+            std::partial_sort(cand.begin(), cand.begin() + kk, cand.end());
+            const double lim = (double)r * h;
+            if (r >= rmax || (double)cand[(size_t)kk - 1].first <= lim * lim * (1.0 - 1e-5)) break;
+        }
+        float a9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t = 0; t < kk; ++t) {
+            const int32_t j = cand[(size_t)t].second;
+            if (nn_out) nn_out[(size_t)q * k + t] = j;
+            const float px = x[j], py = y[j], pz = z[j];
+            a9[0] += px * px;
+            a9[1] += px * py;
+            a9[2] += px * pz;
+            a9[3] += py * py;
+            a9[4] += py * pz;
+            a9[5] += pz * pz;
+            a9[6] += px;
+            a9[7] += py;
+            a9[8] += pz;
+        }
+        if (nn_cnt) nn_cnt[q] = kk;
+        const float rcp = 1.0f / (float)kk;
+        for (int t = 0; t < 9; ++t) a9[t] = a9[t] * rcp;
+        float cov[9];
+        cov[0] = a9[0] - a9[6] * a9[6];
+        cov[1] = a9[1] - a9[6] * a9[7];
+        cov[2] = a9[2] - a9[6] * a9[8];
+        cov[4] = a9[3] - a9[7] * a9[7];
+        cov[5] = a9[4] - a9[7] * a9[8];
+        cov[8] = a9[5] - a9[8] * a9[8];
+        cov[3] = cov[1];
+        cov[6] = cov[2];
+        cov[7] = cov[5];
+        float ev, e[3];
+        eigen33(cov, ORC_TRIG_CR, &ev, e);
+        const float tr = cov[0] + cov[4] + cov[8];
+        curv[q] = tr != 0.0f ? std::fabs(ev / tr) : 0.0f;
+        const float vx = vp[0] - x[q], vy = vp[1] - y[q], vz = vp[2] - z[q];
+        const float ct = vx * e[0] + vy * e[1] + vz * e[2];
+        if (ct < 0) {
+            e[0] *= -1.0f;
+            e[1] *= -1.0f;
+            e[2] *= -1.0f;
+        }
+        nx[q] = e[0];
+        ny[q] = e[1];
+        nz[q] = e[2];
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -122,6 +122,11 @@ int     orc_transform_cloud(const float* x, const float* y, const float* z, int6
 // Returns 1 when the grid would overflow int32 (the output is then the input, n_out = n).
 int     orc_voxel_grid(const float* x, const float* y, const float* z, int64_t n, float lx, float ly, float lz,
                        int32_t sort_mode, float* ox, float* oy, float* oz, int64_t* n_out);
+// NormalEstimation<PointXYZ, Normal> with KdTree + setKSearch(k) (pc_manager.cpp:68-78), viewpoint vp.
+// nn_out (n x k, optional) / nn_cnt (n, optional): the neighbours in summation order.
+int     orc_normal_estimation(const float* x, const float* y, const float* z, int64_t n, int32_t k,
+                              const float vp[3], float* nx, float* ny, float* nz, float* curv,
+                              int32_t* nn_out, int32_t* nn_cnt);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,7 @@ SIGNATURES = {
                                 _i64p, _f32p]),
     "pitt_transform_cloud": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp]),
     "pitt_unpack_pointcloud2": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "pitt_normal_estimation": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32p, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
                                _vp, _i64p, _i32p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),

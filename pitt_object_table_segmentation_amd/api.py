@@ -337,6 +337,21 @@ class Context:
         k = m.value
         return (ox[:k], oy[:k], oz[:k]), fl.value
 
+    def normal_estimation(self, x, y, z, k: int = 50, viewpoint=(0.0, 0.0, 0.0), neighbours: bool = False):
+        """NormalEstimation with KdTree + setKSearch(k) (pc_manager.cpp:68-78) on device tensors:
+        returns device (nx, ny, nz, curvature) [and (neighbour lists n x k, counts n)]."""
+        import torch
+        n = x.numel()
+        out = [torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(4)]
+        nn = torch.full((max(n, 1), k), -1, dtype=torch.int32, device=x.device) if neighbours else None
+        cnt = torch.zeros(max(n, 1), dtype=torch.int32, device=x.device) if neighbours else None
+        vp = np.asarray(viewpoint, np.float32)
+        self._check(lib.pitt_normal_estimation(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, int(k), _fp(vp),
+                                               *(o.data_ptr() for o in out), None if nn is None else nn.data_ptr(),
+                                               None if cnt is None else cnt.data_ptr()), "pitt_normal_estimation")
+        res = tuple(o[:n] for o in out)
+        return res + ((nn[:n], cnt[:n]),) if neighbours else res
+
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
         x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))

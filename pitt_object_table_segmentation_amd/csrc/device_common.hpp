@@ -109,8 +109,9 @@ __device__ inline void compute_roots(const float m[9], float r[3]) {
 
 __device__ __forceinline__ float sqnorm3(float a, float b, float c) { return a * a + (b * b + c * c); }
 
-// Smallest eigenpair's vector of a symmetric 3x3 (row-major), as pcl::eigen33.
-__device__ inline void eigen33(const float mat[9], float vec[3]) {
+// Smallest eigenpair of a symmetric 3x3 (row-major), as pcl::eigen33(mat, eigenvalue, eigenvector):
+// eigenvalue = roots[0] * scale.
+__device__ inline void eigen33v(const float mat[9], float* value, float vec[3]) {
     float scale = 0.0f;
 #pragma unroll
     for (int i = 0; i < 9; ++i) scale = std_max(scale, fabsf(mat[i]));
@@ -120,6 +121,7 @@ __device__ inline void eigen33(const float mat[9], float vec[3]) {
     for (int i = 0; i < 9; ++i) sm[i] = mat[i] / scale;
     float r[3];
     compute_roots(sm, r);
+    *value = r[0] * scale;
     sm[0] -= r[0];
     sm[4] -= r[0];
     sm[8] -= r[0];
@@ -136,6 +138,12 @@ __device__ inline void eigen33(const float mat[9], float vec[3]) {
     vec[0] = ox / s;
     vec[1] = oy / s;
     vec[2] = oz / s;
+}
+
+// The eigenvector only (optimizeModelCoefficients).
+__device__ inline void eigen33(const float mat[9], float vec[3]) {
+    float v;
+    eigen33v(mat, &v, vec);
 }
 
 // Block-wide exclusive scan of one int per thread (kBlock threads, 4 waves).

@@ -242,3 +242,21 @@ def voxel_grid(x, y, z, leaf=(0.01, 0.01, 0.01), sort_mode=SORT_PCL):
     rc = O.orc_voxel_grid(_fp(x), _fp(y), _fp(z), n, *leaf, sort_mode, _fp(o[0]), _fp(o[1]), _fp(o[2]),
                           ctypes.byref(m))
     return o[:, :m.value].T.copy(), rc
+
+
+O.orc_normal_estimation.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 7
+
+
+def normal_estimation(x, y, z, k=50, viewpoint=(0.0, 0.0, 0.0), neighbours=False):
+    """NormalEstimation<PointXYZ, Normal>, KdTree, setKSearch(k) restated (pc_manager.cpp:68-78):
+    (normals Nx3, curvature N) [, (neighbour lists N x k, counts N)]."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    vp = np.asarray(viewpoint, np.float32)
+    o = np.empty((4, max(n, 1)), np.float32)
+    nn = np.full((max(n, 1), k), -1, np.int32) if neighbours else None
+    cnt = np.zeros(max(n, 1), np.int32)
+    O.orc_normal_estimation(_fp(x), _fp(y), _fp(z), n, k, _fp(vp), _fp(o[0]), _fp(o[1]), _fp(o[2]), _fp(o[3]),
+                            None if nn is None else _ip(nn), _ip(cnt))
+    out = (o[:3, :n].T.copy(), o[3, :n].copy())
+    return out + ((nn[:n], cnt[:n]),) if neighbours else out

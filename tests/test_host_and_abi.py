@@ -124,6 +124,8 @@ def test_preprocessing_entry_points_reject_null_context():
     n, fl = ctypes.c_int64(), ctypes.c_int32()
     assert lib.pitt_voxel_grid(None, None, None, None, 0, 0.01, 0.01, 0.01, None, None, None, ctypes.byref(n),
                                ctypes.byref(fl)) == L.PITT_E_INVALID
+    assert lib.pitt_normal_estimation(None, None, None, None, 0, 50, None, None, None, None, None, None,
+                                      None) == L.PITT_E_INVALID
 
 
 def test_ros_adapters_use_only_declared_abi():

@@ -87,6 +87,24 @@ def main():
             if launches:
                 vox["kernels"][k] = {"avg_us": round(ms / launches * 1e3, 1)}
         ctx.profile(False)
+        # NormalEstimation k = 50 on the voxelized frames (estimateNormal's input, obj_segmentation.cpp:253)
+        vframes = [ctx.voxel_grid(*fr)[0] for fr in frames]
+        for vf in vframes[:2]:
+            ctx.normal_estimation(*vf)
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        t0 = time.perf_counter()
+        for vf in vframes:
+            ctx.normal_estimation(*vf)
+        torch.cuda.synchronize()
+        nrm = {"ms_per_frame_wall": round((time.perf_counter() - t0) * 1e3 / len(vframes), 4),
+               "points_per_frame": int(vframes[0][0].numel()), "k": 50, "kernels": {}}
+        for kname in ("k_nrm_grid", "k_knn", "k_normals"):
+            launches, ms, algo = ctx.profile_get(kname)
+            if launches:
+                nrm["kernels"][kname] = {"avg_us": round(ms / launches * 1e3, 1)}
+        ctx.profile(False)
     import oracle_binding as orc
     t0 = time.perf_counter()
     k = 0
@@ -100,9 +118,13 @@ def main():
     for f in range(4):
         orc.voxel_grid(*(a[f * n1:(f + 1) * n1] for a in (x, y, z)))
     vox["cpu_oracle_ms_per_frame_1thread"] = round((time.perf_counter() - t0) * 1e3 / 4, 2)
+    v0, _ = orc.voxel_grid(x[:n1], y[:n1], z[:n1])
+    t0 = time.perf_counter()
+    orc.normal_estimation(*v0.T)
+    nrm["cpu_oracle_ms_per_frame_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
                                   f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
-                      "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox,
+                      "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox, "normal_estimation": nrm,
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
 
