@@ -13,7 +13,8 @@
 // Device pipeline:
 //   k_vox_minmax (voxel.hip)  finite bounding box and count
 //   grid                      linear cell index per finite point (ordered compaction), stable radix
-//                             sort, per-cell [begin, end) in a dense table
+//                             sort, the points' coordinates in cell order, and a dense table of each
+//                             cell's first sorted position (a row of cells is one contiguous range)
 //   k_knn                     one wave per query: the cells of ring r around the query's cell are
 //                             streamed into an LDS candidate buffer (distance bits, point index); the
 //                             k best are selected by bisection on the distance bits (then on the index
@@ -24,6 +25,7 @@
 //                             eigen33, curvature, viewpoint flip
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cfloat>
@@ -79,18 +81,25 @@ struct WriteCellKey {
     }
 };
 
-__global__ void k_fill_i32(int32_t* __restrict__ p, int64_t n, int32_t v) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        p[i] = v;
+// points per cell (cstart = their exclusive prefix sum: the first sorted position of every cell)
+__global__ void k_cell_count(const uint32_t* __restrict__ key, int64_t m, int32_t* __restrict__ cnt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        if (i == 0 || key[i - 1] != key[i]) {
+            int64_t e = i + 1;
+            while (e < m && key[e] == key[i]) ++e;
+            cnt[key[i]] = (int32_t)(e - i);
+        }
 }
 
-// begin[c] / end[c] of every occupied cell from the sorted keys
-__global__ void k_cell_ranges(const uint32_t* __restrict__ key, int64_t m, int32_t* __restrict__ cbeg,
-                              int32_t* __restrict__ cend) {
+// the finite points' coordinates in cell order (contiguous candidate loads in k_knn)
+__global__ void k_gather_sorted(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+                                const uint32_t* __restrict__ idx, int64_t m, float* __restrict__ sx,
+                                float* __restrict__ sy, float* __restrict__ sz) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = key[i];
-        if (i == 0 || key[i - 1] != k) cbeg[k] = (int32_t)i;
-        if (i == m - 1 || key[i + 1] != k) cend[k] = (int32_t)(i + 1);
+        const uint32_t j = idx[i];
+        sx[i] = X[j];
+        sy[i] = Y[j];
+        sz[i] = Z[j];
     }
 }
 
@@ -110,47 +119,56 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 }
 
 // Keep the kk best (distance bits, index) of the fill candidates in slots [0, kk) (any order).
-// The candidates of lane l are slots l + 64 i.  Bisection on the distance bits finds D, the kk-th
-// smallest distance; ties at D are cut by the smallest indices (bisection on the index).
+// The candidates of lane l are slots l + 64 i (i < ceil(fill / 64)).  Bisection on the distance bits
+// (between the candidates' min and max) finds D, the kk-th smallest distance; ties at D are cut by the
+// smallest indices (bisection on the index).  Counts are ballots + popcounts: no cross-lane LDS
+// round trip per bisection step.
 __device__ int nn_select(uint32_t* __restrict__ bd, int32_t* __restrict__ bi, int fill, int kk, int lane) {
     if (fill <= kk) return fill;
     constexpr int R = kNnCap / 64;
+    const int ns = (fill + 63) >> 6;  // wave-uniform
     uint32_t d[R];
     int32_t ix[R];
+    uint32_t dmin = 0xFFFFFFFFu, dmax = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const int s = lane + 64 * i;
-        d[i] = s < fill ? bd[s] : 0xFFFFFFFFu;
-        ix[i] = s < fill ? bi[s] : 0x7FFFFFFF;
+        const bool in = i < ns && s < fill;
+        d[i] = in ? bd[s] : 0xFFFFFFFFu;
+        ix[i] = in ? bi[s] : 0x7FFFFFFF;
+        if (in) {
+            dmin = min(dmin, d[i]);
+            dmax = max(dmax, d[i]);
+        }
     }
-    uint32_t lo = 0, hi = 0x7F800000u;  // finite non-negative floats: bits order = value order
-    while (lo < hi) {                     // smallest D with #(d <= D) >= kk
-        const uint32_t mid = lo + ((hi - lo) >> 1);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o, 64));
+        dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, o, 64));
+    }
+    auto count = [&](auto pred) {
         int c = 0;
 #pragma unroll
-        for (int i = 0; i < R; ++i) c += d[i] <= mid ? 1 : 0;
-        if (wave_sum_i(c) >= kk) hi = mid;
+        for (int i = 0; i < R; ++i)
+            if (i < ns) c += __builtin_popcountll(__builtin_amdgcn_ballot_w64(pred(i)));
+        return c;
+    };
+    uint32_t lo = dmin, hi = dmax;  // finite non-negative floats: bits order = value order
+    while (lo < hi) {                // smallest D with #(d <= D) >= kk
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (count([&](int i) { return d[i] <= mid; }) >= kk) hi = mid;
         else lo = mid + 1;
     }
     const uint32_t D = lo;
-    int lt = 0, eq = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        lt += d[i] < D ? 1 : 0;
-        eq += d[i] == D ? 1 : 0;
-    }
-    lt = wave_sum_i(lt);
-    eq = wave_sum_i(eq);
+    const int lt = count([&](int i) { return d[i] < D; });
+    const int eq = count([&](int i) { return d[i] == D; });
     int32_t I = 0x7FFFFFFF;  // indices at D kept: idx <= I
     const int need = kk - lt;
     if (eq > need) {
         int32_t a = 0, b = 0x7FFFFFFF;
         while (a < b) {
             const int32_t mid = a + ((b - a) >> 1);
-            int c = 0;
-#pragma unroll
-            for (int i = 0; i < R; ++i) c += (d[i] == D && ix[i] <= mid) ? 1 : 0;
-            if (wave_sum_i(c) >= need) b = mid;
+            if (count([&](int i) { return d[i] == D && ix[i] <= mid; }) >= need) b = mid;
             else a = mid + 1;
         }
         I = a;
@@ -159,6 +177,7 @@ __device__ int nn_select(uint32_t* __restrict__ bd, int32_t* __restrict__ bi, in
     int base = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
+        if (i >= ns) break;
         const bool keep = d[i] < D || (d[i] == D && ix[i] <= I);
         const uint64_t b = __builtin_amdgcn_ballot_w64(keep);
         const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -172,10 +191,9 @@ __device__ int nn_select(uint32_t* __restrict__ bd, int32_t* __restrict__ bi, in
 }
 
 template <int KMAX>
-__global__ __launch_bounds__(64 * kNnWaves) void k_knn(const float* __restrict__ X, const float* __restrict__ Y,
-                                                       const float* __restrict__ Z, const uint32_t* __restrict__ fin_idx,
-                                                       int64_t nf, NGrid g, const int32_t* __restrict__ cbeg,
-                                                       const int32_t* __restrict__ cend,
+__global__ __launch_bounds__(64 * kNnWaves) void k_knn(const float* __restrict__ SX, const float* __restrict__ SY,
+                                                       const float* __restrict__ SZ, int64_t nf, NGrid g,
+                                                       const int32_t* __restrict__ cstart,
                                                        const uint32_t* __restrict__ sorted_idx, int k, int kk,
                                                        int32_t* __restrict__ nn, int32_t* __restrict__ nn_cnt) {
     __shared__ uint32_t s_d[kNnWaves][kNnCap];
@@ -186,8 +204,8 @@ __global__ __launch_bounds__(64 * kNnWaves) void k_knn(const float* __restrict__
     int32_t* bi = s_i[w];
     const int rmax = max(g.dim[0], max(g.dim[1], g.dim[2]));
     for (int64_t qi = (int64_t)blockIdx.x * kNnWaves + w; qi < nf; qi += (int64_t)gridDim.x * kNnWaves) {
-        const int q = (int)fin_idx[qi];
-        const float qx = X[q], qy = Y[q], qz = Z[q];
+        const int q = (int)sorted_idx[qi];  // queries in cell order: a block's queries are close
+        const float qx = SX[qi], qy = SY[qi], qz = SZ[qi];
         const int cx = cell_of(g, qx, 0), cy = cell_of(g, qy, 1), cz = cell_of(g, qz, 2);
         int fill = 0;
         // rings 1, 2, 4, ...: an isolated point (few neighbours near it) reaches its k-th neighbour
@@ -197,33 +215,41 @@ __global__ __launch_bounds__(64 * kNnWaves) void k_knn(const float* __restrict__
             const int ax0 = max(cx - r, 0), ax1 = min(cx + r, g.dim[0] - 1);
             const int ay0 = max(cy - r, 0), ay1 = min(cy + r, g.dim[1] - 1);
             const int az0 = max(cz - r, 0), az1 = min(cz + r, g.dim[2] - 1);
-            for (int c = az0; c <= az1; ++c)
-                for (int b = ay0; b <= ay1; ++b) {
+            // cells (ax0..ax1, b, c) are consecutive keys, so each (b, c) row of the ring is one
+            // contiguous range of the cell-sorted points: its bounds for up to 64 rows are loaded
+            // at once (one lane per row), then the rows are streamed in order
+            const int nb = ay1 - ay0 + 1, nrows = nb * (az1 - az0 + 1);
+            for (int r0 = 0; r0 < nrows; r0 += 64) {
+                int rb = 0, re = 0;
+                if (r0 + lane < nrows) {
+                    const int b = ay0 + (r0 + lane) % nb, c = az0 + (r0 + lane) / nb;
                     const int64_t row = (int64_t)g.dim[0] * ((int64_t)b + (int64_t)g.dim[1] * c);
-                    for (int a = ax0; a <= ax1; ++a) {
-                        const int32_t beg = __builtin_amdgcn_readfirstlane(cbeg[row + a]);
-                        if (beg < 0) continue;
-                        const int32_t cnt = __builtin_amdgcn_readfirstlane(cend[row + a]) - beg;
-                        for (int t0 = 0; t0 < cnt; t0 += 64) {
-                            if (fill + 64 > kNnCap) fill = nn_select(bd, bi, fill, kk, lane);
-                            const int t = t0 + lane;
-                            if (t < cnt) {
-                                const int j = (int)sorted_idx[beg + t];
-                                const float dx = qx - X[j], dy = qy - Y[j], dz = qz - Z[j];
-                                const float d2 = (dx * dx + dy * dy) + dz * dz;  // FLANN L2_Simple
-                                bd[fill + lane] = __float_as_uint(d2);
-                                bi[fill + lane] = j;
-                            }
-                            fill += min(64, cnt - t0);
+                    rb = cstart[row + ax0];
+                    re = cstart[row + ax1 + 1];
+                }
+                const int nr = min(64, nrows - r0);
+                for (int ri = 0; ri < nr; ++ri) {
+                    const int beg = __builtin_amdgcn_readlane(rb, ri);
+                    const int cnt = __builtin_amdgcn_readlane(re, ri) - beg;
+                    for (int t0 = 0; t0 < cnt; t0 += 64) {
+                        if (fill + 64 > kNnCap) fill = nn_select(bd, bi, fill, kk, lane);
+                        const int t = beg + t0 + lane;
+                        if (t0 + lane < cnt) {
+                            const float dx = qx - SX[t], dy = qy - SY[t], dz = qz - SZ[t];
+                            const float d2 = (dx * dx + dy * dy) + dz * dz;  // FLANN L2_Simple
+                            bd[fill + lane] = __float_as_uint(d2);
+                            bi[fill + lane] = (int32_t)sorted_idx[t];
                         }
+                        fill += min(64, cnt - t0);
                     }
                 }
+            }
             const bool all = r >= rmax;
             if (fill < kk && !all) continue;
             fill = nn_select(bd, bi, fill, kk, lane);
             // the k-th distance (max of the kept) against the nearest possible outside point
-            float dk = 0.0f;
-            for (int s = lane; s < fill; s += 64) dk = fmaxf(dk, __uint_as_float(bd[s]));
+            float dk = 0.0f;  // fill <= kk <= 64: one slot per lane
+            if (lane < fill) dk = __uint_as_float(bd[lane]);
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) dk = fmaxf(dk, __shfl_xor(dk, d, 64));
             const float lim = (float)r * g.h - g.margin;
@@ -416,19 +442,28 @@ static int normals_impl(pitt_ctx* ctx, const float* x, const float* y, const flo
             if (rc != PITT_OK) return rc;
         }
         const int64_t cells = (int64_t)g.dim[0] * g.dim[1] * g.dim[2];
-        int32_t* cbeg = (int32_t*)ctx->buf("nrm_cbeg", (size_t)cells * 4);
-        int32_t* cend = (int32_t*)ctx->buf("nrm_cend", (size_t)cells * 4);
-        if (!cbeg || !cend) return ctx->fail(PITT_E_NOMEM, "normals cell table");
-        hipLaunchKernelGGL(k_fill_i32, dim3(std::min<int64_t>((cells + 255) / 256, 8192)), dim3(256), 0, s, cbeg, cells, -1);
-        hipLaunchKernelGGL(k_cell_ranges, dim3(grid_for_tiles(ctiles(nf))), dim3(kBlock), 0, s, skey, nf, cbeg, cend);
+        int32_t* cstart = (int32_t*)ctx->buf("nrm_cstart", (size_t)(cells + 1) * 4);
+        float* sxyz = (float*)ctx->buf("nrm_sxyz", (size_t)nf * 12);
+        if (!cstart || !sxyz) return ctx->fail(PITT_E_NOMEM, "normals cell table");
+        int32_t* ccnt = (int32_t*)ctx->buf("nrm_ccnt", (size_t)(cells + 1) * 4);
+        if (!ccnt) return ctx->fail(PITT_E_NOMEM, "normals cell counts");
+        PITT_HIP_TRY(hipMemsetAsync(ccnt, 0, (size_t)(cells + 1) * 4, s));
+        hipLaunchKernelGGL(k_cell_count, dim3(grid_for_tiles(ctiles(nf))), dim3(kBlock), 0, s, skey, nf, ccnt);
+        size_t scan_bytes = 0;
+        PITT_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, ccnt, cstart, (int)(cells + 1), s));
+        void* scan_tmp = ctx->buf("nrm_scan_tmp", std::max<size_t>(scan_bytes, 16));
+        if (!scan_tmp) return ctx->fail(PITT_E_NOMEM, "normals scan scratch");
+        PITT_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, cstart, (int)(cells + 1), s));
+        hipLaunchKernelGGL(k_gather_sorted, dim3(grid_for_tiles(ctiles(nf))), dim3(kBlock), 0, s, x, y, z, sval, nf,
+                           sxyz, sxyz + nf, sxyz + 2 * nf);
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
         // the finite points in input order are the queries: sval holds them sorted by cell, which
         // keeps a block's queries spatially close
         rec = ctx->prof_begin("k_knn", (double)nf * (12.0 + 4.0 * k));
         const int kb = (int)std::min<int64_t>((nf + kNnWaves - 1) / kNnWaves, 65536);
-        hipLaunchKernelGGL(k_knn<kNnMaxK>, dim3(kb), dim3(64 * kNnWaves), 0, s, x, y, z, sval, nf, g, cbeg, cend,
-                           sval, k, kk, nnd, cntd);
+        hipLaunchKernelGGL(k_knn<kNnMaxK>, dim3(kb), dim3(64 * kNnWaves), 0, s, sxyz, sxyz + nf, sxyz + 2 * nf, nf, g,
+                           cstart, sval, k, kk, nnd, cntd);
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
     } else {
