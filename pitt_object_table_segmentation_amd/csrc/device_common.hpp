@@ -12,7 +12,10 @@
 
 namespace pitt {
 
-constexpr int kTile = 2048;        // points per scoring tile (256 threads x 8 points)
+#ifndef PITT_TILE
+#define PITT_TILE 2048
+#endif
+constexpr int kTile = PITT_TILE;   // points per scoring tile (a divisor of PITT_TILE_POINTS)
 constexpr int kBlock = 256;        // threads per tile block
 constexpr int kMaxChunk = 512;     // hypotheses per score launch (LDS counters)
 

@@ -555,9 +555,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     put_coefs<NST>(cl, hyp_coef + (int64_t)cur.f * hcap + h0, Hf, lane);
     for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
     float* gb = group_box + ((int64_t)cur.f * tiles_max + cur.t) * (kTile / kGrp) * 8;
-    if constexpr (!BOX) {  // the tile's 32 group boxes (1 KB, written by the first chunk) into LDS
-        const float4 q = reinterpret_cast<const float4*>(gb)[lane];
-        wbox[w][lane] = q;
+    if constexpr (!BOX) {  // the tile's group boxes (8 floats each, written by the first chunk) into LDS
+        if (lane < (kTile / kGrp) * 2) wbox[w][lane] = reinterpret_cast<const float4*>(gb)[lane];
     }
     const uint32_t gsrc = (uint32_t)(uintptr_t)wbox[w];
     float tb = (lane & 15) < 3 ? __builtin_inff() : -__builtin_inff();  // BOX: this lane's tile-box value
@@ -736,7 +735,7 @@ constexpr int kRDepth = 6;     // raw steps in flight (12 measured the same: the
 constexpr int kRRing = 1024;   // compacted-inlier ring (points, a power of two; 4096 measured the same)
 constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
 
-constexpr int kRMaxTiles = 1024;             // tile list capacity (frames up to 2M points)
+constexpr int kRMaxTiles = (1 << 21) / kTile;  // tile list capacity (frames up to 2M points)
 constexpr int kRStepsPerTile = kTile / kRChunk;
 
 // The nine chain lanes read nine different streams at the same offset in one ds_read_b128: the
