@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, 
                 the data-dependent ones) and its launch time
   clutter       a clutter-scene batch (T = 1001 hypotheses per frame) against the VALU roof
   pcie_fed      frames/s when every batch starts in pinned host memory (H2D copy in the step)
+  config2       one cloud through the single-cloud ABI (host in, host out), median latency
   config5       find_supports + euclidean_clusters on the 1.2M-point fused scene, GPU vs oracle
   cpu_baseline  the oracle (CPU restatement of PCL's path) on the host: frame-parallel on the
                 host's CPU share, and single-core per-frame medians (config 1)
@@ -223,6 +224,25 @@ def pcie_pass(pitt, ctxs, host_batches, dev, params, steps):
     nbytes = sum(t.numel() * 4 for t in (host_batches[0].x, host_batches[0].y, host_batches[0].z))
     return {"frames_per_s": round(frames * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
             "h2d_bytes_per_batch": nbytes, "h2d_GBps": round(nbytes * steps / dt / 1e9, 1), "steps": steps}
+
+
+def config2_pass(pitt, ctx, frame, reps=10):
+    """BASELINE config 2: one 640x480 cloud through the single-cloud ABI (pitt_plane_segment: PointXYZ
+    host array in, inliers and coefficients back on the host -- the service handler's path, PCIe
+    included), median latency of `reps` after 1 warm-up, checked against the oracle."""
+    cloud = np.zeros((len(frame[0]), 4), np.float32)
+    for k in range(3):
+        cloud[:, k] = frame[k]
+    r = ctx.plane_segment(cloud)
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        r = ctx.plane_segment(cloud)
+        ts.append((time.perf_counter() - t) * 1e3)
+    o = oracle().plane_segment(*frame)
+    return {"ms_per_frame": round(float(np.median(ts)), 3), "statistic": f"median of {reps} after 1 warm-up",
+            "inliers": int(len(r.inliers)), "matches_oracle": bool(np.array_equal(r.inliers, o.inliers) and
+                                                                 np.array_equal(r.coefficients, o.coefficients))}
 
 
 def config5_pass(pitt, ctx, threads, reps=5):
@@ -445,6 +465,8 @@ def main():
                                 b.counts, b.capacity) for b in batches]
         line["pcie_fed"] = pcie_pass(pitt, ctxs, host, dev, params, max(3, min(args.steps, 10)))
         log(f"[rank 0] pcie_fed: {line['pcie_fed']}")
+        line["config2"] = config2_pass(pitt, ctx, frames0[0])
+        log(f"[rank 0] config2: {line['config2']}")
         line["config5"] = config5_pass(pitt, ctx, threads)
         log(f"[rank 0] config5: {line['config5']}")
     else:
