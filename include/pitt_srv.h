@@ -8,6 +8,8 @@
  *   pitt_srv_find_supports    <-> findSupports          supports_segmentation_srv.cpp:241
  *   pitt_srv_clusterize       <-> clusterize            cluster_segmentation_srv.cpp:38
  *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
+ *   pitt_srv_call_ransac_plane <-> callRansacPlaneSegmentation  ransac_segmentation.cpp:175-199
+ *   pitt_srv_arbitrate        <-> clustersAcquisition's arbitration  ransac_segmentation.cpp:265-302
  * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
  * Handler calls return 1 when the handler returns true, 0 when false, < 0 on an ABI error.
  */
@@ -50,6 +52,19 @@ int pitt_srv_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int64_t 
                           int32_t* inliers_out /* cap n */, int64_t* n_inliers,
                           float* coefficients_out /* cap 4 */, int32_t* n_coefficients,
                           float centroid_out[3]);
+
+/* callRansacPlaneSegmentation, ransac_segmentation.cpp:175-199: the plane service, accepted (1) only
+ * when its response holds more than 0 inliers (Q2: the min-inliers parameter is read but unused);
+ * 0 leaves *n_inliers = *n_coefficients = 0. */
+int pitt_srv_call_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
+                               int32_t* inliers_out /* cap n */, int64_t* n_inliers,
+                               float* coefficients_out /* cap 4 */, int32_t* n_coefficients);
+
+/* The primitive arbitration of clustersAcquisition, ransac_segmentation.cpp:265-302, over the four
+ * services' inlier counts: returns the reference's tag (0 unknown, 1 plane, 2 sphere, 3 cone,
+ * 4 cylinder; :42-46) or PITT_E_INVALID for a negative count. */
+int pitt_srv_arbitrate(int64_t sphere_inliers, int64_t cylinder_inliers, int64_t cone_inliers,
+                       int64_t plane_inliers);
 
 /* used_out: the response's used_* fields in declaration order:
  * cloud%, plane%, max var, min var, max iter, distance th, normal weight, axis[3], offset[3] */

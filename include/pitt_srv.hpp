@@ -143,6 +143,11 @@ inline std::vector<float> getService3DArrayParameter(const std::vector<float>& i
 
 namespace pitt {
 
+// ransac_segmentation.cpp:37, :42-46
+const float DEFAULT_CONE_OVER_CYLINDER_PRIORITY = 0.9f;
+enum { TXT_UNKNOWN_SHAPE_TAG = 0, TXT_PLANE_SHAPE_TAG = 1, TXT_SPHERE_SHAPE_TAG = 2, TXT_CONE_SHAPE_TAG = 3,
+       TXT_CYLINDER_SHAPE_TAG = 4 };
+
 // ROS parameter server stand-in with roscpp's typed-read rules: a double read as int is rounded
 // (fmod < 0.5 -> floor, else ceil), an int read as double converts, a list reads as vector<float>;
 // any other type mismatch leaves the default (NodeHandle::param).
@@ -194,6 +199,11 @@ public:
     // ransac_segmentation.cpp:175-199: accept iff the response holds > 0 inliers (local minInliers = 0, Q2)
     bool callRansacPlaneSegmentation(const pitt_msgs::PointCloud& cloud, const pitt_msgs::NormalCloud& norm,
                                      pitt_msgs::PrimitiveSegmentation& out);
+    // ransac_segmentation.cpp:265-302: the primitive a cluster is tagged with, from the four services'
+    // inlier counts (0 when a service call failed or returned no inliers): cone first (with the 0.9f
+    // priority over the cylinder, :37, compared in float), then cylinder, plane, sphere; all zero or
+    // no rule -> unknown.  Tags as ransac_segmentation.cpp:42-46.
+    static int arbitratePrimitive(size_t sphereInl, size_t cylinderInl, size_t coneInl, size_t planeInl);
     // obj_segmentation.cpp:143-207 + :261-312: supports (request fields from params, -1 = default),
     // then clusters per support; one ClustersOutput per support with at least one cluster.
     std::vector<pitt_msgs::ClustersOutput> segmentObjects(const pitt_msgs::PointCloud& world_cloud,

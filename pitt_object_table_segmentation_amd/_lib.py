@@ -189,6 +189,8 @@ SIGNATURES.update({
     "pitt_srv_param_set_list": (_i32, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i32]),
     "pitt_srv_param_erase": (_i32, [_vp, ctypes.c_char_p]),
     "pitt_srv_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_srv_call_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p]),
+    "pitt_srv_arbitrate": (_i32, [_i64, _i64, _i64, _i64]),
     "pitt_srv_find_supports": (_i32, [_vp, _f32p, _i64, _i64, ctypes.POINTER(SrvSupportRequest), _i32p, _f32p]),
     "pitt_srv_support_get": (_i32, [_vp, _i32, _i32p, _f32p, _i64p, _i64p]),
     "pitt_srv_support_cloud": (_i32, [_vp, _i32, _i32, _f32p]),

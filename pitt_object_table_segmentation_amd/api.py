@@ -456,6 +456,25 @@ class Services:
                                                 ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)), "ransac_plane")
         return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
 
+    def call_ransac_plane(self, cloud: np.ndarray, n_normals: Optional[int] = None):
+        """callRansacPlaneSegmentation (ransac_segmentation.cpp:175-199): (accepted, inliers, coefficients)."""
+        c = _cloud16(cloud)
+        n = len(c)
+        inl = np.empty(max(n, 1), np.int32)
+        ni, nc = ctypes.c_int64(), ctypes.c_int32()
+        co = np.zeros(4, np.float32)
+        rc = lib.pitt_srv_call_ransac_plane(self.h, _fp(c), n, n if n_normals is None else n_normals, _ip(inl),
+                                            ctypes.byref(ni), _fp(co), ctypes.byref(nc))
+        return self._rc(rc, "pitt_srv_call_ransac_plane"), inl[:ni.value].copy(), co[:nc.value].copy()
+
+    @staticmethod
+    def arbitrate(sphere: int, cylinder: int, cone: int, plane: int) -> int:
+        """The primitive arbitration of ransac_segmentation.cpp:265-302 (tags :42-46)."""
+        rc = lib.pitt_srv_arbitrate(sphere, cylinder, cone, plane)
+        if rc < 0:
+            raise PittError(rc, "pitt_srv_arbitrate")
+        return rc
+
     def find_supports(self, cloud: np.ndarray, n_normals: Optional[int] = None, **req):
         c = _cloud16(cloud)
         n = c.shape[0]

@@ -220,6 +220,19 @@ bool SegmentationServices::callRansacPlaneSegmentation(const pitt_msgs::PointClo
     return false;
 }
 
+// ransac_segmentation.cpp:265-302.  size_t counts as the reference's; the cone rule compares
+// (float)coneInl against (float)cylinderInl * 0.9f (size_t * float is float arithmetic).
+int SegmentationServices::arbitratePrimitive(size_t sphereInl, size_t cylinderInl, size_t coneInl, size_t planeInl) {
+    if (!planeInl && !sphereInl && !cylinderInl && !coneInl) return TXT_UNKNOWN_SHAPE_TAG;
+    if (coneInl >= planeInl && coneInl >= sphereInl &&
+        (float)coneInl >= (float)cylinderInl * DEFAULT_CONE_OVER_CYLINDER_PRIORITY)
+        return TXT_CONE_SHAPE_TAG;
+    if (cylinderInl >= planeInl && cylinderInl >= coneInl && cylinderInl >= sphereInl) return TXT_CYLINDER_SHAPE_TAG;
+    if (planeInl >= coneInl && planeInl >= sphereInl && planeInl >= cylinderInl) return TXT_PLANE_SHAPE_TAG;
+    if (sphereInl >= planeInl && sphereInl >= coneInl && sphereInl >= cylinderInl) return TXT_SPHERE_SHAPE_TAG;
+    return TXT_UNKNOWN_SHAPE_TAG;
+}
+
 // obj_segmentation.cpp:143-207 (callSupportFilter) and :261-312 (support -> cluster glue)
 std::vector<pitt_msgs::ClustersOutput> SegmentationServices::segmentObjects(const pitt_msgs::PointCloud& world_cloud,
                                                                             const pitt_msgs::NormalCloud& normals) {
@@ -321,6 +334,29 @@ int pitt_srv_ransac_plane(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_
         centroid_out[2] = srv.response.z_centroid;
     }
     return ok ? 1 : 0;
+}
+
+int pitt_srv_call_ransac_plane(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals, int32_t* inliers_out,
+                               int64_t* n_inliers, float* coefficients_out, int32_t* n_coefficients) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_inliers || !n_coefficients) return PITT_E_INVALID;
+    pitt_msgs::NormalCloud nc;
+    nc.n = (size_t)n_normals;
+    pitt_msgs::PrimitiveSegmentation out;
+    const bool ok = s->svc.callRansacPlaneSegmentation(cloud_from(xyz16, n), nc, out);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    *n_inliers = ok ? (int64_t)out.response.inliers.size() : 0;
+    *n_coefficients = ok ? (int32_t)out.response.coefficients.size() : 0;
+    if (ok && inliers_out && !out.response.inliers.empty())
+        std::memcpy(inliers_out, out.response.inliers.data(), out.response.inliers.size() * 4);
+    if (ok && coefficients_out && !out.response.coefficients.empty())
+        std::memcpy(coefficients_out, out.response.coefficients.data(), out.response.coefficients.size() * 4);
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_arbitrate(int64_t sphere_inliers, int64_t cylinder_inliers, int64_t cone_inliers, int64_t plane_inliers) {
+    if (sphere_inliers < 0 || cylinder_inliers < 0 || cone_inliers < 0 || plane_inliers < 0) return PITT_E_INVALID;
+    return pitt::SegmentationServices::arbitratePrimitive((size_t)sphere_inliers, (size_t)cylinder_inliers,
+                                                          (size_t)cone_inliers, (size_t)plane_inliers);
 }
 
 int pitt_srv_find_supports(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals,

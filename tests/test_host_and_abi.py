@@ -150,3 +150,34 @@ def test_ros_adapters_use_only_declared_abi():
              "cluster_segmentation_node.cpp": "cluster_Segmentation_srv"}
     for f, name in names.items():
         assert f'advertiseService("{name}"' in open(os.path.join(root, "adapters", "ros", f)).read(), f
+
+
+def test_primitive_arbitration():
+    """ransac_segmentation.cpp:265-302 (host logic behind pitt_srv_arbitrate): cone first with its 0.9f
+    priority over the cylinder (float compare), then cylinder, plane, sphere; tags :42-46."""
+    import numpy as np
+    from pitt_object_table_segmentation_amd import Services
+
+    def ref(sp, cy, co, pl):
+        if not (pl or sp or cy or co):
+            return 0
+        if co >= pl and co >= sp and np.float32(co) >= np.float32(cy) * np.float32(0.9):
+            return 3
+        if cy >= pl and cy >= co and cy >= sp:
+            return 4
+        if pl >= co and pl >= sp and pl >= cy:
+            return 1
+        if sp >= pl and sp >= co and sp >= cy:
+            return 2
+        return 0
+
+    a = Services.arbitrate
+    assert a(0, 0, 0, 0) == 0 and a(0, 0, 0, 5) == 1 and a(7, 0, 0, 5) == 2
+    assert a(10, 100, 90, 50) == 3 and a(10, 100, 89, 50) == 4  # 90 >= 100 * 0.9f, 89 is not
+    assert a(10, 10, 10, 10) == 3  # a four-way tie goes to the cone
+    assert a(0, 10, 9, 10) == 4 and a(11, 10, 9, 10) == 2 and a(0, 9, 9, 9) == 3
+    rng = np.random.default_rng(0)
+    for c in rng.integers(0, 40, (3000, 4)):
+        assert a(*map(int, c)) == ref(*map(int, c)), c
+    with pytest.raises(pitt.PittError):
+        a(-1, 0, 0, 0)

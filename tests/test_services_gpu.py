@@ -128,3 +128,18 @@ def test_segment_objects_glue(srv):
     for o, e in zip(outs, exp):
         assert [list(c["inliers"]) for c in o] == [list(c["inliers"]) for c in e]
         assert all(np.array_equal(c["centroid"], d["centroid"]) for c, d in zip(o, e))
+
+
+def test_call_ransac_plane_client(srv):
+    """callRansacPlaneSegmentation (ransac_segmentation.cpp:175-199): accepted iff the handler's response
+    holds > 0 inliers (Q2), with the handler's response; a normals-size mismatch gives no model."""
+    xyz = _cloud(1002)
+    ok, inl, coef = srv.call_ransac_plane(xyz)
+    h_ok, h_inl, h_coef, _ = srv.ransac_plane(xyz)
+    assert ok and h_ok and np.array_equal(inl, h_inl) and np.array_equal(coef, h_coef)
+    ok, inl, coef = srv.call_ransac_plane(xyz, n_normals=len(xyz) - 1)
+    assert not ok and len(inl) == 0 and len(coef) == 0
+    # the only inlier is point 0, which the handler drops (Q1): the client rejects the empty response
+    two = np.array([[0, 0, 0], [1, 1, 1]], np.float32)
+    ok, inl, _ = srv.call_ransac_plane(two)
+    assert not ok and len(inl) == 0
