@@ -73,8 +73,8 @@ bool deepFiltering(pitt_msgs::DeepFilter::Request& req, pitt_msgs::DeepFilter::R
             int64_t nv = 0;
             int32_t flags = 0;
             float* v = outp;
-            if (pitt_voxel_grid(ctx, x, y, z, n, (float)g_leaf, (float)g_leaf, (float)g_leaf, v, v + n, v + 2 * n,
-                                &nv, &flags) != PITT_OK)
+            if (pitt_voxel_grid(ctx, x, y, z, n, (float)g_leaf, (float)g_leaf, (float)g_leaf, PITT_VOXEL_ORDER_PCL, v,
+                                v + n, v + 2 * n, &nv, &flags) != PITT_OK)
                 return false;
             hipMemcpy(x, v, (size_t)nv * 4, hipMemcpyDeviceToDevice);
             hipMemcpy(x + nv, v + n, (size_t)nv * 4, hipMemcpyDeviceToDevice);

@@ -238,13 +238,22 @@ int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes,
  * (i + j div_x + k div_x div_y); its value is the float mean of the leaf's finite points (sum, then
  * times 1/n).  Non-finite points never count.  When the grid would overflow int32 PCL warns and
  * returns the input unchanged: then out = in, *n_out = n and *flags |= PITT_VOXEL_OVERFLOW_COPY.
- * The points inside a leaf are summed in ascending point order (PCL's std::sort leaves them in
- * libstdc++'s introsort order), so a centroid may differ from PCL's in its last bits.
+ * order: PITT_VOXEL_ORDER_PCL sums each leaf's points in the order PCL's (unstable) std::sort leaves
+ * them -- libstdc++'s introsort permutation, reproduced on the device (assumption A10) -- so the
+ * centroids are PCL's bit for bit; PITT_VOXEL_ORDER_STABLE sums them in ascending point order (faster;
+ * a centroid may then differ from PCL's in its last bits).
  * Device SoA in; device SoA out of capacity n.  Leaf sizes must be > 0. */
 #define PITT_VOXEL_OVERFLOW_COPY 1
+#define PITT_VOXEL_ORDER_PCL 0
+#define PITT_VOXEL_ORDER_STABLE 1
 int pitt_voxel_grid(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
-                    float leaf_x, float leaf_y, float leaf_z, float* out_x, float* out_y, float* out_z,
-                    int64_t* n_out, int32_t* flags);
+                    float leaf_x, float leaf_y, float leaf_z, int32_t order, float* out_x, float* out_y,
+                    float* out_z, int64_t* n_out, int32_t* flags);
+
+/* The permutation libstdc++'s std::sort gives (key, val) pairs compared by key only, in place on
+ * device arrays (the sort inside pitt_voxel_grid's PCL order; exported for its tests).  depth_limit < 0
+ * is the library's 2 floor(log2 n); a smaller one reaches its heapsort fallback. */
+int pitt_sort_pairs(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit);
 
 /* pcl::NormalEstimation<PointXYZ, Normal> with a search::KdTree and setKSearch(k), as called by
  * PCManager::estimateNormal, src/point_cloud_library/pc_manager.cpp:68-78 (k = 50, :18; called at

@@ -970,3 +970,119 @@ int orc_normal_estimation(const float* x, const float* y, const float* z, int64_
 }
 
 }  // extern "C"
+
+// The permutation std::sort gives (key, value) pairs compared by key (VoxelGrid's index_vector), twice:
+// orc_std_sort_pairs runs this image's libstdc++ std::sort; orc_introsort_pairs restates libstdc++'s
+// algorithm (introsort loop with median-of-3 to first and the unguarded Hoare partition, heapsort
+// when the depth limit runs out, final insertion sort) with a settable depth limit (< 0: the
+// library's 2 floor(log2 n)), so the tests can check the restatement against the library and the
+// device emulation against the restatement -- including the heapsort fallback.
+namespace {
+struct KV {
+    uint32_t k, v;
+};
+inline bool kv_less(const KV& a, const KV& b) { return a.k < b.k; }
+
+void is_push_heap(KV* a, long hole, long top, KV value) {
+    long parent = (hole - 1) / 2;
+    while (hole > top && kv_less(a[parent], value)) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = value;
+}
+void is_adjust_heap(KV* a, long hole, long len, KV value) {
+    const long top = hole;
+    long second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (kv_less(a[second], a[second - 1])) second--;
+        a[hole] = a[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        a[hole] = a[second - 1];
+        hole = second - 1;
+    }
+    is_push_heap(a, hole, top, value);
+}
+void is_heap_sort(KV* a, long len) {
+    if (len >= 2)
+        for (long parent = (len - 2) / 2;; --parent) {
+            is_adjust_heap(a, parent, len, a[parent]);
+            if (parent == 0) break;
+        }
+    for (long last = len; last > 1;) {
+        --last;
+        KV value = a[last];
+        a[last] = a[0];
+        is_adjust_heap(a, 0, last, value);
+    }
+}
+void is_loop(KV* a, long first, long last, int depth) {
+    while (last - first > 16) {
+        if (depth == 0) {
+            is_heap_sort(a + first, last - first);
+            return;
+        }
+        --depth;
+        const long mid = first + (last - first) / 2, x = first + 1, y = mid, z = last - 1;
+        long m;
+        if (kv_less(a[x], a[y])) m = kv_less(a[y], a[z]) ? y : kv_less(a[x], a[z]) ? z : x;
+        else m = kv_less(a[x], a[z]) ? x : kv_less(a[y], a[z]) ? z : y;
+        std::swap(a[first], a[m]);
+        long lo = first + 1, hi = last;
+        while (true) {
+            while (kv_less(a[lo], a[first])) ++lo;
+            --hi;
+            while (kv_less(a[first], a[hi])) --hi;
+            if (!(lo < hi)) break;
+            std::swap(a[lo], a[hi]);
+            ++lo;
+        }
+        is_loop(a, lo, last, depth);
+        last = lo;
+    }
+}
+void is_insertion(KV* a, long n) {  // __insertion_sort: stable for equal keys
+    for (long i = 1; i < n; ++i) {
+        KV v = a[i];
+        long j = i;
+        while (j > 0 && kv_less(v, a[j - 1])) {
+            a[j] = a[j - 1];
+            --j;
+        }
+        a[j] = v;
+    }
+}
+}  // namespace
+
+extern "C" {
+void orc_std_sort_pairs(uint32_t* key, uint32_t* val, int64_t n) {
+    std::vector<KV> a((size_t)n);
+    for (int64_t i = 0; i < n; ++i) a[(size_t)i] = {key[i], val[i]};
+    std::sort(a.begin(), a.end(), kv_less);
+    for (int64_t i = 0; i < n; ++i) key[i] = a[(size_t)i].k, val[i] = a[(size_t)i].v;
+}
+
+void orc_partial_sort_pairs(uint32_t* key, uint32_t* val, int64_t n) {  // the library's heapsort path
+    std::vector<KV> a((size_t)n);
+    for (int64_t i = 0; i < n; ++i) a[(size_t)i] = {key[i], val[i]};
+    std::partial_sort(a.begin(), a.end(), a.end(), kv_less);
+    for (int64_t i = 0; i < n; ++i) key[i] = a[(size_t)i].k, val[i] = a[(size_t)i].v;
+}
+
+void orc_introsort_pairs(uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit) {
+    std::vector<KV> a((size_t)n);
+    for (int64_t i = 0; i < n; ++i) a[(size_t)i] = {key[i], val[i]};
+    if (n > 1) {
+        int lg = 0;
+        while (((int64_t)2 << lg) <= n) ++lg;
+        is_loop(a.data(), 0, (long)n, depth_limit >= 0 ? depth_limit : 2 * lg);
+        is_insertion(a.data(), (long)n);
+    }
+    for (int64_t i = 0; i < n; ++i) key[i] = a[(size_t)i].k, val[i] = a[(size_t)i].v;
+}
+}  // extern "C"

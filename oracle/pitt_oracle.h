@@ -127,6 +127,10 @@ int     orc_voxel_grid(const float* x, const float* y, const float* z, int64_t n
 int     orc_normal_estimation(const float* x, const float* y, const float* z, int64_t n, int32_t k,
                               const float vp[3], float* nx, float* ny, float* nz, float* curv,
                               int32_t* nn_out, int32_t* nn_cnt);
+// std::sort of (key, value) pairs by key: the library's, and a restatement with a settable depth limit
+void    orc_std_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
+void    orc_partial_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
+void    orc_introsort_pairs(uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit);
 
 #ifdef __cplusplus
 }

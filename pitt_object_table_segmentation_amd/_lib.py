@@ -23,6 +23,7 @@ PITT_E_NODEVICE = -5
 PITT_TILE_POINTS = 2048
 PITT_FLAG_K_NEAR_INTEGER = 1
 PITT_VOXEL_OVERFLOW_COPY = 1
+PITT_VOXEL_ORDER_PCL, PITT_VOXEL_ORDER_STABLE = 0, 1
 
 REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
 DIV_EIGEN32, DIV_TRUE = 0, 1
@@ -147,8 +148,9 @@ SIGNATURES = {
     "pitt_transform_cloud": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp]),
     "pitt_unpack_pointcloud2": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
     "pitt_normal_estimation": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32p, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
-                               _vp, _i64p, _i32p]),
+    "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32, _vp,
+                               _vp, _vp, _i64p, _i32p]),
+    "pitt_sort_pairs": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
     "pitt_find_supports": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.POINTER(SupportParams),
                                   ctypes.POINTER(SupportList)]),

@@ -324,16 +324,17 @@ class Context:
                                                 z.data_ptr()), "pitt_unpack_pointcloud2")
         return x[:n], y[:n], z[:n]
 
-    def voxel_grid(self, x, y, z, leaf=(0.01, 0.01, 0.01)):
+    def voxel_grid(self, x, y, z, leaf=(0.01, 0.01, 0.01), order: int = L.PITT_VOXEL_ORDER_PCL):
         """VoxelGrid<PointXYZ> downsampling (pc_manager.cpp:55-67) on device tensors: returns device
-        (x, y, z) of the leaf centroids in ascending leaf index, and the flags (PITT_VOXEL_OVERFLOW_COPY)."""
+        (x, y, z) of the leaf centroids in ascending leaf index, and the flags (PITT_VOXEL_OVERFLOW_COPY).
+        order: PCL's std::sort order inside a leaf (default, bit-exact) or stable (faster)."""
         import torch
         n = x.numel()
         ox, oy, oz = (torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(3))
         m, fl = ctypes.c_int64(), ctypes.c_int32()
         self._check(lib.pitt_voxel_grid(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, float(leaf[0]),
-                                        float(leaf[1]), float(leaf[2]), ox.data_ptr(), oy.data_ptr(), oz.data_ptr(),
-                                        ctypes.byref(m), ctypes.byref(fl)), "pitt_voxel_grid")
+                                        float(leaf[1]), float(leaf[2]), int(order), ox.data_ptr(), oy.data_ptr(),
+                                        oz.data_ptr(), ctypes.byref(m), ctypes.byref(fl)), "pitt_voxel_grid")
         k = m.value
         return (ox[:k], oy[:k], oz[:k]), fl.value
 
@@ -351,6 +352,11 @@ class Context:
                                                None if cnt is None else cnt.data_ptr()), "pitt_normal_estimation")
         res = tuple(o[:n] for o in out)
         return res + ((nn[:n], cnt[:n]),) if neighbours else res
+
+    def sort_pairs(self, key, val, depth_limit: int = -1):
+        """std::sort's permutation of (key, val) uint32 pairs by key, in place on device int32 tensors."""
+        self._check(lib.pitt_sort_pairs(self.h, key.data_ptr(), val.data_ptr(), key.numel(), int(depth_limit)),
+                    "pitt_sort_pairs")
 
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:

@@ -21,11 +21,11 @@
 //   k_vox_centroid -> one thread per voxel: the run's points summed in run order, times 1 / n
 //
 // Run order: PCL's std::sort is not stable, so its order of the points inside one voxel is
-// libstdc++'s introsort permutation; the device sort is stable (ascending point index inside a
-// voxel).  The voxel set, their order and every count are PCL's; a centroid equals PCL's whenever
-// the voxel's float sum does not depend on the order (always for 1-2 points), otherwise it is
-// within the reordering bound of a float sum (tests/test_voxel_gpu.py).  Against the oracle's
-// stable mode it is bit-exact.
+// libstdc++'s introsort permutation, and the float centroid depends on it in its last bits.
+// PITT_VOXEL_ORDER_PCL reproduces that permutation (introsort.hip: the introsort partitions on the
+// device, then the stable sort) -- bit-exact against PCL's order under A10; PITT_VOXEL_ORDER_STABLE
+// sorts stably (ascending point index inside a voxel, faster), within the float reordering bound of
+// PCL's centroids.  The voxel set, their order and every count are PCL's in both modes.
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
 
@@ -208,8 +208,10 @@ __global__ __launch_bounds__(kBlock) void k_vox_centroid(const float* __restrict
     }
 }
 
+int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int depth_limit);
+
 static int voxel_impl(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, float lx, float ly,
-                      float lz, float* ox, float* oy, float* oz, int64_t* n_out, int32_t* flags) {
+                      float lz, int32_t order, float* ox, float* oy, float* oz, int64_t* n_out, int32_t* flags) {
     hipStream_t s = ctx->stream;
     *n_out = 0;
     if (flags) *flags = 0;
@@ -258,6 +260,14 @@ static int voxel_impl(pitt_ctx* ctx, const float* x, const float* y, const float
                        WriteVoxKey{x, y, z, prm, key, val}, n, to);
     ctx->prof_end(rec);
     PITT_HIP_TRY(hipGetLastError());
+    // PCL order: the partitions of libstdc++'s introsort first (introsort.hip); the stable sort then
+    // gives std::sort's permutation.  Stable order: the sort alone.
+    if (order == PITT_VOXEL_ORDER_PCL) {
+        rec = ctx->prof_begin("vox_introsort", (double)nf * 8.0);
+        const int irc = introsort_partitions(ctx, key, val, nf, -1);
+        ctx->prof_end(rec);
+        if (irc != PITT_OK) return irc;
+    }
     // stable LSD radix sort of the keys over the bits the grid uses
     int end_bit = 1;
     while (end_bit < 32 && ((int64_t)1 << end_bit) < P.cells) ++end_bit;
@@ -302,13 +312,38 @@ static int voxel_impl(pitt_ctx* ctx, const float* x, const float* y, const float
 }  // namespace pitt
 
 extern "C" int pitt_voxel_grid(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
-                               float leaf_x, float leaf_y, float leaf_z, float* out_x, float* out_y, float* out_z,
-                               int64_t* n_out, int32_t* flags) {
+                               float leaf_x, float leaf_y, float leaf_z, int32_t order, float* out_x, float* out_y,
+                               float* out_z, int64_t* n_out, int32_t* flags) {
     if (!ctx) return PITT_E_INVALID;
+    if (order != PITT_VOXEL_ORDER_PCL && order != PITT_VOXEL_ORDER_STABLE) return ctx->fail(PITT_E_INVALID, "order");
     if (!n_out || n < 0 || (n > 0 && (!x || !y || !z || !out_x || !out_y || !out_z)))
         return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (!(leaf_x > 0.0f) || !(leaf_y > 0.0f) || !(leaf_z > 0.0f)) return ctx->fail(PITT_E_INVALID, "leaf size");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::voxel_impl(ctx, x, y, z, n, leaf_x, leaf_y, leaf_z, out_x, out_y, out_z, n_out, flags);
+    return pitt::voxel_impl(ctx, x, y, z, n, leaf_x, leaf_y, leaf_z, order, out_x, out_y, out_z, n_out, flags);
+}
+
+extern "C" int pitt_sort_pairs(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit) {
+    if (!ctx) return PITT_E_INVALID;
+    if (n < 0 || (n > 0 && (!key || !val))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 pairs");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    if (n < 2) return PITT_OK;
+    hipStream_t s = ctx->stream;
+    int rc = pitt::introsort_partitions(ctx, key, val, n, depth_limit);
+    if (rc != PITT_OK) return rc;
+    uint32_t* k2 = (uint32_t*)ctx->buf("sp_k2", (size_t)n * 4);
+    uint32_t* v2 = (uint32_t*)ctx->buf("sp_v2", (size_t)n * 4);
+    if (!k2 || !v2) return ctx->fail(PITT_E_NOMEM, "sort scratch");
+    hipcub::DoubleBuffer<uint32_t> kb(key, k2), vb(val, v2);
+    size_t tmp_bytes = 0;
+    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (int)n, 0, 32, s));
+    void* tmp = ctx->buf("sp_tmp", std::max<size_t>(tmp_bytes, 16));
+    if (!tmp) return ctx->fail(PITT_E_NOMEM, "sort scratch");
+    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (int)n, 0, 32, s));
+    if (kb.Current() != key) PITT_HIP_TRY(hipMemcpyAsync(key, kb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    if (vb.Current() != val) PITT_HIP_TRY(hipMemcpyAsync(val, vb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    return PITT_OK;
 }

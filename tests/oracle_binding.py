@@ -260,3 +260,19 @@ def normal_estimation(x, y, z, k=50, viewpoint=(0.0, 0.0, 0.0), neighbours=False
                             None if nn is None else _ip(nn), _ip(cnt))
     out = (o[:3, :n].T.copy(), o[3, :n].copy())
     return out + ((nn[:n], cnt[:n]),) if neighbours else out
+
+
+O.orc_std_sort_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+O.orc_introsort_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+
+
+def sort_pairs(keys, vals, depth_limit=None):
+    """std::sort of (key, value) pairs by key (this image's libstdc++), or, with depth_limit, the
+    oracle's restatement of its introsort (-1: the library's limit)."""
+    k = np.ascontiguousarray(keys, np.uint32).copy()
+    v = np.ascontiguousarray(vals, np.uint32).copy()
+    if depth_limit is None:
+        O.orc_std_sort_pairs(k.ctypes.data, v.ctypes.data, len(k))
+    else:
+        O.orc_introsort_pairs(k.ctypes.data, v.ctypes.data, len(k), depth_limit)
+    return k, v

@@ -122,8 +122,9 @@ def test_preprocessing_entry_points_reject_null_context():
     assert lib.pitt_transform_cloud(None, None, None, None, 0, m, 1, None, None, None) == L.PITT_E_INVALID
     assert lib.pitt_unpack_pointcloud2(None, None, 0, 0, 0, 16, 0, 0, 4, 8, None, None, None) == L.PITT_E_INVALID
     n, fl = ctypes.c_int64(), ctypes.c_int32()
-    assert lib.pitt_voxel_grid(None, None, None, None, 0, 0.01, 0.01, 0.01, None, None, None, ctypes.byref(n),
+    assert lib.pitt_voxel_grid(None, None, None, None, 0, 0.01, 0.01, 0.01, 0, None, None, None, ctypes.byref(n),
                                ctypes.byref(fl)) == L.PITT_E_INVALID
+    assert lib.pitt_sort_pairs(None, None, None, 0, -1) == L.PITT_E_INVALID
     assert lib.pitt_normal_estimation(None, None, None, None, 0, 50, None, None, None, None, None, None,
                                       None) == L.PITT_E_INVALID
 

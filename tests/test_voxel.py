@@ -2,9 +2,10 @@
 
 CPU: the oracle's restatement of PCL 1.7 applyFilter against analytic cases and an independent numpy
 restatement of the leaf indices (integer work, exact) and of the stable-order centroids.
-GPU: pitt_voxel_grid against the oracle -- bit-exact against its stable-order mode; against PCL's
-std::sort order the leaf set, order and counts are equal and each centroid is within the float
-reordering bound of its leaf's sum (the one float result that depends on the order).
+GPU: pitt_voxel_grid against the oracle -- in PCL order (the default; libstdc++'s introsort permutation
+reproduced on the device) bit-exact against the oracle's std::sort; in stable order bit-exact against
+the stable restatement and within the float reordering bound of PCL's centroids.  pitt_sort_pairs
+against std::sort and, with a forced depth limit, against the oracle's restatement (heapsort path).
 """
 import numpy as np
 import pytest
@@ -83,6 +84,23 @@ def test_oracle_voxel_overflow_copies_input():
     assert np.array_equal(out[:2], pts[:2]) and np.isinf(out[2, 0])
 
 
+@pytest.mark.parametrize("n,keys", [(17, 3), (5000, 50), (300000, 90000), (50000, 2)])
+def test_oracle_introsort_restatement_is_the_library(n, keys):
+    """The oracle's introsort restatement (used to check the device's heapsort path) equals this
+    image's std::sort, and at depth 0 its heapsort equals std::partial_sort."""
+    import ctypes
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, keys, n).astype(np.uint32)
+    v = np.arange(n, dtype=np.uint32)
+    a, b = orc.sort_pairs(k, v), orc.sort_pairs(k, v, -1)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    orc.O.orc_partial_sort_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    hk, hv = k.copy(), v.copy()
+    orc.O.orc_partial_sort_pairs(hk.ctypes.data, hv.ctypes.data, n)
+    c = orc.sort_pairs(k, v, 0)
+    assert np.array_equal(hk, c[0]) and np.array_equal(hv, c[1])
+
+
 def test_oracle_voxel_empty_and_all_nan():
     out, flag = orc.voxel_grid(np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.float32))
     assert flag == 0 and out.shape == (0, 3)
@@ -105,24 +123,27 @@ def test_oracle_voxel_vs_numpy(scene, seed):
 
 
 # ---- HIP path --------------------------------------------------------------------------------------
-def _gpu_voxel(ctx, x, y, z, leaf=(0.01, 0.01, 0.01)):
+def _gpu_voxel(ctx, x, y, z, leaf=(0.01, 0.01, 0.01), order=0):
     import torch
     t = [torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda() for a in (x, y, z)]
-    (ox, oy, oz), flags = ctx.voxel_grid(*t, leaf=leaf)
+    (ox, oy, oz), flags = ctx.voxel_grid(*t, leaf=leaf, order=order)
     return np.stack([ox.cpu().numpy(), oy.cpu().numpy(), oz.cpu().numpy()], 1), flags
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,seed", [(0, 1000), (1, 1003), (2, 1001)])
 def test_hip_voxel_frames(ctx, scene, seed):
+    """PCL order (default): bit-exact against the oracle's std::sort; stable order: bit-exact against
+    the stable restatement and within the reordering bound of PCL's centroids."""
     x, y, z = frame(scene, seed)
     got, flags = _gpu_voxel(ctx, x, y, z)
-    stable, _ = orc.voxel_grid(x, y, z, sort_mode=orc.SORT_STABLE)
     pcl, _ = orc.voxel_grid(x, y, z)
+    assert flags == 0 and np.array_equal(got, pcl)
+    got_s, _ = _gpu_voxel(ctx, x, y, z, order=1)
+    stable, _ = orc.voxel_grid(x, y, z, sort_mode=orc.SORT_STABLE)
     _, counts, mag = stable_centroids(x, y, z)
-    assert flags == 0
-    assert np.array_equal(got, stable)
-    assert got.shape == pcl.shape and np.all(np.abs(got.astype(np.float64) - pcl) <= reorder_bound(counts, mag))
+    assert np.array_equal(got_s, stable)
+    assert np.all(np.abs(got_s.astype(np.float64) - pcl) <= reorder_bound(counts, mag))
 
 
 @pytest.mark.gpu
@@ -130,8 +151,27 @@ def test_hip_voxel_fused_1p2m(ctx):
     from pitt_object_table_segmentation_amd import api
     x, y, z = api.synth_fused(1000, 4)
     got, _ = _gpu_voxel(ctx, x, y, z)
-    stable, _ = orc.voxel_grid(x, y, z, sort_mode=orc.SORT_STABLE)
-    assert np.array_equal(got, stable)
+    pcl, _ = orc.voxel_grid(x, y, z)
+    assert np.array_equal(got, pcl)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,keys,depth", [(17, 3, -1), (1000, 7, -1), (300000, 90000, -1), (50000, 2, -1),
+                                          (20000, 50, 0), (20000, 50, 2), (5000, 5, 3), (4096, 4096, 1)])
+def test_hip_sort_pairs_is_std_sort(ctx, n, keys, depth):
+    """pitt_sort_pairs reproduces std::sort's permutation of equal keys (the library's own sort at
+    the default depth; the oracle's restatement, validated against the library, with a forced
+    small depth limit that reaches the heapsort fallback)."""
+    import torch
+    rng = np.random.default_rng(n + keys)
+    k = rng.integers(0, keys, n).astype(np.uint32)
+    v = rng.permutation(n).astype(np.uint32)
+    want = orc.sort_pairs(k, v) if depth < 0 else orc.sort_pairs(k, v, depth)
+    tk = torch.from_numpy(k.view(np.int32)).cuda()
+    tv = torch.from_numpy(v.view(np.int32)).cuda()
+    ctx.sort_pairs(tk, tv, depth)
+    assert np.array_equal(tk.cpu().numpy().view(np.uint32), want[0])
+    assert np.array_equal(tv.cpu().numpy().view(np.uint32), want[1])
 
 
 @pytest.mark.gpu
@@ -142,7 +182,7 @@ def test_hip_voxel_edges(ctx):
     p[3, 2] = np.inf
     for leaf in [(0.01, 0.01, 0.01), (0.05, 0.02, 0.013), (1.0, 1.0, 1.0)]:
         got, flags = _gpu_voxel(ctx, *p.T, leaf=leaf)
-        want, _ = orc.voxel_grid(*p.T, leaf=leaf, sort_mode=orc.SORT_STABLE)
+        want, _ = orc.voxel_grid(*p.T, leaf=leaf)
         assert flags == 0 and np.array_equal(got, want), leaf
     # overflow: the input comes back unchanged (non-finite points included)
     big = np.array([[0, 0, 0], [100, 100, 100], [np.nan, 1, 1]], np.float32)

@@ -82,7 +82,7 @@ def main():
         torch.cuda.synchronize()
         vox_ms = (time.perf_counter() - t0) * 1e3 / (vox_reps * len(frames))
         vox = {"ms_per_frame_wall": round(vox_ms, 4), "leaves_last_frame": int(vx.numel()), "kernels": {}}
-        for k in ("k_vox_minmax", "k_vox_keys", "vox_radix_sort", "k_vox_runs", "k_vox_centroid"):
+        for k in ("k_vox_minmax", "k_vox_keys", "vox_introsort", "vox_radix_sort", "k_vox_runs", "k_vox_centroid"):
             launches, ms, algo = ctx.profile_get(k)
             if launches:
                 vox["kernels"][k] = {"avg_us": round(ms / launches * 1e3, 1)}
