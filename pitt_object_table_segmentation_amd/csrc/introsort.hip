@@ -19,7 +19,6 @@
 //           last) (make_heap + sort_heap, one thread).
 // The caller then runs a stable radix sort by key.
 #include <hip/hip_runtime.h>
-#include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -35,7 +34,15 @@ struct ISeg {
     int32_t nL, nR, K, cut, childL, childR, active, pad;
 };
 
+struct ISmall {
+    int32_t f, l, depth, pad;
+};
+
 constexpr int kIsThreshold = 16;  // _S_threshold
+constexpr int kIsSmall = 2048;
+#ifndef PITT_IS_COOP_MAX
+#define PITT_IS_COOP_MAX 64
+#endif    // segments this short finish in one wave, in LDS
 
 __device__ __forceinline__ void is_swap(uint32_t* key, uint32_t* val, int a, int b) {
     const uint32_t ka = key[a], va = val[a];
@@ -45,139 +52,236 @@ __device__ __forceinline__ void is_swap(uint32_t* key, uint32_t* val, int a, int
     val[b] = va;
 }
 
-// pivot: median of (first + 1, mid, last - 1) to first; a segment out of depth goes to the heap list
-__global__ void k_is_pivot(ISeg* __restrict__ segs, int nseg, uint32_t* __restrict__ key, uint32_t* __restrict__ val,
-                           int32_t* __restrict__ heap, int32_t* __restrict__ heap_cnt) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    ISeg g = segs[s];
-    g.K = 0;
-    g.active = 1;
-    if (g.depth == 0) {
-        g.active = 0;
-        heap[atomicAdd(heap_cnt, 1)] = s;
-        segs[s] = g;
-        return;
+// children of <= 16 are final; children of <= kIsSmall go to the one-wave list, larger ones to the next level
+__device__ __forceinline__ int is_child(int f, int l, int d, ISeg* next, int32_t* next_cnt, ISmall* small,
+                                        int32_t* small_cnt) {
+    if (l - f <= kIsThreshold) return -1;
+    if (l - f <= kIsSmall) {
+        small[atomicAdd(small_cnt, 1)] = ISmall{f, l, d, 0};
+        return -1;
     }
-    const int f = g.f, a = f + 1, b = f + (g.l - f) / 2, c = g.l - 1;
-    const uint32_t ka = key[a], kb = key[b], kc = key[c];
-    int m;
-    if (ka < kb) m = (kb < kc) ? b : (ka < kc) ? c : a;
-    else m = (ka < kc) ? a : (kb < kc) ? c : b;
-    is_swap(key, val, f, m);
-    g.pivot = key[f];
-    segs[s] = g;
+    const int id = atomicAdd(next_cnt, 1);
+    ISeg c = {};
+    c.f = f;
+    c.l = l;
+    c.depth = d;
+    next[id] = c;
+    return id;
 }
 
-__global__ void k_is_flags(const int32_t* __restrict__ segid, const ISeg* __restrict__ segs, const uint32_t* __restrict__ key,
-                           int64_t n, int32_t* __restrict__ FL, int32_t* __restrict__ FR) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
-        int fl = 0, fr = 0;
-        if (i < n) {
-            const int s = segid[i];
-            if (s >= 0 && segs[s].active && i != segs[s].f) {
-                const uint32_t p = segs[s].pivot, k = key[i];
-                fl = !(k < p);
-                fr = !(p < k);
+__device__ __forceinline__ int is_load_count(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kIsLvT = 1024;  // threads per block of the level kernel
+constexpr int kIsLvW = kIsLvT / 64;
+
+// Exclusive scan of two flags over a kIsLvT-thread block; ta / tb = the block totals.
+__device__ __forceinline__ void is_block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int ia = a, ib = b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int xa = __shfl_up(ia, off, 64), xb = __shfl_up(ib, off, 64);
+        if (lane >= off) {
+            ia += xa;
+            ib += xb;
+        }
+    }
+    if (lane == 63) {
+        sh[w] = ia;
+        sh[kIsLvW + w] = ib;
+    }
+    __syncthreads();
+    int oa = 0, ob = 0;
+    ta = tb = 0;
+#pragma unroll
+    for (int j = 0; j < kIsLvW; ++j) {
+        const int sa = sh[j], sb = sh[kIsLvW + j];
+        oa += j < w ? sa : 0;
+        ob += j < w ? sb : 0;
+        ta += sa;
+        tb += sb;
+    }
+    __syncthreads();
+    ea = oa + ia - a;
+    eb = ob + ib - b;
+}
+
+// Grid barrier over a monotonically rising arrival counter (zeroed before the launch): barrier j
+// waits for j * gridDim.x arrivals.  The grid is small enough that every block is resident.  Agent-
+// scope release / acquire make the blocks' writes visible across the XCDs' L2s.
+__device__ __forceinline__ void is_grid_sync(uint32_t* bar, uint32_t& target) {
+    __syncthreads();
+    target += gridDim.x;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+}
+
+// All levels of segments longer than kIsSmall in one launch of a resident grid; a level is six grid-wide
+// phases (grid barriers between them):
+//   1 pivot   per segment: median of (first + 1, mid, last - 1) to first; depth 0 -> the heap list;
+//   2 flags   per element: left stop (key >= p) / right stop (key <= p) of its segment, block-local
+//             exclusive ranks over the block's contiguous chunk, block totals;
+//   3 offsets the chunk prefix of the block totals added: global exclusive ranks SL / SR;
+//   4 ranks   per element: posL[first + 1 + k] = the k-th left stop, posR[first + 1 + k] = the k-th
+//             right stop from the end; per segment nL / nR;
+//   5 K       per segment: the swaps __unguarded_partition makes (posL[k] < posR[k] holds on a prefix);
+//   6 swap    per element k < K: swap posL[k] <-> posR[k]; per segment: the cut, the children;
+//   7 segid   per element: its child segment (or -1), then every block reads the next level's count.
+__global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, ISeg* __restrict__ segB,
+                                                   ISeg* __restrict__ heap, ISmall* __restrict__ small,
+                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ segid,
+                                                   uint8_t* __restrict__ F, int32_t* __restrict__ SL,
+                                                   int32_t* __restrict__ SR, int32_t* __restrict__ posL,
+                                                   int32_t* __restrict__ posR, int32_t* __restrict__ bsum,
+                                                   uint32_t* __restrict__ key, uint32_t* __restrict__ val, int64_t n,
+                                                   int64_t chunk, int levels, uint32_t* __restrict__ bar) {
+    __shared__ int sh[2 * kIsLvW];
+    uint32_t target = 0;
+    const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+    const int64_t gt = (int64_t)b * kIsLvT + tid, gstride = (int64_t)G * kIsLvT;
+    const int64_t c0 = min(n, (int64_t)b * chunk), c1 = min(n, c0 + chunk);
+    ISeg* cur = segA;
+    ISeg* nxt = segB;
+    for (int v = 0; v < levels; ++v) {
+        const int nseg = is_load_count(cnt + 2 + v);
+        // 1 pivot
+        for (int64_t s = gt; s < nseg; s += gstride) {
+            ISeg g = cur[s];
+            g.K = 0;
+            g.active = 1;
+            g.childL = g.childR = -1;
+            if (g.depth == 0) {
+                g.active = 0;
+                heap[atomicAdd(cnt, 1)] = g;
+            } else {
+                const int f = g.f, a = f + 1, bb = f + (g.l - f) / 2, c = g.l - 1;
+                const uint32_t ka = key[a], kb = key[bb], kc = key[c];
+                int m;
+                if (ka < kb) m = (kb < kc) ? bb : (ka < kc) ? c : a;
+                else m = (ka < kc) ? a : (kb < kc) ? c : bb;
+                is_swap(key, val, f, m);
+                g.pivot = key[f];
+            }
+            cur[s] = g;
+        }
+        is_grid_sync(bar, target);
+        // 2 flags and block-local ranks
+        int carL = 0, carR = 0;
+        for (int64_t base = c0; base < c1; base += kIsLvT) {
+            const int64_t i = base + tid;
+            int fl = 0, fr = 0;
+            if (i < c1) {
+                const int s = segid[i];
+                if (s >= 0) {
+                    const ISeg& g = cur[s];
+                    if (g.active && i != g.f) {
+                        const uint32_t p = g.pivot, k = key[i];
+                        fl = !(k < p);
+                        fr = !(p < k);
+                    }
+                }
+            }
+            int el, er, tl, tr;
+            is_block_scan2(fl, fr, el, er, tl, tr, sh);
+            if (i < c1) {
+                SL[i] = carL + el;
+                SR[i] = carR + er;
+                F[i] = (uint8_t)(fl | (fr << 1));
+            }
+            carL += tl;
+            carR += tr;
+        }
+        if (tid == 0) {
+            bsum[b] = carL;
+            bsum[G + b] = carR;
+        }
+        is_grid_sync(bar, target);
+        // 3 global ranks
+        {
+            int a = 0, r = 0;
+            for (int j = tid; j < b; j += kIsLvT) {
+                a += bsum[j];
+                r += bsum[G + j];
+            }
+            int ea, er, offL, offR;
+            is_block_scan2(a, r, ea, er, offL, offR, sh);
+            for (int64_t i = c0 + tid; i < c1; i += kIsLvT) {
+                SL[i] += offL;
+                SR[i] += offR;
+            }
+            if (b == G - 1 && tid == 0) {
+                SL[n] = offL + carL;
+                SR[n] = offR + carR;
             }
         }
-        FL[i] = fl;
-        FR[i] = fr;
-    }
-}
-
-__global__ void k_is_counts(ISeg* __restrict__ segs, int nseg, const int32_t* __restrict__ SL,
-                            const int32_t* __restrict__ SR) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg || !segs[s].active) return;
-    const int b = segs[s].f + 1, l = segs[s].l;
-    segs[s].nL = SL[l] - SL[b];
-    segs[s].nR = SR[l] - SR[b];
-}
-
-// posL[first + 1 + k] = position of the k-th left stop; posR[first + 1 + k] = the k-th right stop
-// from the end (both inside the segment's own range)
-__global__ void k_is_rank(const int32_t* __restrict__ segid, const ISeg* __restrict__ segs,
-                          const int32_t* __restrict__ FL, const int32_t* __restrict__ FR, const int32_t* __restrict__ SL,
-                          const int32_t* __restrict__ SR, int64_t n, int32_t* __restrict__ posL,
-                          int32_t* __restrict__ posR) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (!FL[i] && !FR[i]) continue;
-        const ISeg& g = segs[segid[i]];
-        const int b = g.f + 1;
-        if (FL[i]) posL[b + (SL[i] - SL[b])] = (int32_t)i;
-        if (FR[i]) posR[b + (SR[g.l] - SR[i + 1])] = (int32_t)i;
-    }
-}
-
-// K = the number of k < min(nL, nR) with posL[k] < posR[k]: the predicate holds on a prefix (posL
-// rises, posR falls), so one thread per segment finds its end by bisection
-__global__ void k_is_k(ISeg* __restrict__ segs, int nseg, const int32_t* __restrict__ posL,
-                       const int32_t* __restrict__ posR) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg || !segs[s].active) return;
-    const int b = segs[s].f + 1;
-    int lo = 0, hi = min(segs[s].nL, segs[s].nR);  // first k where the predicate fails
-    while (lo < hi) {
-        const int mid = lo + ((hi - lo) >> 1);
-        if (posL[b + mid] < posR[b + mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    segs[s].K = lo;
-}
-
-__global__ void k_is_swap(const int32_t* __restrict__ segid, const ISeg* __restrict__ segs,
-                          const int32_t* __restrict__ posL, const int32_t* __restrict__ posR, int64_t n,
-                          uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
-    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-        const int s = segid[j];
-        if (s < 0 || !segs[s].active) continue;
-        const int k = (int)j - (segs[s].f + 1);
-        if (k >= 0 && k < segs[s].K) is_swap(key, val, posL[j], posR[j]);  // disjoint pairs
-    }
-}
-
-__global__ void k_is_split(ISeg* __restrict__ segs, int nseg, const int32_t* __restrict__ posL,
-                           const int32_t* __restrict__ posR, ISeg* __restrict__ next, int32_t* __restrict__ next_cnt) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    ISeg g = segs[s];
-    g.childL = g.childR = -1;
-    if (g.active) {
-        const int b = g.f + 1, K = g.K;
-        int cut;
-        if (K < g.nL) cut = K > 0 ? min(posL[b + K], posR[b + K - 1]) : posL[b + K];
-        else cut = posR[b + K - 1];
-        g.cut = cut;
-        const int d = g.depth - 1;
-        if (cut - g.f > kIsThreshold) {
-            const int id = atomicAdd(next_cnt, 1);
-            ISeg c = {};
-            c.f = g.f;
-            c.l = cut;
-            c.depth = d;
-            next[id] = c;
-            g.childL = id;
+        is_grid_sync(bar, target);
+        // 4 stop positions; stop counts
+        for (int64_t s = gt; s < nseg; s += gstride) {
+            if (!cur[s].active) continue;
+            const int bb = cur[s].f + 1, l = cur[s].l;
+            cur[s].nL = SL[l] - SL[bb];
+            cur[s].nR = SR[l] - SR[bb];
         }
-        if (g.l - cut > kIsThreshold) {
-            const int id = atomicAdd(next_cnt, 1);
-            ISeg c = {};
-            c.f = cut;
-            c.l = g.l;
-            c.depth = d;
-            next[id] = c;
-            g.childR = id;
+        for (int64_t i = gt; i < n; i += gstride) {
+            const int fb = F[i];
+            if (!fb) continue;
+            const ISeg& g = cur[segid[i]];
+            const int bb = g.f + 1;
+            if (fb & 1) posL[bb + (SL[i] - SL[bb])] = (int32_t)i;
+            if (fb & 2) posR[bb + (SR[g.l] - SR[i + 1])] = (int32_t)i;
         }
-    }
-    segs[s] = g;
-}
-
-__global__ void k_is_segid(int32_t* __restrict__ segid, const ISeg* __restrict__ segs, int64_t n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int s = segid[i];
-        if (s < 0) continue;
-        const ISeg& g = segs[s];
-        segid[i] = !g.active ? -1 : (i < g.cut ? g.childL : g.childR);
+        is_grid_sync(bar, target);
+        // 5 K by bisection
+        for (int64_t s = gt; s < nseg; s += gstride) {
+            if (!cur[s].active) continue;
+            const int bb = cur[s].f + 1;
+            int lo = 0, hi = min(cur[s].nL, cur[s].nR);
+            while (lo < hi) {
+                const int mid = lo + ((hi - lo) >> 1);
+                if (posL[bb + mid] < posR[bb + mid]) lo = mid + 1;
+                else hi = mid;
+            }
+            cur[s].K = lo;
+        }
+        is_grid_sync(bar, target);
+        // 6 swaps; cut and children
+        for (int64_t j = gt; j < n; j += gstride) {
+            const int s = segid[j];
+            if (s < 0) continue;
+            const ISeg& g = cur[s];
+            if (!g.active) continue;
+            const int k = (int)j - (g.f + 1);
+            if (k >= 0 && k < g.K) is_swap(key, val, posL[j], posR[j]);  // disjoint pairs
+        }
+        for (int64_t s = gt; s < nseg; s += gstride) {
+            ISeg g = cur[s];
+            if (!g.active) continue;
+            const int bb = g.f + 1, K = g.K;
+            int cut;
+            if (K < g.nL) cut = K > 0 ? min(posL[bb + K], posR[bb + K - 1]) : posL[bb + K];
+            else cut = posR[bb + K - 1];
+            cur[s].cut = cut;  // the swap loop above reads the other fields of cur[s]
+            cur[s].childL = is_child(g.f, cut, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
+            cur[s].childR = is_child(cut, g.l, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
+        }
+        is_grid_sync(bar, target);
+        // 7 next segment ids
+        for (int64_t i = gt; i < n; i += gstride) {
+            const int s = segid[i];
+            if (s < 0) continue;
+            const ISeg& g = cur[s];
+            segid[i] = !g.active ? -1 : (i < g.cut ? g.childL : g.childR);
+        }
+        ISeg* t = cur;
+        cur = nxt;
+        nxt = t;
+        if (is_load_count(cnt + 3 + v) == 0) break;  // the same value in every block (after the barrier)
+        is_grid_sync(bar, target);
     }
 }
 
@@ -213,14 +317,7 @@ __device__ void is_adjust_heap(uint32_t* key, uint32_t* val, int hole, int len, 
     is_push_heap(key, val, hole, top, vk, vv);
 }
 
-__global__ void k_is_heap(const ISeg* __restrict__ segs, const int32_t* __restrict__ heap,
-                          const int32_t* __restrict__ heap_cnt, uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
-    const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= *heap_cnt) return;
-    const ISeg g = segs[heap[h]];
-    uint32_t* k = key + g.f;
-    uint32_t* v = val + g.f;
-    const int len = g.l - g.f;
+__device__ void is_heap_sort(uint32_t* k, uint32_t* v, int len) {
     if (len >= 2) {  // __make_heap
         for (int parent = (len - 2) / 2;; --parent) {
             is_adjust_heap(k, v, parent, len, k[parent], v[parent]);
@@ -236,92 +333,316 @@ __global__ void k_is_heap(const ISeg* __restrict__ segs, const int32_t* __restri
     }
 }
 
-static inline int is_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
+// Heap segments (depth exhausted, all longer than kIsSmall) -- one 256-thread block each, the keys
+// and 16-bit local indices resident in LDS (6 B per element):
+//   make_heap  the parents of one heap depth sift down in parallel (their subtrees are disjoint, and
+//              __make_heap takes every deeper parent first), deepest depth first;
+//   sort_heap  one wave: each __adjust_heap descent reads the six-level subtree below the hole at
+//              once (lane j: internal node j, its larger child by `right < left`), walks the path in
+//              scalar registers and moves the path's children up with one store per lane; the
+//              push-up of the displaced value runs on one lane.
+// The values follow the local indices at the end (vtmp: the segment's original values).  A segment
+// above kHeapLds elements falls back to the one-thread global-memory heapsort.
+constexpr int kHeapLds = 26624;  // 6 B x 26624 = 156 KB of LDS
+
+// Orders one wave's LDS accesses across lanes: a compiler barrier plus lgkmcnt(0).
+__device__ __forceinline__ void is_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ void is_sift_lds(uint32_t* sk, uint16_t* si, int hole, int len, uint32_t vk, uint16_t vi) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (sk[second] < sk[second - 1]) second--;
+        sk[hole] = sk[second];
+        si[hole] = si[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        sk[hole] = sk[second - 1];
+        si[hole] = si[second - 1];
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && sk[parent] < vk) {
+        sk[hole] = sk[parent];
+        si[hole] = si[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    sk[hole] = vk;
+    si[hole] = vi;
+}
+
+__global__ __launch_bounds__(256) void k_is_heap(const ISeg* __restrict__ segs, const int32_t* __restrict__ heap_cnt,
+                                                 uint32_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                 uint32_t* __restrict__ vtmp) {
+    extern __shared__ uint32_t is_smem[];
+    if ((int)blockIdx.x >= *heap_cnt) return;
+    const ISeg g = segs[blockIdx.x];
+    const int len = g.l - g.f, tid = threadIdx.x, lane = tid & 63;
+    if (len > kHeapLds) {
+        if (tid == 0) is_heap_sort(key + g.f, val + g.f, len);
+        return;
+    }
+    uint32_t* sk = is_smem;
+    uint16_t* si = reinterpret_cast<uint16_t*>(is_smem + len);
+    for (int i = tid; i < len; i += 256) {
+        sk[i] = key[g.f + i];
+        si[i] = (uint16_t)i;
+        vtmp[g.f + i] = val[g.f + i];
+    }
+    __syncthreads();
+    if (len >= 2) {  // __make_heap, one heap depth at a time
+        const int last_parent = (len - 2) / 2;
+        int D = 0;
+        while ((2 << D) - 1 <= last_parent) ++D;  // depth of the last parent
+        for (int d = D; d >= 0; --d) {
+            const int lo = (1 << d) - 1, hi = min((2 << d) - 2, last_parent);
+            for (int p = hi - tid; p >= lo; p -= 256) is_sift_lds(sk, si, p, len, sk[p], si[p]);
+            __syncthreads();
+        }
+    }
+    if (tid < 64) {  // __sort_heap
+        // lane j < 63: internal node j of a six-level subtree (breadth-first: depth dj, offset oj)
+        const int dj = 31 - __clz(lane + 1), oj = lane + 1 - (1 << dj);
+        for (int last = len - 1; last >= 1; --last) {
+            const uint32_t vk = sk[last];
+            const uint16_t vi = si[last];
+            sk[last] = sk[0];
+            si[last] = si[0];
+            is_lds_fence();  // the stores above land before the reads below (LDS is in order per wave)
+            const int n2 = (last - 1) / 2;  // nodes below n2 have two children inside [0, last)
+            int hole = 0;
+            while (hole < n2) {
+                const int gn = ((hole + 1) << dj) - 1 + oj;
+                const bool has2 = lane < 63 && gn < n2;
+                uint32_t kl = 0, kr = 0;
+                uint16_t il = 0, ir = 0;
+                if (has2) {
+                    kl = sk[2 * gn + 1];
+                    kr = sk[2 * gn + 2];
+                    il = si[2 * gn + 1];
+                    ir = si[2 * gn + 2];
+                }
+                const bool left = has2 && kr < kl;  // libstdc++: second-- when right < left
+                const uint64_t m2 = __ballot(has2), ml = __ballot(left);
+                uint64_t path = 0;
+                int j = 0;
+                while (j < 63 && ((m2 >> j) & 1)) {
+                    path |= 1ull << j;
+                    j = 2 * j + (((ml >> j) & 1) ? 1 : 2);
+                }
+                is_lds_fence();
+                if ((path >> lane) & 1) {
+                    sk[gn] = left ? kl : kr;
+                    si[gn] = left ? il : ir;
+                }
+                const int dd = 31 - __clz(j + 1);
+                hole = ((hole + 1) << dd) - 1 + (j + 1 - (1 << dd));
+                is_lds_fence();
+            }
+            if (lane == 0) {  // the even-length tail and __push_heap of the displaced value
+                const int len2 = last;
+                if ((len2 & 1) == 0 && hole == (len2 - 2) / 2) {
+                    const int c = 2 * (hole + 1) - 1;
+                    sk[hole] = sk[c];
+                    si[hole] = si[c];
+                    hole = c;
+                }
+                int parent = (hole - 1) / 2;
+                while (hole > 0 && sk[parent] < vk) {
+                    sk[hole] = sk[parent];
+                    si[hole] = si[parent];
+                    hole = parent;
+                    parent = (hole - 1) / 2;
+                }
+                sk[hole] = vk;
+                si[hole] = vi;
+            }
+            is_lds_fence();
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < len; i += 256) {
+        key[g.f + i] = sk[i];
+        val[g.f + i] = vtmp[g.f + si[i]];
+    }
+}
+
+// One wave finishes a segment of <= kIsSmall elements in LDS: the same median / unguarded-partition /
+// depth / heapsort steps as the level kernels, run one partition at a time with an explicit stack
+// (right part pushed, left part continued, as __introsort_loop recurses).  Stops are ranked with
+// ballots: left stops forward from first + 1, right stops backward from last - 1.
+__global__ __launch_bounds__(64) void k_is_small(const ISmall* __restrict__ segs, const int32_t* __restrict__ small_cnt,
+                                                 uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+    __shared__ uint32_t sk[kIsSmall], sv[kIsSmall];
+    __shared__ int32_t pl[kIsSmall], pr[kIsSmall];
+    __shared__ int32_t stk[3 * 72];
+    if ((int)blockIdx.x >= *small_cnt) return;
+    const ISmall g = segs[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int len = g.l - g.f;
+    for (int i = lane; i < len; i += 64) {
+        sk[i] = key[g.f + i];
+        sv[i] = val[g.f + i];
+    }
+    __syncthreads();
+    int sp = 0, f = 0, l = len, depth = g.depth;
+    for (;;) {
+        while (l - f > kIsThreshold) {
+            if (depth == 0) {
+                if (lane == 0) is_heap_sort(sk + f, sv + f, l - f);
+                __syncthreads();
+                break;
+            }
+            --depth;
+            const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+            const uint32_t ka = sk[a], kb = sk[b], kc = sk[c];
+            int m;
+            if (ka < kb) m = (kb < kc) ? b : (ka < kc) ? c : a;
+            else m = (ka < kc) ? a : (kb < kc) ? c : b;
+            __syncthreads();
+            if (lane == 0) {
+                const uint32_t tk = sk[f], tv = sv[f];
+                sk[f] = sk[m];
+                sv[f] = sv[m];
+                sk[m] = tk;
+                sv[m] = tv;
+            }
+            __syncthreads();
+            const uint32_t p = sk[f];
+            int nL = 0, nR = 0;
+            for (int base = f + 1; base < l; base += 64) {
+                const int i = base + lane;
+                const bool st = i < l && !(sk[i] < p);
+                const uint64_t bal = __ballot(st);
+                if (st) pl[nL + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = i;
+                nL += __popcll(bal);
+            }
+            for (int base = l - 1; base > f; base -= 64) {
+                const int i = base - lane;
+                const bool st = i > f && !(p < sk[i]);
+                const uint64_t bal = __ballot(st);
+                if (st) pr[nR + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = i;
+                nR += __popcll(bal);
+            }
+            __syncthreads();
+            const int kmax = min(nL, nR);
+            int K = kmax;  // the swaps run while the k-th left stop lies left of the k-th right stop
+            for (int k0 = 0; k0 < kmax; k0 += 64) {
+                const int k = k0 + lane;
+                const uint64_t bal = __ballot(k < kmax && !(pl[k] < pr[k]));
+                if (bal) {
+                    K = k0 + __builtin_ctzll(bal);
+                    break;
+                }
+            }
+            for (int k = lane; k < K; k += 64) {
+                const int x = pl[k], y = pr[k];
+                const uint32_t tk = sk[x], tv = sv[x];
+                sk[x] = sk[y];
+                sv[x] = sv[y];
+                sk[y] = tk;
+                sv[y] = tv;
+            }
+            const int cut = K < nL ? (K > 0 ? min(pl[K], pr[K - 1]) : pl[K]) : pr[K - 1];
+            __syncthreads();
+            if (l - cut > kIsThreshold) {  // __introsort_loop(cut, last, depth)
+                stk[3 * sp] = cut;
+                stk[3 * sp + 1] = l;
+                stk[3 * sp + 2] = depth;
+                ++sp;
+            }
+            l = cut;
+        }
+        if (sp == 0) break;
+        --sp;
+        f = stk[3 * sp];
+        l = stk[3 * sp + 1];
+        depth = stk[3 * sp + 2];
+    }
+    __syncthreads();
+    for (int i = lane; i < len; i += 64) {
+        key[g.f + i] = sk[i];
+        val[g.f + i] = sv[i];
+    }
+}
 
 // Leaves key/val so that a stable sort by key gives std::sort's order.  depth_limit < 0: libstdc++'s
 // 2 floor(log2 n); otherwise the given limit (tests reach the heapsort fallback with it).
 int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int depth_limit) {
     hipStream_t s = ctx->stream;
     if (n <= kIsThreshold) return PITT_OK;
-    const int64_t cap = n / kIsThreshold + 16;  // active segments hold > 16 elements each
+    if (n > INT32_MAX - 1) return ctx->fail(PITT_E_INVALID, "introsort: n exceeds int32 positions");
+    const int64_t cap = n / kIsSmall + 16;            // level segments hold > kIsSmall elements each
+    const int64_t cap_small = n / kIsThreshold + 16;  // one-wave segments hold > 16 each
+    const int kMaxLevels = 128;
+    int lg = 0;
+    while (((int64_t)2 << lg) <= n) ++lg;  // std::__lg(n)
+    const int depth = depth_limit >= 0 ? depth_limit : 2 * lg;
+    // every level lowers the depth of all its segments, so depth + 1 levels bound the loop
+    if (depth > kMaxLevels - 4) return ctx->fail(PITT_E_INVALID, "introsort: depth limit above 124");
+    // grid barriers need every block resident: at most PITT_IS_COOP_MAX blocks (64), well under one
+    // block per CU, each within the occupancy limit (checked once).  A plain launch: the cooperative
+    // launch API measured ~3.5 ms of host-side cost per call.
+    static int coop_blocks = 0;
+    if (coop_blocks == 0) {
+        int dev = 0, per_cu = 0;
+        hipDeviceProp_t prop;
+        PITT_HIP_TRY(hipGetDevice(&dev));
+        PITT_HIP_TRY(hipGetDeviceProperties(&prop, dev));
+        PITT_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_is_levels, kIsLvT, 0));
+        if (per_cu < 1) return ctx->fail(PITT_E_NODEVICE, "introsort: level kernel does not fit a CU");
+        PITT_HIP_TRY(hipFuncSetAttribute((const void*)k_is_heap, hipFuncAttributeMaxDynamicSharedMemorySize, kHeapLds * 6));
+        coop_blocks = std::max(1, std::min(prop.multiProcessorCount * std::min(per_cu, 1), PITT_IS_COOP_MAX));
+    }
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(coop_blocks, (n + kIsLvT - 1) / kIsLvT));
+    const int64_t chunk = (n + G - 1) / G;
     ISeg* segA = (ISeg*)ctx->buf("is_segA", (size_t)cap * sizeof(ISeg));
     ISeg* segB = (ISeg*)ctx->buf("is_segB", (size_t)cap * sizeof(ISeg));
+    ISeg* heapsegs = (ISeg*)ctx->buf("is_heapsegs", (size_t)cap * sizeof(ISeg));
+    ISmall* small = (ISmall*)ctx->buf("is_small", (size_t)cap_small * sizeof(ISmall));
     int32_t* segid = (int32_t*)ctx->buf("is_segid", (size_t)n * 4);
-    int32_t* FL = (int32_t*)ctx->buf("is_FL", (size_t)(n + 1) * 4);
-    int32_t* FR = (int32_t*)ctx->buf("is_FR", (size_t)(n + 1) * 4);
+    uint8_t* F = (uint8_t*)ctx->buf("is_F", (size_t)n);
     int32_t* SL = (int32_t*)ctx->buf("is_SL", (size_t)(n + 1) * 4);
     int32_t* SR = (int32_t*)ctx->buf("is_SR", (size_t)(n + 1) * 4);
     int32_t* posL = (int32_t*)ctx->buf("is_posL", (size_t)n * 4);
     int32_t* posR = (int32_t*)ctx->buf("is_posR", (size_t)n * 4);
-    int32_t* cnt = (int32_t*)ctx->buf("is_cnt", 16);
-    int32_t* heap = (int32_t*)ctx->buf("is_heap", (size_t)cap * 4);
+    int32_t* bsum = (int32_t*)ctx->buf("is_bsum", (size_t)2 * 512 * 4);
+    // cnt[0] heap segments, cnt[1] one-wave segments, cnt[2 + v] level v's segment count
+    // cnt[kMaxLevels + 2]: the grid barrier's arrival counter
+    int32_t* cnt = (int32_t*)ctx->buf("is_cnt", (size_t)(kMaxLevels + 4) * 4);
     int32_t* hcnt = (int32_t*)ctx->pinned("is_hcnt", 16);
-    if (!segA || !segB || !segid || !FL || !FR || !SL || !SR || !posL || !posR || !cnt || !heap || !hcnt)
+    uint32_t* vtmp = (uint32_t*)ctx->buf("is_vtmp", (size_t)n * 4);
+    if (!vtmp || !segA || !segB || !heapsegs || !small || !segid || !F || !SL || !SR || !posL || !posR || !bsum || !cnt ||
+        !hcnt)
         return ctx->fail(PITT_E_NOMEM, "introsort scratch");
-    size_t scan_bytes = 0;
-    PITT_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, FL, SL, (int)(n + 1), s));
-    void* scan_tmp = ctx->buf("is_scan_tmp", std::max<size_t>(scan_bytes, 16));
-    if (!scan_tmp) return ctx->fail(PITT_E_NOMEM, "introsort scan scratch");
-    int lg = 0;
-    while (((int64_t)2 << lg) <= n) ++lg;  // std::__lg(n)
+    PITT_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(kMaxLevels + 4) * 4, s));
+    uint32_t* bar = (uint32_t*)(cnt + kMaxLevels + 2);
+    const int32_t one = 1;
+    const ISmall sroot = {0, (int32_t)n, depth, 0};
     ISeg root = {};
     root.f = 0;
     root.l = (int32_t)n;
-    root.depth = depth_limit >= 0 ? depth_limit : 2 * lg;
-    PITT_HIP_TRY(hipStreamSynchronize(s));
-    PITT_HIP_TRY(hipMemcpy(segA, &root, sizeof root, hipMemcpyHostToDevice));
-    PITT_HIP_TRY(hipMemsetAsync(segid, 0, (size_t)n * 4, s));
-    PITT_HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
-    int nseg = 1;
-    // heap segments are appended across levels into one list; their descriptors stay in a copy
-    ISeg* heapsegs = (ISeg*)ctx->buf("is_heapsegs", (size_t)cap * sizeof(ISeg));
-    int32_t* heapmap = (int32_t*)ctx->buf("is_heapmap", (size_t)cap * 4);
-    if (!heapsegs || !heapmap) return ctx->fail(PITT_E_NOMEM, "introsort heap list");
-    int nheap = 0;
-    ISeg* cur = segA;
-    ISeg* nxt = segB;
-    const int g = is_grid(n);
-    while (nseg > 0) {
-        const int sb = (nseg + 255) / 256;
-        PITT_HIP_TRY(hipMemsetAsync(cnt, 0, 16, s));
-        hipLaunchKernelGGL(k_is_pivot, dim3(sb), dim3(256), 0, s, cur, nseg, key, val, heap, cnt + 1);
-        hipLaunchKernelGGL(k_is_flags, dim3(g), dim3(256), 0, s, segid, cur, key, n, FL, FR);
-        PITT_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, FL, SL, (int)(n + 1), s));
-        PITT_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, FR, SR, (int)(n + 1), s));
-        hipLaunchKernelGGL(k_is_counts, dim3(sb), dim3(256), 0, s, cur, nseg, SL, SR);
-        hipLaunchKernelGGL(k_is_rank, dim3(g), dim3(256), 0, s, segid, cur, FL, FR, SL, SR, n, posL, posR);
-        hipLaunchKernelGGL(k_is_k, dim3(sb), dim3(256), 0, s, cur, nseg, posL, posR);
-        hipLaunchKernelGGL(k_is_swap, dim3(g), dim3(256), 0, s, segid, cur, posL, posR, n, key, val);
-        hipLaunchKernelGGL(k_is_split, dim3(sb), dim3(256), 0, s, cur, nseg, posL, posR, nxt, cnt);
-        hipLaunchKernelGGL(k_is_segid, dim3(g), dim3(256), 0, s, segid, cur, n);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        const int nh = hcnt[1];
-        if (nh > 0) {  // this level's depth-exhausted segments: keep their descriptors for the heap pass
-            std::vector<int32_t> hl((size_t)nh);
-            PITT_HIP_TRY(hipMemcpy(hl.data(), heap, (size_t)nh * 4, hipMemcpyDeviceToHost));
-            for (int i = 0; i < nh; ++i) {
-                PITT_HIP_TRY(hipMemcpyAsync(heapsegs + nheap, cur + hl[(size_t)i], sizeof(ISeg),
-                                            hipMemcpyDeviceToDevice, s));
-                ++nheap;
-            }
-        }
-        nseg = hcnt[0];
-        std::swap(cur, nxt);
+    root.depth = depth;
+    if (n <= kIsSmall) {
+        PITT_HIP_TRY(hipMemcpyAsync(small, &sroot, sizeof sroot, hipMemcpyHostToDevice, s));
+        PITT_HIP_TRY(hipMemcpyAsync(cnt + 1, &one, 4, hipMemcpyHostToDevice, s));
+    } else {
+        PITT_HIP_TRY(hipMemcpyAsync(segA, &root, sizeof root, hipMemcpyHostToDevice, s));
+        PITT_HIP_TRY(hipMemcpyAsync(cnt + 2, &one, 4, hipMemcpyHostToDevice, s));
+        PITT_HIP_TRY(hipMemsetAsync(segid, 0, (size_t)n * 4, s));
+        hipLaunchKernelGGL(k_is_levels, dim3(G), dim3(kIsLvT), 0, s, segA, segB, heapsegs, small, cnt, segid, F, SL, SR,
+                           posL, posR, bsum, key, val, n, chunk, depth + 1, bar);
     }
-    if (nheap > 0) {
-        std::vector<int32_t> ids((size_t)nheap);
-        for (int i = 0; i < nheap; ++i) ids[(size_t)i] = i;
-        int32_t* hc = (int32_t*)ctx->buf("is_heapcnt", 16);
-        if (!hc) return ctx->fail(PITT_E_NOMEM, "introsort heap count");
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        PITT_HIP_TRY(hipMemcpy(heapmap, ids.data(), (size_t)nheap * 4, hipMemcpyHostToDevice));
-        PITT_HIP_TRY(hipMemcpy(hc, &nheap, 4, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(k_is_heap, dim3((nheap + 63) / 64), dim3(64), 0, s, heapsegs, heapmap, hc, key, val);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-    }
+    PITT_HIP_TRY(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, s));
+    PITT_HIP_TRY(hipStreamSynchronize(s));  // the host memcpys above read stack values: complete them too
+    if (hcnt[1] > 0) hipLaunchKernelGGL(k_is_small, dim3(hcnt[1]), dim3(64), 0, s, small, cnt + 1, key, val);
+    if (hcnt[0] > 0)
+        hipLaunchKernelGGL(k_is_heap, dim3(hcnt[0]), dim3(256), kHeapLds * 6, s, heapsegs, cnt, key, val, vtmp);
+    PITT_HIP_TRY(hipGetLastError());
     return PITT_OK;
 }
 

@@ -104,19 +104,27 @@ __global__ __launch_bounds__(kBlock) void k_vox_minmax(const float* __restrict__
     }
 }
 
-// One thread: combine the block partials, then PCL's grid arithmetic in float / int.
-__global__ void k_vox_setup(const float* __restrict__ part, const int64_t* __restrict__ part_n, int blocks,
-                            float lx, float ly, float lz, VoxParams* __restrict__ out) {
-    if (threadIdx.x != 0) return;
+// One wave: combine the block partials (min / max are order-free; the partials are finite or the
+// FLT_MAX sentinels), then PCL's grid arithmetic in float / int on lane 0.
+__global__ __launch_bounds__(64) void k_vox_setup(const float* __restrict__ part, const int64_t* __restrict__ part_n,
+                                                  int blocks, float lx, float ly, float lz, VoxParams* __restrict__ out) {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int64_t nf = 0;
-    for (int b = 0; b < blocks; ++b) {
+    for (int b = threadIdx.x; b < blocks; b += 64) {
         for (int k = 0; k < 3; ++k) {
             mn[k] = fminf(mn[k], part[b * 8 + k]);
             mx[k] = fmaxf(mx[k], part[b * 8 + 3 + k]);
         }
         nf += part_n[b];
     }
+    for (int off = 32; off > 0; off >>= 1) {
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], off, 64));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off, 64));
+        }
+        nf += __shfl_xor(nf, off, 64);
+    }
+    if (threadIdx.x != 0) return;
     VoxParams p;
     p.inv[0] = 1.0f / lx;
     p.inv[1] = 1.0f / ly;
