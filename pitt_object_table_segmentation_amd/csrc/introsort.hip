@@ -345,10 +345,12 @@ __device__ void is_heap_sort(uint32_t* k, uint32_t* v, int len) {
 // above kHeapLds elements falls back to the one-thread global-memory heapsort.
 constexpr int kHeapLds = 26624;  // 6 B x 26624 = 156 KB of LDS
 
-// Orders one wave's LDS accesses across lanes: a compiler barrier plus lgkmcnt(0).
-__device__ __forceinline__ void is_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Orders one wave's LDS accesses across lanes: LDS executes a wave's accesses in issue order, so a
+// compiler barrier (no reordering of the accesses around it) is enough.
+__device__ __forceinline__ void is_lds_fence() { asm volatile("" ::: "memory"); }
 
-__device__ void is_sift_lds(uint32_t* sk, uint16_t* si, int hole, int len, uint32_t vk, uint16_t vi) {
+template <typename V>
+__device__ void is_sift_lds(uint32_t* sk, V* si, int hole, int len, uint32_t vk, V vi) {
     const int top = hole;
     int second = hole;
     while (second < (len - 1) / 2) {
@@ -375,13 +377,96 @@ __device__ void is_sift_lds(uint32_t* sk, uint16_t* si, int hole, int len, uint3
     si[hole] = vi;
 }
 
+// __make_heap over LDS by NT threads (t = this thread's rank): one heap depth at a time, deepest first
+// (the parents of one depth have disjoint subtrees, and __make_heap takes every deeper parent first).
+template <int NT, typename V>
+__device__ void is_make_heap_lds(uint32_t* sk, V* si, int len, int t) {
+    if (len < 2) return;
+    const int last_parent = (len - 2) / 2;
+    int D = 0;
+    while ((2 << D) - 1 <= last_parent) ++D;  // depth of the last parent
+    for (int d = D; d >= 0; --d) {
+        const int lo = (1 << d) - 1, hi = min((2 << d) - 2, last_parent);
+        for (int p = hi - t; p >= lo; p -= NT) is_sift_lds(sk, si, p, len, sk[p], si[p]);
+        if constexpr (NT == 64) is_lds_fence();
+        else __syncthreads();
+    }
+}
+
+// __sort_heap over LDS by one wave: each __adjust_heap descent reads the six-level subtree below the
+// hole at once (lane j: internal node j, its larger child by `right < left`), walks the path in
+// scalar registers and moves the path's children up with one store per lane; the push-up of the
+// displaced value runs on lane 0.
+template <typename V>
+__device__ void is_sort_heap_wave(uint32_t* sk, V* si, int len, int lane) {
+    // lane j < 63: internal node j of a six-level subtree (breadth-first: depth dj, offset oj)
+    const int dj = 31 - __clz(lane + 1), oj = lane + 1 - (1 << dj);
+    for (int last = len - 1; last >= 1; --last) {
+        const uint32_t vk = sk[last];
+        const V vi = si[last];
+        is_lds_fence();
+        if (lane == 0) {
+            sk[last] = sk[0];
+            si[last] = si[0];
+        }
+        is_lds_fence();  // the stores above land before the reads below (LDS is in order per wave)
+        const int n2 = (last - 1) / 2;  // nodes below n2 have two children inside [0, last)
+        int hole = 0;
+        while (hole < n2) {
+            const int gn = ((hole + 1) << dj) - 1 + oj;
+            const bool has2 = lane < 63 && gn < n2;
+            uint32_t kl = 0, kr = 0;
+            V il = 0, ir = 0;
+            if (has2) {
+                kl = sk[2 * gn + 1];
+                kr = sk[2 * gn + 2];
+                il = si[2 * gn + 1];
+                ir = si[2 * gn + 2];
+            }
+            const bool left = has2 && kr < kl;  // libstdc++: second-- when right < left
+            const uint64_t m2 = __ballot(has2), ml = __ballot(left);
+            uint64_t path = 0;
+            int j = 0;
+            while (j < 63 && ((m2 >> j) & 1)) {
+                path |= 1ull << j;
+                j = 2 * j + (((ml >> j) & 1) ? 1 : 2);
+            }
+            if ((path >> lane) & 1) {  // the next round reads below the new hole only
+                sk[gn] = left ? kl : kr;
+                si[gn] = left ? il : ir;
+            }
+            const int dd = 31 - __clz(j + 1);
+            hole = ((hole + 1) << dd) - 1 + (j + 1 - (1 << dd));
+        }
+        is_lds_fence();
+        if (lane == 0) {  // the even-length tail and __push_heap of the displaced value
+            if ((last & 1) == 0 && hole == (last - 2) / 2) {
+                const int c = 2 * (hole + 1) - 1;
+                sk[hole] = sk[c];
+                si[hole] = si[c];
+                hole = c;
+            }
+            int parent = (hole - 1) / 2;
+            while (hole > 0 && sk[parent] < vk) {
+                sk[hole] = sk[parent];
+                si[hole] = si[parent];
+                hole = parent;
+                parent = (hole - 1) / 2;
+            }
+            sk[hole] = vk;
+            si[hole] = vi;
+        }
+        is_lds_fence();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_is_heap(const ISeg* __restrict__ segs, const int32_t* __restrict__ heap_cnt,
                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ val,
                                                  uint32_t* __restrict__ vtmp) {
     extern __shared__ uint32_t is_smem[];
     if ((int)blockIdx.x >= *heap_cnt) return;
     const ISeg g = segs[blockIdx.x];
-    const int len = g.l - g.f, tid = threadIdx.x, lane = tid & 63;
+    const int len = g.l - g.f, tid = threadIdx.x;
     if (len > kHeapLds) {
         if (tid == 0) is_heap_sort(key + g.f, val + g.f, len);
         return;
@@ -394,76 +479,8 @@ __global__ __launch_bounds__(256) void k_is_heap(const ISeg* __restrict__ segs, 
         vtmp[g.f + i] = val[g.f + i];
     }
     __syncthreads();
-    if (len >= 2) {  // __make_heap, one heap depth at a time
-        const int last_parent = (len - 2) / 2;
-        int D = 0;
-        while ((2 << D) - 1 <= last_parent) ++D;  // depth of the last parent
-        for (int d = D; d >= 0; --d) {
-            const int lo = (1 << d) - 1, hi = min((2 << d) - 2, last_parent);
-            for (int p = hi - tid; p >= lo; p -= 256) is_sift_lds(sk, si, p, len, sk[p], si[p]);
-            __syncthreads();
-        }
-    }
-    if (tid < 64) {  // __sort_heap
-        // lane j < 63: internal node j of a six-level subtree (breadth-first: depth dj, offset oj)
-        const int dj = 31 - __clz(lane + 1), oj = lane + 1 - (1 << dj);
-        for (int last = len - 1; last >= 1; --last) {
-            const uint32_t vk = sk[last];
-            const uint16_t vi = si[last];
-            sk[last] = sk[0];
-            si[last] = si[0];
-            is_lds_fence();  // the stores above land before the reads below (LDS is in order per wave)
-            const int n2 = (last - 1) / 2;  // nodes below n2 have two children inside [0, last)
-            int hole = 0;
-            while (hole < n2) {
-                const int gn = ((hole + 1) << dj) - 1 + oj;
-                const bool has2 = lane < 63 && gn < n2;
-                uint32_t kl = 0, kr = 0;
-                uint16_t il = 0, ir = 0;
-                if (has2) {
-                    kl = sk[2 * gn + 1];
-                    kr = sk[2 * gn + 2];
-                    il = si[2 * gn + 1];
-                    ir = si[2 * gn + 2];
-                }
-                const bool left = has2 && kr < kl;  // libstdc++: second-- when right < left
-                const uint64_t m2 = __ballot(has2), ml = __ballot(left);
-                uint64_t path = 0;
-                int j = 0;
-                while (j < 63 && ((m2 >> j) & 1)) {
-                    path |= 1ull << j;
-                    j = 2 * j + (((ml >> j) & 1) ? 1 : 2);
-                }
-                is_lds_fence();
-                if ((path >> lane) & 1) {
-                    sk[gn] = left ? kl : kr;
-                    si[gn] = left ? il : ir;
-                }
-                const int dd = 31 - __clz(j + 1);
-                hole = ((hole + 1) << dd) - 1 + (j + 1 - (1 << dd));
-                is_lds_fence();
-            }
-            if (lane == 0) {  // the even-length tail and __push_heap of the displaced value
-                const int len2 = last;
-                if ((len2 & 1) == 0 && hole == (len2 - 2) / 2) {
-                    const int c = 2 * (hole + 1) - 1;
-                    sk[hole] = sk[c];
-                    si[hole] = si[c];
-                    hole = c;
-                }
-                int parent = (hole - 1) / 2;
-                while (hole > 0 && sk[parent] < vk) {
-                    sk[hole] = sk[parent];
-                    si[hole] = si[parent];
-                    hole = parent;
-                    parent = (hole - 1) / 2;
-                }
-                sk[hole] = vk;
-                si[hole] = vi;
-            }
-            is_lds_fence();
-        }
-    }
+    is_make_heap_lds<256>(sk, si, len, tid);
+    if (tid < 64) is_sort_heap_wave(sk, si, len, tid);
     __syncthreads();
     for (int i = tid; i < len; i += 256) {
         key[g.f + i] = sk[i];
@@ -493,7 +510,9 @@ __global__ __launch_bounds__(64) void k_is_small(const ISmall* __restrict__ segs
     for (;;) {
         while (l - f > kIsThreshold) {
             if (depth == 0) {
-                if (lane == 0) is_heap_sort(sk + f, sv + f, l - f);
+                __syncthreads();
+                is_make_heap_lds<64>(sk + f, sv + f, l - f, lane);
+                is_sort_heap_wave(sk + f, sv + f, l - f, lane);
                 __syncthreads();
                 break;
             }
