@@ -87,6 +87,14 @@ def main():
             if launches:
                 vox["kernels"][k] = {"avg_us": round(ms / launches * 1e3, 1)}
         ctx.profile(False)
+        # the same frames in stable order (PITT_VOXEL_ORDER_STABLE: no introsort partitions)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(vox_reps):
+            for fr in frames:
+                ctx.voxel_grid(*fr, order=pitt._lib.PITT_VOXEL_ORDER_STABLE)
+        torch.cuda.synchronize()
+        vox["stable_order_ms_per_frame_wall"] = round((time.perf_counter() - t0) * 1e3 / (vox_reps * len(frames)), 4)
         # NormalEstimation k = 50 on the voxelized frames (estimateNormal's input, obj_segmentation.cpp:253)
         vframes = [ctx.voxel_grid(*fr)[0] for fr in frames]
         for vf in vframes[:2]:
