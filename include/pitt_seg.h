@@ -24,6 +24,9 @@
  *        src/point_cloud_library/pc_manager.cpp:55-67, src/obj_segmentation.cpp:238
  *   pitt_normal_estimation        replaces  NormalEstimation<PointXYZ, Normal>::compute (estimateNormal)
  *        src/point_cloud_library/pc_manager.cpp:68-78
+ *   pitt_axis_height              replaces  the projection + O(n^2) height loop after seg.segment in
+ *        src/segmentation_services/cylinder_segmentation_srv.cpp:129-189 and
+ *        src/segmentation_services/cone_segmentation_srv.cpp:129-189
  *
  * Conventions: plain pointers and sizes, no C++ types, no exceptions.  Every call returns an
  * int status (PITT_OK, PITT_NO_MODEL, or a negative PITT_E_*).  A context is not thread-safe;
@@ -266,6 +269,21 @@ int pitt_sort_pairs(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int3
 int pitt_normal_estimation(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                            int32_t k, const float viewpoint[3], float* nx, float* ny, float* nz,
                            float* curvature, int32_t* neighbours, int32_t* neighbour_count);
+
+/* The post-processing of the cylinder and cone services once PCL has fitted the model
+ * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).
+ * coef[0..5] (host): the model's axis point (cylinder) or apex (cone) and axis direction.  Every point
+ * of the cloud is projected on the axis; *height is the largest float distance
+ * sqrt((dx*dx + dy*dy) + dz*dz) between two projected points, (*idx1, *idx2) the first pair (i > j)
+ * reaching it in the reference's loop order, and centroid[3] the midpoint of that pair
+ * (PITT_AXIS_CYLINDER) or coef[0..2] + 3/4 * height * direction (PITT_AXIS_CONE).  With fewer than two
+ * points (no pair) height = -1 and idx = -1, as the reference leaves them; the cylinder centroid is then
+ * NaN (the reference reads points[-1]).  The reference runs this only when the model has inliers.
+ * x/y/z device SoA of n points; px/py/pz optional device outputs (the projected cloud). */
+enum { PITT_AXIS_CYLINDER = 0, PITT_AXIS_CONE = 1 };
+int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                     const float coef[6], int32_t mode, float* px, float* py, float* pz, float* height,
+                     int32_t* idx1, int32_t* idx2, float centroid[3]);
 
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };

@@ -1085,4 +1085,56 @@ void orc_introsort_pairs(uint32_t* key, uint32_t* val, int64_t n, int32_t depth_
     }
     for (int64_t i = 0; i < n; ++i) key[i] = a[(size_t)i].k, val[i] = a[(size_t)i].v;
 }
+
+// cylinder_segmentation_srv.cpp:53-79 (getNormalizeAxesDirectionVector, getPointOnAxes,
+// getVectorBetweenPoints) and :129-178; cone_segmentation_srv.cpp:129-178 differs only in the centroid.
+// Every operation is a float operation in source order (x86-64 SSE, no FMA); sqrt of a float is the
+// correctly rounded float sqrt (std::sqrt(float), or the double sqrt rounded to float: the same value).
+void orc_axis_height(const float* x, const float* y, const float* z, int64_t n, const float coef[6], int32_t mode,
+                     float* px, float* py, float* pz, float* height, int32_t* idx1, int32_t* idx2,
+                     float centroid[3]) {
+    const float norm = std::sqrt(coef[3] * coef[3] + coef[4] * coef[4] + coef[5] * coef[5]);
+    const float dx = coef[3] / norm, dy = coef[4] / norm, dz = coef[5] / norm;
+    const float a1x = coef[0] + dx * -1.0f, a1y = coef[1] + dy * -1.0f, a1z = coef[2] + dz * -1.0f;
+    const float a2x = coef[0] + dx * 1.0f, a2y = coef[1] + dy * 1.0f, a2z = coef[2] + dz * 1.0f;
+    const float ux = a2x - a1x, uy = a2y - a1y, uz = a2z - a1z;
+    const float gdiv = ux * ux + uy * uy + uz * uz;
+    std::vector<float> qx((size_t)n), qy((size_t)n), qz((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        const float vx = x[i] - a1x, vy = y[i] - a1y, vz = z[i] - a1z;
+        const float g = (vx * ux + vy * uy + vz * uz) / gdiv;
+        qx[(size_t)i] = a1x + g * ux;
+        qy[(size_t)i] = a1y + g * uy;
+        qz[(size_t)i] = a1z + g * uz;
+    }
+    float h = -1.0f;
+    int32_t b1 = -1, b2 = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = 0; j < i; ++j) {  // the reference's j loop, i > j
+            const float ex = qx[(size_t)i] - qx[(size_t)j], ey = qy[(size_t)i] - qy[(size_t)j],
+                        ez = qz[(size_t)i] - qz[(size_t)j];
+            const float d = std::sqrt(ex * ex + ey * ey + ez * ez);
+            if (d > h) {
+                h = d;
+                b1 = (int32_t)i;
+                b2 = (int32_t)j;
+            }
+        }
+    }
+    *height = h;
+    *idx1 = b1;
+    *idx2 = b2;
+    if (mode == 0) {  // cylinder: the midpoint of the pair (no pair: the reference reads points[-1])
+        const float nan = std::numeric_limits<float>::quiet_NaN();
+        centroid[0] = b1 < 0 ? nan : (qx[(size_t)b1] + qx[(size_t)b2]) / 2;
+        centroid[1] = b1 < 0 ? nan : (qy[(size_t)b1] + qy[(size_t)b2]) / 2;
+        centroid[2] = b1 < 0 ? nan : (qz[(size_t)b1] + qz[(size_t)b2]) / 2;
+    } else {  // cone: apex + 3/4 of the height along the axis
+        centroid[0] = coef[0] + 3.0f / 4.0f * h * dx;
+        centroid[1] = coef[1] + 3.0f / 4.0f * h * dy;
+        centroid[2] = coef[2] + 3.0f / 4.0f * h * dz;
+    }
+    if (px)
+        for (int64_t i = 0; i < n; ++i) px[i] = qx[(size_t)i], py[i] = qy[(size_t)i], pz[i] = qz[(size_t)i];
+}
 }  // extern "C"

@@ -131,6 +131,13 @@ int     orc_normal_estimation(const float* x, const float* y, const float* z, in
 void    orc_std_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
 void    orc_partial_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
 void    orc_introsort_pairs(uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit);
+// The axis "height" post-processing of the cylinder / cone services (cylinder_segmentation_srv.cpp:129-189,
+// cone_segmentation_srv.cpp:129-189): every point projected on the axis of coef[0..5], the pair (i > j)
+// of projected points farthest apart (first maximum in loop order), and the centroid (mode 0 cylinder:
+// the pair's midpoint; mode 1 cone: apex + 3/4 height along the axis).  px/py/pz optional.
+void    orc_axis_height(const float* x, const float* y, const float* z, int64_t n, const float coef[6],
+                        int32_t mode, float* px, float* py, float* pz, float* height, int32_t* idx1,
+                        int32_t* idx2, float centroid[3]);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,7 @@ PITT_TILE_POINTS = 2048
 PITT_FLAG_K_NEAR_INTEGER = 1
 PITT_VOXEL_OVERFLOW_COPY = 1
 PITT_VOXEL_ORDER_PCL, PITT_VOXEL_ORDER_STABLE = 0, 1
+PITT_AXIS_CYLINDER, PITT_AXIS_CONE = 0, 1
 
 REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
 DIV_EIGEN32, DIV_TRUE = 0, 1
@@ -151,6 +152,7 @@ SIGNATURES = {
     "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32, _vp,
                                _vp, _vp, _i64p, _i32p]),
     "pitt_sort_pairs": (_i32, [_vp, _vp, _vp, _i64, _i32]),
+    "pitt_axis_height": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp, _f32p, _i32p, _i32p, _f32p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
     "pitt_find_supports": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.POINTER(SupportParams),
                                   ctypes.POINTER(SupportList)]),

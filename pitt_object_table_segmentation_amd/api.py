@@ -358,6 +358,26 @@ class Context:
         self._check(lib.pitt_sort_pairs(self.h, key.data_ptr(), val.data_ptr(), key.numel(), int(depth_limit)),
                     "pitt_sort_pairs")
 
+    def axis_height(self, x, y, z, coefficients, mode: int = L.PITT_AXIS_CYLINDER, projected: bool = False):
+        """The cylinder / cone services' post-processing (cylinder_segmentation_srv.cpp:129-189,
+        cone_segmentation_srv.cpp:129-189) on device tensors: (height, idx1, idx2, centroid[3])
+        [, (px, py, pz) the cloud projected on the axis]."""
+        import torch
+        n = x.numel()
+        coef = np.ascontiguousarray(np.asarray(coefficients, np.float32)[:6])
+        if coef.size != 6:
+            raise ValueError("coefficients: the axis point and direction (6 values) are needed")
+        proj = [torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(3)] if projected else None
+        h = ctypes.c_float()
+        i1, i2 = ctypes.c_int32(), ctypes.c_int32()
+        cen = np.zeros(3, np.float32)
+        self._check(lib.pitt_axis_height(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, _fp(coef), int(mode),
+                                         *((p.data_ptr() for p in proj) if proj else (None, None, None)),
+                                         ctypes.byref(h), ctypes.byref(i1), ctypes.byref(i2), _fp(cen)),
+                    "pitt_axis_height")
+        res = (h.value, i1.value, i2.value, cen)
+        return res + (tuple(p[:n] for p in proj),) if projected else res
+
     # ---- supports ---------------------------------------------------------------------------
     def find_supports(self, x, y, z, params: Optional[L.SupportParams] = None) -> List[SupportResult]:
         x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))

@@ -1,0 +1,268 @@
+// primitives.hip -- the device side of the normal-based primitive services:
+// the axis "height" post-processing that cylinder_segmentation_srv.cpp:129-189 and
+// cone_segmentation_srv.cpp:129-189 run on the cloud once PCL has fitted the model:
+//
+//   1. the axis direction c[3..5] / |c[3..5]|, two axis points A1 = c - d, A2 = c + d (:53-79);
+//   2. every point P projected on the axis: A1 + G (A2 - A1), G = dot(P - A1, A1A2) / dot(A1A2, A1A2)
+//      (:141-154);
+//   3. the pair (i > j) of projected points farthest apart -- float distance
+//      sqrt((dx dx + dy dy) + dz dz), the first maximum in the reference's (i, j) loop order
+//      (:156-171, O(n^2));
+//   4. the centroid: cylinder, the midpoint of that pair (:173-176); cone, c + 3/4 height d (:173-176).
+//
+// Every float operation is the reference's, in source order, without FMA (restated in
+// oracle/pitt_oracle.cpp: orc_axis_height).  Step 3 is exact without a square root per pair: sqrt is
+// monotonic, so the height is sqrt(max s) over the pairs' squared sums s, and the pairs whose distance
+// equals it are those with s >= s_lo, the smallest float whose sqrt rounds to the height.  Two passes
+// over the pairs: the maximum s (an order-free float max), then the first pair (minimum i n + j) at
+// or above s_lo.
+//
+// Kernels (one 256-point i tile x one 256-point j tile per block, j tile <= i tile, the j tile staged
+// in LDS and read by broadcast ds_read_b128; per pair 3 v_sub + 3 v_mul + 2 v_add + 1 v_max):
+//   k_axis_project   12 B read + 12 B written per point                 HBM
+//   k_pair_max       9 VALU ops per pair, one atomic per block           VALU (n^2 / 2 pairs)
+//   k_pair_first     the first pair at or above s_lo, only in the tile pairs whose maximum (kept
+//                    by k_pair_max) reaches it                           a few tiles
+//   k_axis_final     height, indices, centroid (one thread)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "ctx.hpp"
+#include "device_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pitt {
+
+struct AxisGeo {
+    float c[3], d[3];  // the model's axis point and the normalised direction
+    float a1[3], u[3];  // A1 and A1A2
+    float gdiv;
+};
+
+constexpr int kPairTile = 256;
+
+__global__ __launch_bounds__(256) void k_axis_project(const float* __restrict__ X, const float* __restrict__ Y,
+                                                      const float* __restrict__ Z, int64_t n, AxisGeo G,
+                                                      float* __restrict__ qx, float* __restrict__ qy,
+                                                      float* __restrict__ qz) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float vx = X[i] - G.a1[0], vy = Y[i] - G.a1[1], vz = Z[i] - G.a1[2];
+        const float g = (vx * G.u[0] + vy * G.u[1] + vz * G.u[2]) / G.gdiv;
+        qx[i] = G.a1[0] + g * G.u[0];
+        qy[i] = G.a1[1] + g * G.u[1];
+        qz[i] = G.a1[2] + g * G.u[2];
+    }
+}
+
+// tile pair t -> (ti, tj) with tj <= ti: t = ti (ti + 1) / 2 + tj
+__device__ __forceinline__ void pair_tile(int64_t t, int& ti, int& tj) {
+    int a = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((int64_t)(a + 1) * (a + 2) / 2 <= t) ++a;
+    while ((int64_t)a * (a + 1) / 2 > t) --a;
+    ti = a;
+    tj = (int)(t - (int64_t)a * (a + 1) / 2);
+}
+
+// the reference's squared sum for points i and j: (dx dx + dy dy) + dz dz, d = p_i - p_j
+__device__ __forceinline__ float pair_s(float xi, float yi, float zi, float xj, float yj, float zj) {
+    const float ex = xi - xj, ey = yi - yj, ez = zi - zj;
+    return ex * ex + ey * ey + ez * ez;
+}
+
+__device__ __forceinline__ float vmaxf(float a, float b) {  // IEEE max: a NaN operand never wins
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(kPairTile) void k_pair_scan(const float* __restrict__ qx, const float* __restrict__ qy,
+                                                         const float* __restrict__ qz, int64_t n,
+                                                         const float* __restrict__ s_lo_p,
+                                                         uint32_t* __restrict__ smax_bits,
+                                                         unsigned long long* __restrict__ first,
+                                                         float* __restrict__ tile_max) {
+    __shared__ float4 jq[kPairTile];  // the j tile, one broadcast ds_read_b128 per pair
+    // the second pass scans only the tile pairs whose largest s reaches the height
+    if (FIRST && !(tile_max[blockIdx.x] >= *s_lo_p)) return;
+    __shared__ float red[kPairTile / 64];
+    __shared__ unsigned long long redk[kPairTile / 64];
+    int ti, tj;
+    pair_tile(blockIdx.x, ti, tj);
+    const int64_t j0 = (int64_t)tj * kPairTile;
+    const int t = threadIdx.x;
+    if (j0 + t < n) jq[t] = make_float4(qx[j0 + t], qy[j0 + t], qz[j0 + t], 0.0f);
+    __syncthreads();
+    const int64_t i = (int64_t)ti * kPairTile + t;
+    const int jn = (int)std::min<int64_t>(kPairTile, std::min<int64_t>(n - j0, i - j0));  // j < i, j < n
+    float best = -1.0f;  // the largest s (s >= +0; NaN sums never win)
+    unsigned long long key = ~0ull;
+    if (i < n && jn > 0) {
+        const float xi = qx[i], yi = qy[i], zi = qz[i];
+        if constexpr (!FIRST) {
+            if (jn == kPairTile) {  // off-diagonal tiles: a constant trip count, unrolled
+#pragma unroll 16
+                for (int j = 0; j < kPairTile; ++j) {
+                    const float4 q = jq[j];
+                    best = vmaxf(best, pair_s(xi, yi, zi, q.x, q.y, q.z));
+                }
+            } else {
+                for (int j = 0; j < jn; ++j) {
+                    const float4 q = jq[j];
+                    best = vmaxf(best, pair_s(xi, yi, zi, q.x, q.y, q.z));
+                }
+            }
+        } else {
+            const float s_lo = *s_lo_p;
+            for (int j = 0; j < jn; ++j) {
+                const float4 q = jq[j];
+                if (pair_s(xi, yi, zi, q.x, q.y, q.z) >= s_lo) {  // the first j of this i at the height
+                    key = (unsigned long long)i * (unsigned long long)n + (unsigned long long)(j0 + j);
+                    break;
+                }
+            }
+        }
+    }
+    const int lane = t & 63, w = t >> 6;
+    if constexpr (!FIRST) {
+        for (int off = 32; off > 0; off >>= 1) best = vmaxf(best, __shfl_xor(best, off, 64));
+        if (lane == 0) red[w] = best;
+        __syncthreads();
+        if (t == 0) {
+            float m = red[0];
+            for (int k = 1; k < kPairTile / 64; ++k) m = vmaxf(m, red[k]);
+            tile_max[blockIdx.x] = m;
+            if (m >= 0.0f) atomicMax(smax_bits, __float_as_uint(m) + 1u);  // 0 = no pair
+        }
+    } else {
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(key, off, 64);
+            key = o < key ? o : key;
+        }
+        if (lane == 0) redk[w] = key;
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long m = redk[0];
+            for (int k = 1; k < kPairTile / 64; ++k) m = redk[k] < m ? redk[k] : m;
+            if (m != ~0ull) atomicMin(first, m);
+        }
+    }
+}
+
+// AxisOut: height, idx1, idx2, centroid[3]
+struct AxisOut {
+    float height;
+    int32_t idx1, idx2;
+    float centroid[3];
+};
+
+__global__ void k_axis_final(const float* __restrict__ qx, const float* __restrict__ qy, const float* __restrict__ qz,
+                             int64_t n, AxisGeo G, int mode, const uint32_t* __restrict__ smax_bits, const unsigned long long* __restrict__ first,
+                             AxisOut* __restrict__ out) {
+    AxisOut o;
+    o.height = -1.0f;
+    o.idx1 = o.idx2 = -1;
+    if (*smax_bits) {
+        o.height = sqrtf(__uint_as_float(*smax_bits - 1u));
+        const unsigned long long k = *first;
+        o.idx1 = (int32_t)(k / (unsigned long long)n);
+        o.idx2 = (int32_t)(k % (unsigned long long)n);
+    }
+    if (mode == PITT_AXIS_CYLINDER) {
+        const float nan = __builtin_nanf("");
+        const bool ok = o.idx1 >= 0;
+        o.centroid[0] = ok ? (qx[o.idx1] + qx[o.idx2]) / 2 : nan;
+        o.centroid[1] = ok ? (qy[o.idx1] + qy[o.idx2]) / 2 : nan;
+        o.centroid[2] = ok ? (qz[o.idx1] + qz[o.idx2]) / 2 : nan;
+    } else {
+        o.centroid[0] = G.c[0] + 3.0f / 4.0f * o.height * G.d[0];
+        o.centroid[1] = G.c[1] + 3.0f / 4.0f * o.height * G.d[1];
+        o.centroid[2] = G.c[2] + 3.0f / 4.0f * o.height * G.d[2];
+    }
+    *out = o;
+}
+
+}  // namespace pitt
+
+extern "C" int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                const float coef[6], int32_t mode, float* px, float* py, float* pz, float* height,
+                                int32_t* idx1, int32_t* idx2, float centroid[3]) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (n < 0 || !coef || !height || !idx1 || !idx2 || !centroid || (n > 0 && (!x || !y || !z)))
+        return ctx->fail(PITT_E_INVALID, "null argument");
+    if (mode != PITT_AXIS_CYLINDER && mode != PITT_AXIS_CONE) return ctx->fail(PITT_E_INVALID, "mode");
+    if ((px || py || pz) && !(px && py && pz)) return ctx->fail(PITT_E_INVALID, "px / py / pz: all or none");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    hipStream_t s = ctx->stream;
+    // the axis geometry, host float arithmetic in the reference's order (scalar set-up, :53-79, :143-144)
+    AxisGeo G;
+    const float norm = std::sqrt(coef[3] * coef[3] + coef[4] * coef[4] + coef[5] * coef[5]);
+    for (int k = 0; k < 3; ++k) {
+        G.c[k] = coef[k];
+        G.d[k] = coef[3 + k] / norm;
+        G.a1[k] = coef[k] + G.d[k] * -1.0f;
+    }
+    for (int k = 0; k < 3; ++k) G.u[k] = (coef[k] + G.d[k] * 1.0f) - G.a1[k];
+    G.gdiv = G.u[0] * G.u[0] + G.u[1] * G.u[1] + G.u[2] * G.u[2];
+    const size_t nb = (size_t)std::max<int64_t>(n, 1) * 4;
+    float* qx = px ? px : (float*)ctx->buf("ax_qx", nb);
+    float* qy = py ? py : (float*)ctx->buf("ax_qy", nb);
+    float* qz = pz ? pz : (float*)ctx->buf("ax_qz", nb);
+    uint32_t* w = (uint32_t*)ctx->buf("ax_work", 64);  // [0] s max bits + 1 (0: no pair), [2] s_lo, [4..5] first
+    AxisOut* hout = (AxisOut*)ctx->pinned("ax_out", sizeof(AxisOut) + 16);
+    if (!qx || !qy || !qz || !w || !hout) return ctx->fail(PITT_E_NOMEM, "axis height scratch");
+    unsigned long long* first = (unsigned long long*)(w + 4);
+    AxisOut* dout = (AxisOut*)(w + 8);
+    PITT_HIP_TRY(hipMemsetAsync(w, 0, 16, s));
+    PITT_HIP_TRY(hipMemsetAsync(first, 0xff, 8, s));
+    if (n > 0) {
+        int rec = ctx->prof_begin("k_axis_project", (double)n * 24.0);
+        const int g = (int)std::min<int64_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_axis_project, dim3(g), dim3(256), 0, s, x, y, z, n, G, qx, qy, qz);
+        ctx->prof_end(rec);
+        const int64_t tiles = (n + kPairTile - 1) / kPairTile;
+        const int64_t tp = tiles * (tiles + 1) / 2;
+        if (tp > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "axis height: too many point tiles");
+        float* tmax = (float*)ctx->buf("ax_tile_max", (size_t)tp * 4);
+        if (!tmax) return ctx->fail(PITT_E_NOMEM, "axis height tile maxima");
+        rec = ctx->prof_begin("k_pair_max", (double)n * (double)(n - 1) / 2.0);
+        hipLaunchKernelGGL(k_pair_scan<false>, dim3((unsigned)tp), dim3(kPairTile), 0, s, qx, qy, qz, n,
+                           (const float*)nullptr, w, first, tmax);
+        ctx->prof_end(rec);
+        PITT_HIP_TRY(hipGetLastError());
+        uint32_t* hw = (uint32_t*)ctx->pinned("ax_w", 16);
+        if (!hw) return ctx->fail(PITT_E_NOMEM, "axis height pinned");
+        PITT_HIP_TRY(hipMemcpyAsync(hw, w, 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        if (hw[0]) {
+            // s_lo: the smallest float whose (correctly rounded) sqrt is the height
+            const float smax = __builtin_bit_cast(float, hw[0] - 1u);
+            const float hgt = std::sqrt(smax);
+            float lo = smax;
+            while (lo > 0.0f && std::sqrt(std::nextafter(lo, 0.0f)) == hgt) lo = std::nextafter(lo, 0.0f);
+            float* hs = (float*)ctx->pinned("ax_slo", 16);
+            if (!hs) return ctx->fail(PITT_E_NOMEM, "axis height pinned");
+            *hs = lo;
+            PITT_HIP_TRY(hipMemcpyAsync(w + 2, hs, 4, hipMemcpyHostToDevice, s));
+            rec = ctx->prof_begin("k_pair_first", (double)n * (double)(n - 1) / 2.0);
+            hipLaunchKernelGGL(k_pair_scan<true>, dim3((unsigned)tp), dim3(kPairTile), 0, s, qx, qy, qz, n,
+                               (const float*)(w + 2), w, first, tmax);
+            ctx->prof_end(rec);
+            PITT_HIP_TRY(hipGetLastError());
+        }
+    }
+    hipLaunchKernelGGL(k_axis_final, dim3(1), dim3(1), 0, s, qx, qy, qz, n, G, (int)mode, w, first, dout);
+    PITT_HIP_TRY(hipGetLastError());
+    PITT_HIP_TRY(hipMemcpyAsync(hout, dout, sizeof(AxisOut), hipMemcpyDeviceToHost, s));
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    *height = hout->height;
+    *idx1 = hout->idx1;
+    *idx2 = hout->idx2;
+    for (int k = 0; k < 3; ++k) centroid[k] = hout->centroid[k];
+    return PITT_OK;
+}

@@ -276,3 +276,23 @@ def sort_pairs(keys, vals, depth_limit=None):
     else:
         O.orc_introsort_pairs(k.ctypes.data, v.ctypes.data, len(k), depth_limit)
     return k, v
+
+
+O.orc_axis_height.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32] + \
+    [ctypes.c_void_p] * 7
+O.orc_axis_height.restype = None
+
+
+def axis_height(x, y, z, coef, mode=0):
+    """The cylinder (mode 0) / cone (mode 1) height post-processing restated
+    (cylinder_segmentation_srv.cpp:129-189): (height, idx1, idx2, centroid[3], projected Nx3)."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    c = np.ascontiguousarray(np.asarray(coef, np.float32)[:6])
+    p = np.empty((3, max(n, 1)), np.float32)
+    h = ctypes.c_float()
+    i1, i2 = ctypes.c_int32(), ctypes.c_int32()
+    cen = np.zeros(3, np.float32)
+    O.orc_axis_height(_fp(x), _fp(y), _fp(z), n, _fp(c), mode, _fp(p[0]), _fp(p[1]), _fp(p[2]), ctypes.byref(h),
+                      ctypes.byref(i1), ctypes.byref(i2), _fp(cen))
+    return h.value, i1.value, i2.value, cen, p[:, :n].T.copy()

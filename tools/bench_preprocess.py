@@ -113,6 +113,33 @@ def main():
             if launches:
                 nrm["kernels"][kname] = {"avg_us": round(ms / launches * 1e3, 1)}
         ctx.profile(False)
+        # cylinder / cone post-processing: the O(n^2) axis "height" search on object-sized clusters
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_axis_height import cylinder_cloud
+        axis = {}
+        for na in (5000, 50000):
+            pa, coef = cylinder_cloud(na, na)
+            ta = [torch.from_numpy(np.ascontiguousarray(pa[:, k])).cuda() for k in range(3)]
+            ctx.axis_height(*ta, coef)
+            torch.cuda.synchronize()
+            ctx.profile(True)
+            ctx.profile_reset()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                ctx.axis_height(*ta, coef)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) * 1e3 / 5
+            pairs = na * (na - 1) / 2
+            e = {"ms_per_call_wall": round(wall, 3), "pairs": pairs, "kernels": {}}
+            for kname in ("k_axis_project", "k_pair_max", "k_pair_first"):
+                launches, ms, algo = ctx.profile_get(kname)
+                if launches:
+                    us = ms / launches * 1e3
+                    e["kernels"][kname] = {"avg_us": round(us, 1)}
+                    if kname == "k_pair_max":  # 8 VALU ops per pair (3 sub, 3 mul, 2 add; + 1 max) vs 78.6 Tops/s
+                        e["kernels"][kname]["valu_frac"] = round(pairs * 8 / (us * 1e-6) / 78.6e12, 3)
+            ctx.profile(False)
+            axis[str(na)] = e
     import oracle_binding as orc
     t0 = time.perf_counter()
     k = 0
@@ -130,9 +157,14 @@ def main():
     t0 = time.perf_counter()
     orc.normal_estimation(*v0.T)
     nrm["cpu_oracle_ms_per_frame_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
+    pa, coef = cylinder_cloud(5000, 5000)
+    t0 = time.perf_counter()
+    orc.axis_height(*pa.T, coef)
+    axis["5000"]["cpu_oracle_ms_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
                                   f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
                       "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox, "normal_estimation": nrm,
+                      "axis_height": axis,
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
 
