@@ -24,6 +24,7 @@
  *        src/point_cloud_library/pc_manager.cpp:55-67, src/obj_segmentation.cpp:238
  *   pitt_normal_estimation        replaces  NormalEstimation<PointXYZ, Normal>::compute (estimateNormal)
  *        src/point_cloud_library/pc_manager.cpp:68-78
+ *   pitt_sphere_segment           replaces  seg.segment in src/segmentation_services/sphere_segmentation_srv.cpp:57-73
  *   pitt_axis_height              replaces  the projection + O(n^2) height loop after seg.segment in
  *        src/segmentation_services/cylinder_segmentation_srv.cpp:129-189 and
  *        src/segmentation_services/cone_segmentation_srv.cpp:129-189
@@ -269,6 +270,27 @@ int pitt_sort_pairs(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int3
 int pitt_normal_estimation(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                            int32_t k, const float viewpoint[3], float* nx, float* ny, float* nz,
                            float* curvature, int32_t* neighbours, int32_t* neighbour_count);
+
+/* The sphere service's seg.segment (sphere_segmentation_srv.cpp:57-73): SACSegmentationFromNormals with
+ * SACMODEL_SPHERE falls through to the plain SampleConsensusModelSphere (normals unused).  RANSAC over
+ * 4-point samples (A2 sampler, seed), Eigen 3.2's 4 x 4 determinants in float, the radius limits
+ * (-DBL_MAX / DBL_MAX = unset; a model outside them counts 0 inliers), PCL's computeModel loop with
+ * w^4; optimize: more than 4 inliers refine the centre and radius by least squares of ||p - c|| - r
+ * (PCL: Eigen's float Levenberg-Marquardt -- equal within its tolerance, not bit for bit), then the
+ * final selectWithinDistance.  x/y/z device SoA; inliers (device, capacity n) ascending.
+ * Returns PITT_OK with a model (coef = centre x, y, z, radius), PITT_NO_MODEL without. */
+typedef struct {
+    double   threshold;       /* 0.007 (sphere_segmentation_srv.cpp:20) */
+    int32_t  max_iterations;  /* 1000 (:23) */
+    int32_t  optimize;        /* 1 (:61) */
+    double   probability;     /* 0.99 (PCL default) */
+    double   radius_min, radius_max;  /* 0.005, 0.5 (:21-22) */
+    uint32_t seed;            /* 12345 (PCL's SampleConsensusModel) */
+    int32_t  pad;
+} pitt_sphere_params;
+int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                        const pitt_sphere_params* params, int32_t* inliers, int64_t* n_inliers, float coef[4],
+                        int32_t* hypotheses);
 
 /* The post-processing of the cylinder and cone services once PCL has fitted the model
  * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).

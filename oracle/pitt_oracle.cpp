@@ -1137,4 +1137,213 @@ void orc_axis_height(const float* x, const float* y, const float* z, int64_t n, 
     if (px)
         for (int64_t i = 0; i < n; ++i) px[i] = qx[(size_t)i], py[i] = qy[(size_t)i], pz[i] = qz[(size_t)i];
 }
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Sphere (PCL 1.7 sample_consensus/impl/sac_model_sphere.hpp; the RANSAC loop as segment() above).
+namespace {
+// Eigen 3.2 determinant_impl<4>: Costabel's 30-multiplication expansion, terms left to right.
+inline float det4_helper(const float m[16], int j, int k, int a, int b) {
+    return (m[j * 4 + 0] * m[k * 4 + 1] - m[k * 4 + 0] * m[j * 4 + 1]) *
+           (m[a * 4 + 2] * m[b * 4 + 3] - m[b * 4 + 2] * m[a * 4 + 3]);
+}
+inline float det4(const float m[16]) {
+    return det4_helper(m, 0, 1, 2, 3) - det4_helper(m, 0, 2, 1, 3) + det4_helper(m, 0, 3, 1, 2) +
+           det4_helper(m, 1, 2, 0, 3) - det4_helper(m, 1, 3, 0, 2) + det4_helper(m, 2, 3, 0, 1);
+}
+
+// computeModelCoefficients: Cramer's rule on the 4 x 4 system, temp's columns permuted in place.
+bool sphere_from4(const float px[4], const float py[4], const float pz[4], float c[4]) {
+    float t[16];
+    for (int i = 0; i < 4; ++i) t[i * 4 + 0] = px[i], t[i * 4 + 1] = py[i], t[i * 4 + 2] = pz[i], t[i * 4 + 3] = 1;
+    const float m11 = det4(t);
+    if (m11 == 0) return false;  // the points don't define a sphere
+    for (int i = 0; i < 4; ++i) t[i * 4 + 0] = px[i] * px[i] + py[i] * py[i] + pz[i] * pz[i];
+    const float m12 = det4(t);
+    for (int i = 0; i < 4; ++i) t[i * 4 + 1] = t[i * 4 + 0], t[i * 4 + 0] = px[i];
+    const float m13 = det4(t);
+    for (int i = 0; i < 4; ++i) t[i * 4 + 2] = t[i * 4 + 1], t[i * 4 + 1] = py[i];
+    const float m14 = det4(t);
+    for (int i = 0; i < 4; ++i)
+        t[i * 4 + 0] = t[i * 4 + 2], t[i * 4 + 1] = px[i], t[i * 4 + 2] = py[i], t[i * 4 + 3] = pz[i];
+    const float m15 = det4(t);
+    c[0] = 0.5f * m12 / m11;
+    c[1] = 0.5f * m13 / m11;
+    c[2] = 0.5f * m14 / m11;
+    c[3] = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] - m15 / m11);
+    return true;
+}
+
+// isModelValid: the radius limits (set by setRadiusLimits; -DBL_MAX / DBL_MAX = unset)
+bool sphere_valid(const float c[4], double rmin, double rmax) {
+    if (rmin != -DBL_MAX && c[3] < rmin) return false;
+    if (rmax != DBL_MAX && c[3] > rmax) return false;
+    return true;
+}
+
+// |sqrtf((x - c0)^2 + (y - c1)^2 + (z - c2)^2) - c3| < threshold (float promoted to double, A4)
+inline bool sphere_in(const Cloud& c, int64_t i, const float m[4], double th) {
+    const float dx = c.x[i] - m[0], dy = c.y[i] - m[1], dz = c.z[i] - m[2];
+    return std::fabs(std::sqrt(dx * dx + dy * dy + dz * dz) - m[3]) < th;
+}
+
+// Levenberg-Marquardt in double over the inliers' residuals ||p - c|| - r (the same iteration the
+// library's host loop runs on device sums, pitt_sphere_segment).
+void sphere_refine(const Cloud& c, const std::vector<int>& inl, const float in[4], float out[4]) {
+    double x[4] = {in[0], in[1], in[2], in[3]};
+    auto sums = [&](const double* v, double* jtj, double* jtr, double* cost) {
+        for (int i = 0; i < 10; ++i) jtj[i] = 0;
+        for (int i = 0; i < 4; ++i) jtr[i] = 0;
+        *cost = 0;
+        for (int id : inl) {
+            const double dx = (double)c.x[id] - v[0], dy = (double)c.y[id] - v[1], dz = (double)c.z[id] - v[2];
+            const double d = std::sqrt(dx * dx + dy * dy + dz * dz);
+            const double r = d - v[3];
+            const double j[4] = {d > 0 ? -dx / d : 0.0, d > 0 ? -dy / d : 0.0, d > 0 ? -dz / d : 0.0, -1.0};
+            int q = 0;
+            for (int a = 0; a < 4; ++a)
+                for (int b = a; b < 4; ++b) jtj[q++] += j[a] * j[b];
+            for (int a = 0; a < 4; ++a) jtr[a] += j[a] * r;
+            *cost += r * r;
+        }
+    };
+    double jtj[10], jtr[4], cost;
+    sums(x, jtj, jtr, &cost);
+    double lambda = 1e-3;
+    for (int it = 0; it < 100; ++it) {
+        bool moved = false;
+        double step = 0;
+        while (lambda < 1e10) {
+            double A[4][5];
+            int q = 0;
+            for (int a = 0; a < 4; ++a)
+                for (int b = a; b < 4; ++b) A[a][b] = A[b][a] = jtj[q++];
+            for (int a = 0; a < 4; ++a) A[a][a] += lambda * A[a][a], A[a][4] = -jtr[a];
+            // Gaussian elimination with partial pivoting on the 4 x 4 system
+            bool ok = true;
+            for (int col = 0; col < 4 && ok; ++col) {
+                int piv = col;
+                for (int r = col + 1; r < 4; ++r)
+                    if (std::fabs(A[r][col]) > std::fabs(A[piv][col])) piv = r;
+                if (A[piv][col] == 0) { ok = false; break; }
+                if (piv != col)
+                    for (int k = 0; k < 5; ++k) std::swap(A[col][k], A[piv][k]);
+                for (int r = col + 1; r < 4; ++r) {
+                    const double f = A[r][col] / A[col][col];
+                    for (int k = col; k < 5; ++k) A[r][k] -= f * A[col][k];
+                }
+            }
+            if (!ok) break;
+            double dlt[4];
+            for (int r = 3; r >= 0; --r) {
+                double acc = A[r][4];
+                for (int k = r + 1; k < 4; ++k) acc -= A[r][k] * dlt[k];
+                dlt[r] = acc / A[r][r];
+            }
+            double xn[4], jn[10], rn[4], cn;
+            for (int a = 0; a < 4; ++a) xn[a] = x[a] + dlt[a];
+            sums(xn, jn, rn, &cn);
+            if (cn < cost) {
+                step = 0;
+                double nx = 0;
+                for (int a = 0; a < 4; ++a) step += dlt[a] * dlt[a], nx += xn[a] * xn[a];
+                step = std::sqrt(step / (nx + 1e-300));
+                for (int a = 0; a < 4; ++a) x[a] = xn[a];
+                std::memcpy(jtj, jn, sizeof jtj);
+                std::memcpy(jtr, rn, sizeof jtr);
+                cost = cn;
+                lambda *= 0.1;
+                moved = true;
+                break;
+            }
+            lambda *= 10;
+        }
+        if (!moved || step < 1e-12) break;
+    }
+    for (int a = 0; a < 4; ++a) out[a] = (float)x[a];
+}
+}  // namespace
+
+extern "C" {
+int orc_sphere_from4(const float xyz[12], float coef[4]) {
+    const float px[4] = {xyz[0], xyz[3], xyz[6], xyz[9]}, py[4] = {xyz[1], xyz[4], xyz[7], xyz[10]},
+                pz[4] = {xyz[2], xyz[5], xyz[8], xyz[11]};
+    return sphere_from4(px, py, pz, coef) ? 1 : 0;
+}
+
+int orc_sphere_segment(const float* x, const float* y, const float* z, int64_t n, const orc_sphere_params* p,
+                       int32_t* inliers, int64_t* n_inliers, float coef[4], float best_out[4], int32_t* hypotheses,
+                       int32_t* counts, int32_t counts_cap, int32_t* n_counts) {
+    Cloud c{x, y, z, n};
+    *n_inliers = 0;
+    *hypotheses = 0;
+    if (n_counts) *n_counts = 0;
+    if (n < 4) return 0;  // getSamples: "Can not select 4 unique points"
+    std::mt19937 mt(p->seed);
+    std::vector<int> sh((size_t)n);
+    std::iota(sh.begin(), sh.end(), 0);
+    int iterations = 0, n_best = -std::numeric_limits<int>::max();
+    double k = 1.0;
+    const double log_probability = std::log(1.0 - p->probability);
+    const double one_over_indices = 1.0 / (double)n;
+    unsigned skipped = 0;
+    const unsigned max_skip = (unsigned)p->max_iterations * 10u;
+    bool have = false;
+    float best[4] = {0, 0, 0, 0};
+    int nc = 0;
+    while (iterations < k && skipped < max_skip) {
+        // getSamples: SampleConsensusModelSphere::isSampleGood accepts every sample
+        for (unsigned i = 0; i < 4; ++i)
+            std::swap(sh[i], sh[i + ((size_t)(mt() >> 1) % ((size_t)n - i))]);
+        const float px[4] = {x[sh[0]], x[sh[1]], x[sh[2]], x[sh[3]]}, py[4] = {y[sh[0]], y[sh[1]], y[sh[2]], y[sh[3]]},
+                    pz[4] = {z[sh[0]], z[sh[1]], z[sh[2]], z[sh[3]]};
+        float m[4];
+        if (!sphere_from4(px, py, pz, m)) {
+            ++skipped;
+            continue;
+        }
+        int n_in = 0;
+        if (sphere_valid(m, p->radius_min, p->radius_max))  // countWithinDistance: 0 for an invalid model
+            for (int64_t i = 0; i < n; ++i) n_in += sphere_in(c, i, m, p->threshold);
+        if (counts && nc < counts_cap) counts[nc] = n_in;
+        ++nc;
+        if (n_in > n_best) {
+            n_best = n_in;
+            have = true;
+            std::memcpy(best, m, sizeof m);
+            const double w = (double)n_best * one_over_indices;
+            double p_no = 1.0 - std::pow(w, 4.0);
+            p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
+            p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
+            k = log_probability / std::log(p_no);
+        }
+        ++iterations;
+        if (iterations > p->max_iterations) break;
+    }
+    *hypotheses = iterations;
+    if (n_counts) *n_counts = nc;
+    if (!have) return 0;
+    std::memcpy(best_out, best, sizeof best);
+    std::vector<int> inl;
+    auto select = [&](const float* m) {
+        inl.clear();
+        if (!sphere_valid(m, p->radius_min, p->radius_max)) return;  // selectWithinDistance: none
+        for (int64_t i = 0; i < n; ++i)
+            if (sphere_in(c, i, m, p->threshold)) inl.push_back((int)i);
+    };
+    select(best);
+    float out[4];
+    std::memcpy(out, best, sizeof out);
+    if (p->optimize && inl.size() > 4) {  // optimizeModelCoefficients needs more than 4 inliers
+        sphere_refine(c, inl, best, out);
+        select(out);
+    } else if (p->optimize) {
+        select(out);
+    }
+    std::memcpy(coef, out, sizeof out);
+    for (size_t i = 0; i < inl.size(); ++i) inliers[i] = inl[i];
+    *n_inliers = (int64_t)inl.size();
+    return 1;
+}
 }  // extern "C"

@@ -131,6 +131,25 @@ int     orc_normal_estimation(const float* x, const float* y, const float* z, in
 void    orc_std_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
 void    orc_partial_sort_pairs(uint32_t* key, uint32_t* val, int64_t n);
 void    orc_introsort_pairs(uint32_t* key, uint32_t* val, int64_t n, int32_t depth_limit);
+// The sphere service (sphere_segmentation_srv.cpp:57-73): SACSegmentationFromNormals with SACMODEL_SPHERE
+// falls through to the plain SampleConsensusModelSphere (normals unused), RANSAC, radius limits,
+// optimize.  RANSAC bit-exact restatement; the refinement is a double Levenberg-Marquardt to the
+// least-squares optimum (PCL: Eigen's float LM with numerical differences -- matched within tolerance).
+typedef struct {
+    double  threshold;
+    int32_t max_iterations;
+    int32_t optimize;
+    double  probability;
+    double  radius_min, radius_max;
+    uint32_t seed;
+    int32_t pad;
+} orc_sphere_params;
+// returns 1 with a model, 0 without; inliers (cap n) ascending; counts (cap counts_cap) per hypothesis
+int     orc_sphere_segment(const float* x, const float* y, const float* z, int64_t n, const orc_sphere_params* p,
+                           int32_t* inliers, int64_t* n_inliers, float coef[4], float best[4],
+                           int32_t* hypotheses, int32_t* counts, int32_t counts_cap, int32_t* n_counts);
+// SampleConsensusModelSphere::computeModelCoefficients on 4 points (xyz[4][3]); returns 0 when m11 == 0
+int     orc_sphere_from4(const float xyz[12], float coef[4]);
 // The axis "height" post-processing of the cylinder / cone services (cylinder_segmentation_srv.cpp:129-189,
 // cone_segmentation_srv.cpp:129-189): every point projected on the axis of coef[0..5], the pair (i > j)
 // of projected points farthest apart (first maximum in loop order), and the centroid (mode 0 cylinder:

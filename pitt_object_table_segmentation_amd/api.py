@@ -358,6 +358,25 @@ class Context:
         self._check(lib.pitt_sort_pairs(self.h, key.data_ptr(), val.data_ptr(), key.numel(), int(depth_limit)),
                     "pitt_sort_pairs")
 
+    def sphere_segment(self, x, y, z, threshold: float = 0.007, max_iterations: int = 1000, optimize: bool = True,
+                       radius_min: float = 0.005, radius_max: float = 0.5, probability: float = 0.99,
+                       seed: int = 12345):
+        """The sphere service's seg.segment (sphere_segmentation_srv.cpp:57-73; defaults :19-27) on device
+        tensors: (inliers device int32, coefficients [cx, cy, cz, r] or None, hypotheses)."""
+        import torch
+        n = x.numel()
+        prm = L.SphereParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max, seed, 0)
+        inl = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
+        ni = ctypes.c_int64()
+        coef = np.zeros(4, np.float32)
+        hyp = ctypes.c_int32()
+        rc = lib.pitt_sphere_segment(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), n, ctypes.byref(prm),
+                                     inl.data_ptr(), ctypes.byref(ni), _fp(coef), ctypes.byref(hyp))
+        if rc == L.PITT_NO_MODEL:
+            return inl[:0], None, hyp.value
+        self._check(rc, "pitt_sphere_segment")
+        return inl[:ni.value], coef, hyp.value
+
     def axis_height(self, x, y, z, coefficients, mode: int = L.PITT_AXIS_CYLINDER, projected: bool = False):
         """The cylinder / cone services' post-processing (cylinder_segmentation_srv.cpp:129-189,
         cone_segmentation_srv.cpp:129-189) on device tensors: (height, idx1, idx2, centroid[3])

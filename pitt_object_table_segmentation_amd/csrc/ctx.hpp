@@ -53,7 +53,7 @@ struct pitt_ctx {
     std::unordered_map<std::string, std::pair<void*, size_t>> host_pinned;
 
     // sampler tables (host) keyed by (n, seed, attempts)
-    std::map<std::tuple<int64_t, uint32_t, int64_t>, std::vector<int32_t>> tables;
+    std::map<std::tuple<int64_t, uint32_t, int64_t, int>, std::vector<int32_t>> tables;
     // device pool of the last batch's tables
     std::vector<std::tuple<int64_t, uint32_t, int64_t>> pool_keys;
 
@@ -112,7 +112,8 @@ struct pitt_ctx {
 
 namespace pitt {
 // Host sampler table (A2): attempts*3 indices of drawIndexSample for n points.
-const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts);
+// (k = 4: the sphere model's samples)
+const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts, int k = 3);
 // Smallest float t with (double)|d| < th  <=>  |d| < t for every float d (A4).
 float float_threshold(double th);
 }  // namespace pitt

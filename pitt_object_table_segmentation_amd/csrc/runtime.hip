@@ -20,11 +20,11 @@ int finish_batch(pitt_ctx* ctx);
 // A2: drawIndexSample's index triples for a cloud of n points.  The shuffled index vector of
 // SampleConsensusModel is the identity except at the positions the swaps touched, so it is kept
 // sparsely: O(attempts) instead of the O(n) array PCL rebuilds on every segment().
-const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts) {
-    auto key = std::make_tuple(n, seed, attempts);
+const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t seed, int64_t attempts, int k) {
+    auto key = std::make_tuple(n, seed, attempts, k);
     auto it = ctx->tables.find(key);
     if (it != ctx->tables.end()) return it->second;
-    std::vector<int32_t> t((size_t)attempts * 3);
+    std::vector<int32_t> t((size_t)attempts * k);
     std::mt19937 mt(seed);  // boost::mt19937 and std::mt19937 produce the same stream
     std::unordered_map<int64_t, int64_t> sh;
     sh.reserve((size_t)attempts * 4);
@@ -33,16 +33,14 @@ const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t see
         return f == sh.end() ? i : f->second;
     };
     for (int64_t a = 0; a < attempts; ++a) {
-        for (int64_t i = 0; i < 3; ++i) {
+        for (int64_t i = 0; i < k; ++i) {
             const uint32_t r = (uint32_t)mt() >> 1;           // uniform_int<>(0, INT_MAX)
             const int64_t j = i + (int64_t)((uint64_t)r % (uint64_t)(n - i));
             const int64_t vi = get(i), vj = get(j);
             sh[i] = vj;
             sh[j] = vi;
         }
-        t[(size_t)a * 3 + 0] = (int32_t)get(0);
-        t[(size_t)a * 3 + 1] = (int32_t)get(1);
-        t[(size_t)a * 3 + 2] = (int32_t)get(2);
+        for (int64_t i = 0; i < k; ++i) t[(size_t)(a * k + i)] = (int32_t)get(i);
     }
     return ctx->tables.emplace(key, std::move(t)).first->second;
 }

@@ -296,3 +296,42 @@ def axis_height(x, y, z, coef, mode=0):
     O.orc_axis_height(_fp(x), _fp(y), _fp(z), n, _fp(c), mode, _fp(p[0]), _fp(p[1]), _fp(p[2]), ctypes.byref(h),
                       ctypes.byref(i1), ctypes.byref(i2), _fp(cen))
     return h.value, i1.value, i2.value, cen, p[:, :n].T.copy()
+
+
+class SphereParams(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("radius_min", ctypes.c_double), ("radius_max", ctypes.c_double),
+                ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+
+
+def sphere_params(threshold=0.007, max_iterations=1000, optimize=True, radius_min=0.005, radius_max=0.5,
+                  probability=0.99, seed=12345):
+    """sphere_segmentation_srv.cpp:19-27 defaults (distance 0.007, 1000 iterations, radius 0.005-0.5)."""
+    return SphereParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max, seed, 0)
+
+
+O.orc_sphere_segment.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.POINTER(SphereParams)] + \
+    [ctypes.c_void_p] * 6 + [ctypes.c_int32, ctypes.c_void_p]
+O.orc_sphere_from4.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+
+
+def sphere_from4(p4):
+    c = np.zeros(4, np.float32)
+    ok = O.orc_sphere_from4(_fp(np.ascontiguousarray(p4, np.float32)), _fp(c))
+    return bool(ok), c
+
+
+def sphere_segment(x, y, z, params=None, counts_cap=20000):
+    """The sphere service's seg.segment restated: dict(ok, inliers, coef, best, hypotheses, counts)."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    n = len(x)
+    p = params or sphere_params()
+    inl = np.empty(max(n, 1), np.int32)
+    ni = ctypes.c_int64()
+    coef, best = np.zeros(4, np.float32), np.zeros(4, np.float32)
+    hyp, nc = ctypes.c_int32(), ctypes.c_int32()
+    cnt = np.zeros(counts_cap, np.int32)
+    ok = O.orc_sphere_segment(_fp(x), _fp(y), _fp(z), n, ctypes.byref(p), _ip(inl), ctypes.byref(ni), _fp(coef),
+                              _fp(best), ctypes.byref(hyp), _ip(cnt), counts_cap, ctypes.byref(nc))
+    return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value,
+            "counts": cnt[:min(nc.value, counts_cap)].copy()}
