@@ -291,6 +291,9 @@ typedef struct {
 int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                         const pitt_sphere_params* params, int32_t* inliers, int64_t* n_inliers, float coef[4],
                         int32_t* hypotheses);
+/* The same on a host PointXYZ cloud (x, y, z, pad: 16-byte stride); inliers in host memory. */
+int pitt_sphere_segment_host(pitt_ctx* ctx, const float* xyz16, int64_t n, const pitt_sphere_params* params,
+                             int32_t* inliers, int64_t* n_inliers, float coef[4], int32_t* hypotheses);
 
 /* The post-processing of the cylinder and cone services once PCL has fitted the model
  * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).

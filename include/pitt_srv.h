@@ -8,6 +8,7 @@
  *   pitt_srv_find_supports    <-> findSupports          supports_segmentation_srv.cpp:241
  *   pitt_srv_clusterize       <-> clusterize            cluster_segmentation_srv.cpp:38
  *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
+ *   pitt_srv_ransac_sphere    <-> ransacSphereDetection sphere_segmentation_srv.cpp:29
  *   pitt_srv_call_ransac_plane <-> callRansacPlaneSegmentation  ransac_segmentation.cpp:175-199
  *   pitt_srv_arbitrate        <-> clustersAcquisition's arbitration  ransac_segmentation.cpp:265-302
  * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
@@ -52,6 +53,12 @@ int pitt_srv_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int64_t 
                           int32_t* inliers_out /* cap n */, int64_t* n_inliers,
                           float* coefficients_out /* cap 4 */, int32_t* n_coefficients,
                           float centroid_out[3]);
+
+/* The sphere service: inliers (index 0 dropped, Q1), coefficients (centre, radius; none without a
+ * model), centroid_out = the centre when there are coefficients. */
+int pitt_srv_ransac_sphere(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
+                           int32_t* inliers_out /* cap n */, int64_t* n_inliers,
+                           float* coefficients_out /* cap 4 */, int32_t* n_coefficients, float centroid_out[3]);
 
 /* callRansacPlaneSegmentation, ransac_segmentation.cpp:175-199: the plane service, accepted (1) only
  * when its response holds more than 0 inliers (Q2: the min-inliers parameter is read but unused);

@@ -121,6 +121,15 @@ const std::string PARAM_NAME_PLANE_EPS_ANGLE_TH = "/pitt/srv/plane_segmentation/
 const std::string PARAM_NAME_PLANE_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_segmentation/min_opening_angle_deg";
 const std::string PARAM_NAME_PLANE_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_segmentation/max_opening_angle_deg";
 const std::string PARAM_NAME_PLANE_MIN_INLIERS = "/pitt/srv/plane_segmentation/min_inliers";
+const std::string SRV_NAME_RANSAC_SPHERE_FILTER = "sphere_segmentation_srv";
+const std::string PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/sphere_segmentation/normal_distance_weight";
+const std::string PARAM_NAME_SPHERE_DISTANCE_TH = "/pitt/srv/sphere_segmentation/distance_th";
+const std::string PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT = "/pitt/srv/sphere_segmentation/max_iter_limit";
+const std::string PARAM_NAME_SPHERE_MIN_RADIUS_LIMIT = "/pitt/srv/sphere_segmentation/min_radius_limit";
+const std::string PARAM_NAME_SPHERE_MAX_RADIUS_LIMIT = "/pitt/srv/sphere_segmentation/max_radius_limit";
+const std::string PARAM_NAME_SPHERE_EPS_ANGLE_TH = "/pitt/srv/sphere_segmentation/eps_angle_th";
+const std::string PARAM_NAME_SPHERE_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/sphere_segmentation/min_opening_angle_deg";
+const std::string PARAM_NAME_SPHERE_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/sphere_segmentation/max_opening_angle_deg";
 const std::string PARAM_NAME_MIN_ITERATIVE_CLOUD_PERCENTAGE = "/pitt/srv/supports_segmentation/min_iter_cloud_percent";
 const std::string PARAM_NAME_MIN_ITERATIVE_SUPPORT_PERCENTAGE = "/pitt/srv/supports_segmentation/min_iter_support_percent";
 const std::string PARAM_NAME_HORIZONTAL_VARIANCE_THRESHOLD = "/pitt/srv/supports_segmentation/horizontal_variance_th";
@@ -191,6 +200,9 @@ public:
     // plane_segmentation_srv.cpp:27
     bool ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
                               pitt_msgs::PrimitiveSegmentation::Response& res);
+    // sphere_segmentation_srv.cpp:29-96
+    bool ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
+                               pitt_msgs::PrimitiveSegmentation::Response& res);
     // supports_segmentation_srv.cpp:241
     bool findSupports(pitt_msgs::SupportSegmentation::Request& req, pitt_msgs::SupportSegmentation::Response& res);
     // cluster_segmentation_srv.cpp:38

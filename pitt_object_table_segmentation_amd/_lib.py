@@ -159,6 +159,7 @@ SIGNATURES = {
     "pitt_voxel_grid": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32, _vp,
                                _vp, _vp, _i64p, _i32p]),
     "pitt_sort_pairs": (_i32, [_vp, _vp, _vp, _i64, _i32]),
+    "pitt_sphere_segment_host": (_i32, [_vp, _f32p, _i64, ctypes.POINTER(SphereParams), _i32p, _i64p, _f32p, _i32p]),
     "pitt_sphere_segment": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SphereParams), _vp, _i64p, _f32p, _i32p]),
     "pitt_axis_height": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp, _f32p, _i32p, _i32p, _f32p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),
@@ -201,6 +202,7 @@ SIGNATURES.update({
     "pitt_srv_param_set_list": (_i32, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i32]),
     "pitt_srv_param_erase": (_i32, [_vp, ctypes.c_char_p]),
     "pitt_srv_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_srv_ransac_sphere": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
     "pitt_srv_call_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p]),
     "pitt_srv_arbitrate": (_i32, [_i64, _i64, _i64, _i64]),
     "pitt_srv_find_supports": (_i32, [_vp, _f32p, _i64, _i64, ctypes.POINTER(SrvSupportRequest), _i32p, _f32p]),

@@ -501,6 +501,19 @@ class Services:
                                                 ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)), "ransac_plane")
         return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
 
+    def ransac_sphere(self, cloud: np.ndarray, n_normals: Optional[int] = None):
+        """ransacSphereDetection (sphere_segmentation_srv.cpp:29-96): (ok, inliers (index 0 dropped),
+        coefficients [cx, cy, cz, r] or empty, centroid = the centre)."""
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        inl = np.empty(max(n, 1), np.int32)
+        ni, nc = ctypes.c_int64(), ctypes.c_int32()
+        co = np.zeros(4, np.float32)
+        ce = np.zeros(3, np.float32)
+        ok = self._rc(lib.pitt_srv_ransac_sphere(self.h, _fp(c), n, n if n_normals is None else n_normals, _ip(inl),
+                                                 ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)), "ransac_sphere")
+        return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
+
     def call_ransac_plane(self, cloud: np.ndarray, n_normals: Optional[int] = None):
         """callRansacPlaneSegmentation (ransac_segmentation.cpp:175-199): (accepted, inliers, coefficients)."""
         c = _cloud16(cloud)

@@ -98,6 +98,56 @@ bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation
     return true;
 }
 
+// sphere_segmentation_srv.cpp:29-96.  SACSegmentationFromNormals with SACMODEL_SPHERE falls through to
+// the plain sphere model: the normal weight, eps angle and opening angles are read but unused.
+bool SegmentationServices::ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
+                                                 pitt_msgs::PrimitiveSegmentation::Response& res) {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
+        maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
+    params_.param(srvm::PARAM_NAME_SPHERE_DISTANCE_TH, distanceThreshold, 0.007);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_SPHERE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.005);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
+    params_.param(srvm::PARAM_NAME_SPHERE_EPS_ANGLE_TH, epsAngleTh, 0.0);
+    params_.param(srvm::PARAM_NAME_SPHERE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 100.0);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 180.0);
+    (void)normalDistanceWeight; (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;
+
+    pitt_sphere_params p;
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    p.optimize = 1;
+    p.probability = 0.99;
+    p.radius_min = minRadiusLimit;
+    p.radius_max = maxRadiusLimit;
+    p.seed = 12345u;
+    p.pad = 0;
+    std::vector<int32_t> inl(req.cloud.size() + 1);
+    int64_t n_inl = 0;
+    float coef[4] = {0, 0, 0, 0};
+    int32_t n_coef = 0;
+    status_ = PITT_OK;
+    if (req.normals.size() == req.cloud.size()) {  // initSACModel: normals must match the cloud
+        status_ = pitt_sphere_segment_host(ctx_, req.cloud.data.data(), (int64_t)req.cloud.size(), &p, inl.data(),
+                                           &n_inl, coef, nullptr);
+        if (status_ == PITT_OK) n_coef = 4;
+        if (status_ != PITT_OK) n_inl = 0;  // no model: PCL clears both outputs
+        if (status_ == PITT_NO_MODEL) status_ = PITT_OK;
+    }
+    res.inliers.clear();  // inlierToVectorMsg drops index 0 (Q1)
+    for (int64_t i = 0; i < n_inl; ++i)
+        if (inl[(size_t)i] != 0) res.inliers.push_back(inl[(size_t)i]);
+    res.coefficients.assign(coef, coef + n_coef);
+    if (n_coef > 0) {  // :79-83, the centre
+        res.x_centroid = coef[0];
+        res.y_centroid = coef[1];
+        res.z_centroid = coef[2];
+    }
+    return true;
+}
+
 // supports_segmentation_srv.cpp:241-361 (+ initializeInputParameters :70-86)
 bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request& req,
                                         pitt_msgs::SupportSegmentation::Response& res) {
@@ -321,6 +371,28 @@ int pitt_srv_ransac_plane(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_
     srv.request.cloud = cloud_from(xyz16, n);
     srv.request.normals.n = (size_t)n_normals;
     bool ok = s->svc.ransacPlaneDetaction(srv.request, srv.response);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    *n_inliers = (int64_t)srv.response.inliers.size();
+    *n_coefficients = (int32_t)srv.response.coefficients.size();
+    if (inliers_out && !srv.response.inliers.empty())
+        std::memcpy(inliers_out, srv.response.inliers.data(), srv.response.inliers.size() * 4);
+    if (coefficients_out && !srv.response.coefficients.empty())
+        std::memcpy(coefficients_out, srv.response.coefficients.data(), srv.response.coefficients.size() * 4);
+    if (centroid_out) {
+        centroid_out[0] = srv.response.x_centroid;
+        centroid_out[1] = srv.response.y_centroid;
+        centroid_out[2] = srv.response.z_centroid;
+    }
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_ransac_sphere(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals, int32_t* inliers_out,
+                           int64_t* n_inliers, float* coefficients_out, int32_t* n_coefficients, float centroid_out[3]) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_inliers || !n_coefficients) return PITT_E_INVALID;
+    pitt_msgs::PrimitiveSegmentation srv;
+    srv.request.cloud = cloud_from(xyz16, n);
+    srv.request.normals.n = (size_t)n_normals;
+    bool ok = s->svc.ransacSphereDetection(srv.request, srv.response);
     if (s->svc.last_status() < 0) return s->svc.last_status();
     *n_inliers = (int64_t)srv.response.inliers.size();
     *n_coefficients = (int32_t)srv.response.coefficients.size();

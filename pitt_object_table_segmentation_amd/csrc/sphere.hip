@@ -366,3 +366,39 @@ extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y
     for (int r = 0; r < 4; ++r) coef_out[r] = out[r];
     return PITT_OK;
 }
+
+// Host-memory form (the service handlers' PointXYZ clouds, 16-byte stride): the cloud is staged into
+// the context's device SoA buffers, the inliers copied back.
+extern "C" int pitt_sphere_segment_host(pitt_ctx* ctx, const float* xyz16, int64_t n,
+                                        const pitt_sphere_params* params, int32_t* inliers, int64_t* n_inliers,
+                                        float coef[4], int32_t* hypotheses) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (n < 0 || (n > 0 && (!xyz16 || !inliers)) || !n_inliers || !coef) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    const size_t nb = (size_t)std::max<int64_t>(n, 1) * 4;
+    float* dx = (float*)ctx->buf("sph_hx", nb);
+    float* dy = (float*)ctx->buf("sph_hy", nb);
+    float* dz = (float*)ctx->buf("sph_hz", nb);
+    int32_t* di = (int32_t*)ctx->buf("sph_hi", nb);
+    if (!dx || !dy || !dz || !di) return ctx->fail(PITT_E_NOMEM, "sphere staging");
+    std::vector<float> soa((size_t)n * 3);
+    for (int64_t i = 0; i < n; ++i) {
+        soa[(size_t)i] = xyz16[4 * i];
+        soa[(size_t)(n + i)] = xyz16[4 * i + 1];
+        soa[(size_t)(2 * n + i)] = xyz16[4 * i + 2];
+    }
+    hipStream_t s = ctx->stream;
+    if (n > 0) {
+        PITT_HIP_TRY(hipMemcpyAsync(dx, soa.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+        PITT_HIP_TRY(hipMemcpyAsync(dy, soa.data() + n, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        PITT_HIP_TRY(hipMemcpyAsync(dz, soa.data() + 2 * n, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    const int rc = pitt_sphere_segment(ctx, dx, dy, dz, n, params, di, n_inliers, coef, hypotheses);
+    if (rc < 0) return rc;
+    if (*n_inliers > 0) {
+        PITT_HIP_TRY(hipMemcpyAsync(inliers, di, (size_t)*n_inliers * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+    }
+    return rc;
+}

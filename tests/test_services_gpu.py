@@ -143,3 +143,27 @@ def test_call_ransac_plane_client(srv):
     two = np.array([[0, 0, 0], [1, 1, 1]], np.float32)
     ok, inl, _ = srv.call_ransac_plane(two)
     assert not ok and len(inl) == 0
+
+
+def test_sphere_handler(srv):
+    """ransacSphereDetection (sphere_segmentation_srv.cpp:29-96): params, Q1, centroid = centre."""
+    from test_sphere import sphere_scene
+    xyz = sphere_scene(1500, 800, 9)
+    ok, inl, coef, centroid = srv.ransac_sphere(xyz)
+    want = orc.sphere_segment(*xyz.T)
+    assert ok and want["ok"] and len(coef) == 4
+    assert np.allclose(coef, want["coef"], rtol=2e-6, atol=1e-7)
+    assert np.array_equal(centroid, coef[:3])
+    ref = want["inliers"][want["inliers"] != 0]
+    assert len(np.setxor1d(inl, ref)) <= max(3, len(ref) // 1000) and 0 not in inl
+    # radius limits from the parameter server: a 0.05 m sphere outside [0.1, 0.5] has no inliers
+    srv.set_param("/pitt/srv/sphere_segmentation/min_radius_limit", 0.1)
+    try:
+        ok, inl, coef, centroid = srv.ransac_sphere(xyz)
+        want = orc.sphere_segment(*xyz.T, orc.sphere_params(radius_min=0.1))
+        assert ok and len(inl) == len(want["inliers"][want["inliers"] != 0])
+    finally:
+        srv.erase_param("/pitt/srv/sphere_segmentation/min_radius_limit")
+    # normals of the wrong size: PCL clears the outputs
+    ok, inl, coef, centroid = srv.ransac_sphere(xyz, n_normals=len(xyz) - 1)
+    assert ok and len(inl) == 0 and len(coef) == 0 and not centroid.any()
