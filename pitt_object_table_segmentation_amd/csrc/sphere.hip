@@ -18,8 +18,7 @@
 // Device pipeline: k_sph_model (one thread per attempt: the 4 x 4 determinants), k_sph_count per
 // chunk of attempts (one 2048-point tile x one hypothesis per block, ballot counts), the RANSAC replay
 // on the host over the chunk's counts (scalar control), compaction of the inliers, and for the
-// refinement k_sph_sums (per-block double partials of J^T J, J^T r, r^T r) + k_sph_sums_final (fixed
-// order: the same bits on every run), the 4 x 4 damped solve on the host.
+// refinement k_sph_lm: the whole Levenberg-Marquardt iteration in one block (deterministic sums).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -124,19 +123,20 @@ struct WriteIdx {
     __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = (int32_t)i; }
 };
 
-// per-block partial sums (15 doubles: J^T J upper triangle, J^T r, r^T r) over the inliers at x
-constexpr int kSphSumBlocks = 256;
-__global__ __launch_bounds__(256) void k_sph_sums(const float* __restrict__ X, const float* __restrict__ Y,
-                                                  const float* __restrict__ Z, const int32_t* __restrict__ inl,
-                                                  int64_t m, double x0, double x1, double x2, double x3,
-                                                  double* __restrict__ part) {
+// Levenberg-Marquardt over the inliers' residuals ||p - c|| - r in double, one block: every thread
+// sums its strided inliers (J^T J upper triangle, J^T r, r^T r), a fixed shuffle + LDS tree combines
+// them, thread 0 solves the damped 4 x 4 system and decides; control is uniform through LDS.
+constexpr int kLmThreads = 1024;
+
+__device__ void sph_lm_sums(const float* X, const float* Y, const float* Z, const int32_t* inl, int64_t m,
+                            const double* v, double (*red)[15], double* out) {
     double acc[15];
     for (int q = 0; q < 15; ++q) acc[q] = 0;
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = threadIdx.x; k < m; k += kLmThreads) {
         const int id = inl[k];
-        const double dx = (double)X[id] - x0, dy = (double)Y[id] - x1, dz = (double)Z[id] - x2;
+        const double dx = (double)X[id] - v[0], dy = (double)Y[id] - v[1], dz = (double)Z[id] - v[2];
         const double d = sqrt(dx * dx + dy * dy + dz * dz);
-        const double r = d - x3;
+        const double r = d - v[3];
         const double j[4] = {d > 0 ? -dx / d : 0.0, d > 0 ? -dy / d : 0.0, d > 0 ? -dz / d : 0.0, -1.0};
         int q = 0;
         for (int a = 0; a < 4; ++a)
@@ -144,25 +144,112 @@ __global__ __launch_bounds__(256) void k_sph_sums(const float* __restrict__ X, c
         for (int a = 0; a < 4; ++a) acc[10 + a] += j[a] * r;
         acc[14] += r * r;
     }
-    __shared__ double red[4][15];
     for (int q = 0; q < 15; ++q) {
-        double v = acc[q];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = v;
+        double t = acc[q];
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = t;
     }
     __syncthreads();
     if (threadIdx.x < 15) {
-        const int q = threadIdx.x;
-        part[blockIdx.x * 15 + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+        double t = 0;
+        for (int w = 0; w < kLmThreads / 64; ++w) t += red[w][threadIdx.x];
+        out[threadIdx.x] = t;
     }
+    __syncthreads();
 }
 
-__global__ void k_sph_sums_final(const double* __restrict__ part, int nb, double* __restrict__ out) {
-    const int q = threadIdx.x;
-    if (q >= 15) return;
-    double s = 0;
-    for (int b = 0; b < nb; ++b) s += part[b * 15 + q];
-    out[q] = s;
+__global__ __launch_bounds__(kLmThreads) void k_sph_lm(const float* __restrict__ X, const float* __restrict__ Y,
+                                                       const float* __restrict__ Z, const int32_t* __restrict__ inl,
+                                                       int64_t m, float4 init, float4* __restrict__ out) {
+    __shared__ double red[kLmThreads / 64][15];
+    __shared__ double cur[15], trial[15];
+    __shared__ double xv[4], xn[4];
+    __shared__ int state;  // 0 go on, 1 accepted, 2 rejected (more damping), 3 stop
+    if (threadIdx.x == 0) {
+        xv[0] = init.x, xv[1] = init.y, xv[2] = init.z, xv[3] = init.w;
+    }
+    __syncthreads();
+    sph_lm_sums(X, Y, Z, inl, m, xv, red, cur);
+    double lambda = 1e-3;  // thread 0's
+    for (int it = 0; it < 100; ++it) {
+        bool moved = false, stop = false;
+        for (;;) {
+            if (threadIdx.x == 0) {
+                state = 0;
+                if (!(lambda < 1e10)) state = 3;
+                else {
+                    double M[4][5];
+                    int q = 0;
+                    for (int r = 0; r < 4; ++r)
+                        for (int c = r; c < 4; ++c) M[r][c] = M[c][r] = cur[q++];
+                    for (int r = 0; r < 4; ++r) M[r][r] += lambda * M[r][r], M[r][4] = -cur[10 + r];
+                    for (int col = 0; col < 4 && state == 0; ++col) {
+                        int piv = col;
+                        for (int r = col + 1; r < 4; ++r)
+                            if (fabs(M[r][col]) > fabs(M[piv][col])) piv = r;
+                        if (M[piv][col] == 0) {
+                            state = 3;
+                            break;
+                        }
+                        if (piv != col)
+                            for (int c = 0; c < 5; ++c) {
+                                const double t = M[col][c];
+                                M[col][c] = M[piv][c];
+                                M[piv][c] = t;
+                            }
+                        for (int r = col + 1; r < 4; ++r) {
+                            const double f = M[r][col] / M[col][col];
+                            for (int c = col; c < 5; ++c) M[r][c] -= f * M[col][c];
+                        }
+                    }
+                    if (state == 0) {
+                        double dl[4];
+                        for (int r = 3; r >= 0; --r) {
+                            double acc = M[r][4];
+                            for (int c = r + 1; c < 4; ++c) acc -= M[r][c] * dl[c];
+                            dl[r] = acc / M[r][r];
+                        }
+                        for (int r = 0; r < 4; ++r) xn[r] = xv[r] + dl[r];
+                    }
+                }
+            }
+            __syncthreads();
+            const int st0 = state;
+            __syncthreads();  // every thread has read state before thread 0 writes it again
+            if (st0 == 3) {
+                stop = true;
+                break;
+            }
+            sph_lm_sums(X, Y, Z, inl, m, xn, red, trial);
+            if (threadIdx.x == 0) {
+                if (trial[14] < cur[14]) {
+                    double step = 0, nx = 0;
+                    for (int r = 0; r < 4; ++r) {
+                        const double d = xn[r] - xv[r];
+                        step += d * d;
+                        nx += xn[r] * xn[r];
+                        xv[r] = xn[r];
+                    }
+                    for (int q = 0; q < 15; ++q) cur[q] = trial[q];
+                    lambda *= 0.1;
+                    state = sqrt(step / (nx + 1e-300)) < 1e-12 ? 3 : 1;
+                } else {
+                    lambda *= 10;
+                    state = 2;
+                }
+            }
+            __syncthreads();
+            const int st1 = state;
+            __syncthreads();
+            if (st1 == 2) continue;
+            moved = true;
+            stop = st1 == 3;
+            break;
+        }
+        __syncthreads();
+        if (!moved || stop) break;
+    }
+    if (threadIdx.x == 0) *out = make_float4((float)xv[0], (float)xv[1], (float)xv[2], (float)xv[3]);
 }
 
 }  // namespace pitt
@@ -196,7 +283,7 @@ extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y
     const int64_t nt = ctiles(n);
     int32_t* tc = (int32_t*)ctx->buf("sph_tc", (size_t)(nt + 1) * 4);
     int32_t* to = (int32_t*)ctx->buf("sph_to", (size_t)(nt + 1) * 4);
-    double* part = (double*)ctx->buf("sph_part", (size_t)kSphSumBlocks * 15 * 8 + 15 * 8);
+    double* part = (double*)ctx->buf("sph_part", 64);
     if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !part) return ctx->fail(PITT_E_NOMEM, "sphere scratch");
     PITT_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), (size_t)A * 16, hipMemcpyHostToDevice, s));
     int rec = ctx->prof_begin("k_sph_model", (double)A * 48.0);
@@ -286,80 +373,21 @@ extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y
     if (rc != PITT_OK) return rc;
     float out[4] = {bc.x, bc.y, bc.z, bc.w};
     if (p->optimize && *n_inliers > 4) {
-        // Levenberg-Marquardt in double on device sums over the inliers (the oracle's sphere_refine)
-        double* sums = part + kSphSumBlocks * 15;
-        double* hs = (double*)ctx->pinned("sph_sums_h", 15 * 8);
-        if (!hs) return ctx->fail(PITT_E_NOMEM, "sphere pinned");
-        const int64_t m = *n_inliers;
-        auto eval = [&](const double* v, double* jtj, double* jtr, double* cost) -> int {
-            hipLaunchKernelGGL(k_sph_sums, dim3(kSphSumBlocks), dim3(256), 0, s, x, y, z, inliers, m, v[0], v[1], v[2],
-                               v[3], part);
-            hipLaunchKernelGGL(k_sph_sums_final, dim3(1), dim3(64), 0, s, part, kSphSumBlocks, sums);
-            PITT_HIP_TRY(hipGetLastError());
-            PITT_HIP_TRY(hipMemcpyAsync(hs, sums, 15 * 8, hipMemcpyDeviceToHost, s));
-            PITT_HIP_TRY(hipStreamSynchronize(s));
-            std::memcpy(jtj, hs, 10 * 8);
-            std::memcpy(jtr, hs + 10, 4 * 8);
-            *cost = hs[14];
-            return PITT_OK;
-        };
-        double xv[4] = {bc.x, bc.y, bc.z, bc.w}, jtj[10], jtr[4], cost;
-        rc = eval(xv, jtj, jtr, &cost);
-        if (rc != PITT_OK) return rc;
-        double lambda = 1e-3;
-        for (int it = 0; it < 100; ++it) {
-            bool moved = false;
-            double step = 0;
-            while (lambda < 1e10) {
-                double M[4][5];
-                int q = 0;
-                for (int r = 0; r < 4; ++r)
-                    for (int c = r; c < 4; ++c) M[r][c] = M[c][r] = jtj[q++];
-                for (int r = 0; r < 4; ++r) M[r][r] += lambda * M[r][r], M[r][4] = -jtr[r];
-                bool ok = true;
-                for (int col = 0; col < 4 && ok; ++col) {
-                    int piv = col;
-                    for (int r = col + 1; r < 4; ++r)
-                        if (std::fabs(M[r][col]) > std::fabs(M[piv][col])) piv = r;
-                    if (M[piv][col] == 0) {
-                        ok = false;
-                        break;
-                    }
-                    if (piv != col)
-                        for (int c = 0; c < 5; ++c) std::swap(M[col][c], M[piv][c]);
-                    for (int r = col + 1; r < 4; ++r) {
-                        const double f = M[r][col] / M[col][col];
-                        for (int c = col; c < 5; ++c) M[r][c] -= f * M[col][c];
-                    }
-                }
-                if (!ok) break;
-                double dl[4];
-                for (int r = 3; r >= 0; --r) {
-                    double acc = M[r][4];
-                    for (int c = r + 1; c < 4; ++c) acc -= M[r][c] * dl[c];
-                    dl[r] = acc / M[r][r];
-                }
-                double xn[4], jn[10], rn[4], cn;
-                for (int r = 0; r < 4; ++r) xn[r] = xv[r] + dl[r];
-                rc = eval(xn, jn, rn, &cn);
-                if (rc != PITT_OK) return rc;
-                if (cn < cost) {
-                    double nx = 0;
-                    for (int r = 0; r < 4; ++r) step += dl[r] * dl[r], nx += xn[r] * xn[r];
-                    step = std::sqrt(step / (nx + 1e-300));
-                    std::memcpy(xv, xn, sizeof xv);
-                    std::memcpy(jtj, jn, sizeof jtj);
-                    std::memcpy(jtr, rn, sizeof jtr);
-                    cost = cn;
-                    lambda *= 0.1;
-                    moved = true;
-                    break;
-                }
-                lambda *= 10;
-            }
-            if (!moved || step < 1e-12) break;
-        }
-        for (int r = 0; r < 4; ++r) out[r] = (float)xv[r];
+        // Levenberg-Marquardt in double, the whole iteration in one 1024-thread block (the oracle's
+        // sphere_refine; fixed reduction order, so the same bits on every run)
+        float4* dref = (float4*)part;
+        rec = ctx->prof_begin("k_sph_lm", (double)*n_inliers * 12.0);
+        hipLaunchKernelGGL(k_sph_lm, dim3(1), dim3(kLmThreads), 0, s, x, y, z, inliers, *n_inliers, bc, dref);
+        ctx->prof_end(rec);
+        PITT_HIP_TRY(hipGetLastError());
+        float4* hr = (float4*)ctx->pinned("sph_ref_h", 16);
+        if (!hr) return ctx->fail(PITT_E_NOMEM, "sphere pinned");
+        PITT_HIP_TRY(hipMemcpyAsync(hr, dref, 16, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        out[0] = hr->x;
+        out[1] = hr->y;
+        out[2] = hr->z;
+        out[3] = hr->w;
         rc = select(make_float4(out[0], out[1], out[2], out[3]));
         if (rc != PITT_OK) return rc;
     }

@@ -140,6 +140,28 @@ def main():
                         e["kernels"][kname]["valu_frac"] = round(pairs * 8 / (us * 1e-6) / 78.6e12, 3)
             ctx.profile(False)
             axis[str(na)] = e
+        # sphere service: RANSAC (radius limits) + refinement on object-sized clusters with clutter
+        from test_sphere import sphere_scene
+        sph = {}
+        for ns, no in ((4000, 1000), (40000, 10000)):
+            ps = sphere_scene(ns, no, 7)
+            ts = [torch.from_numpy(np.ascontiguousarray(ps[:, k])).cuda() for k in range(3)]
+            ctx.sphere_segment(*ts)
+            torch.cuda.synchronize()
+            ctx.profile(True)
+            ctx.profile_reset()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                inl_s, coef_s, hyp_s = ctx.sphere_segment(*ts)
+            torch.cuda.synchronize()
+            e = {"ms_per_call_wall": round((time.perf_counter() - t0) * 1e3 / 5, 3), "points": ns + no,
+                 "hypotheses": hyp_s, "inliers": int(inl_s.numel()), "kernels": {}}
+            for kname in ("k_sph_model", "k_sph_count", "k_sph_lm"):
+                launches, ms, algo = ctx.profile_get(kname)
+                if launches:
+                    e["kernels"][kname] = {"launches_per_call": launches / 5, "avg_us": round(ms / launches * 1e3, 1)}
+            ctx.profile(False)
+            sph[str(ns + no)] = e
     import oracle_binding as orc
     t0 = time.perf_counter()
     k = 0
@@ -161,10 +183,14 @@ def main():
     t0 = time.perf_counter()
     orc.axis_height(*pa.T, coef)
     axis["5000"]["cpu_oracle_ms_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
+    ps = sphere_scene(4000, 1000, 7)
+    t0 = time.perf_counter()
+    orc.sphere_segment(*ps.T)
+    sph["5000"]["cpu_oracle_ms_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
                                   f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
                       "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox, "normal_estimation": nrm,
-                      "axis_height": axis,
+                      "axis_height": axis, "sphere_segment": sph,
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
 
