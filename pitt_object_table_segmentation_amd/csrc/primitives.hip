@@ -20,7 +20,8 @@
 // Kernels (one 256-point i tile x one 256-point j tile per block, j tile <= i tile, the j tile staged
 // in LDS and read by broadcast ds_read_b128; per pair 3 v_sub + 3 v_mul + 2 v_add + 1 v_max):
 //   k_axis_project   12 B read + 12 B written per point                 HBM
-//   k_pair_max       9 VALU ops per pair, one atomic per block           VALU (n^2 / 2 pairs)
+//   k_pair_max       9 VALU ops per pair, one 64-lane wave per tile pair with four i points per
+//                    lane (one LDS read per four pairs), one atomic per tile pair   VALU (n^2 / 2 pairs)
 //   k_pair_first     the first pair at or above s_lo, only in the tile pairs whose maximum (kept
 //                    by k_pair_max) reaches it                           a few tiles
 //   k_axis_final     height, indices, centroid (one thread)
@@ -152,6 +153,57 @@ __global__ __launch_bounds__(kPairTile) void k_pair_scan(const float* __restrict
     }
 }
 
+// The maximum pass with four i points per thread (one 64-lane wave per tile pair): each broadcast
+// ds_read_b128 of a j point feeds four pairs.
+__global__ __launch_bounds__(64) void k_pair_max4(const float* __restrict__ qx, const float* __restrict__ qy,
+                                                  const float* __restrict__ qz, int64_t n,
+                                                  uint32_t* __restrict__ smax_bits, float* __restrict__ tile_max) {
+    __shared__ float4 jq[kPairTile];
+    int ti, tj;
+    pair_tile(blockIdx.x, ti, tj);
+    const int64_t j0 = (int64_t)tj * kPairTile, i0 = (int64_t)ti * kPairTile;
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t j = j0 + lane + 64 * k;
+        if (j < n) jq[lane + 64 * k] = make_float4(qx[j], qy[j], qz[j], 0.0f);
+    }
+    __syncthreads();
+    float xi[4], yi[4], zi[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = min(i0 + lane + 64 * k, n - 1);
+        xi[k] = qx[i];
+        yi[k] = qy[i];
+        zi[k] = qz[i];
+    }
+    float best[4] = {-1.0f, -1.0f, -1.0f, -1.0f};
+    if (tj < ti && i0 + kPairTile <= n) {  // every j < every i, all in range: a constant trip count
+#pragma unroll 8
+        for (int j = 0; j < kPairTile; ++j) {
+            const float4 q = jq[j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) best[k] = vmaxf(best[k], pair_s(xi[k], yi[k], zi[k], q.x, q.y, q.z));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = i0 + lane + 64 * k;
+            const int jn = i < n ? (int)std::min<int64_t>(kPairTile, std::min<int64_t>(n - j0, i - j0)) : 0;
+            for (int j = 0; j < jn; ++j) {
+                const float4 q = jq[j];
+                best[k] = vmaxf(best[k], pair_s(xi[k], yi[k], zi[k], q.x, q.y, q.z));
+            }
+        }
+    }
+    float b = vmaxf(vmaxf(best[0], best[1]), vmaxf(best[2], best[3]));
+    for (int off = 32; off > 0; off >>= 1) b = vmaxf(b, __shfl_xor(b, off, 64));
+    if (lane == 0) {
+        tile_max[blockIdx.x] = b;
+        if (b >= 0.0f) atomicMax(smax_bits, __float_as_uint(b) + 1u);  // 0 = no pair
+    }
+}
+
 // AxisOut: height, idx1, idx2, centroid[3]
 struct AxisOut {
     float height;
@@ -231,8 +283,11 @@ extern "C" int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, c
         float* tmax = (float*)ctx->buf("ax_tile_max", (size_t)tp * 4);
         if (!tmax) return ctx->fail(PITT_E_NOMEM, "axis height tile maxima");
         rec = ctx->prof_begin("k_pair_max", (double)n * (double)(n - 1) / 2.0);
-        hipLaunchKernelGGL(k_pair_scan<false>, dim3((unsigned)tp), dim3(kPairTile), 0, s, qx, qy, qz, n,
-                           (const float*)nullptr, w, first, tmax);
+        if (tp >= 4096)  // enough tile pairs to fill the chip with one-wave blocks
+            hipLaunchKernelGGL(k_pair_max4, dim3((unsigned)tp), dim3(64), 0, s, qx, qy, qz, n, w, tmax);
+        else
+            hipLaunchKernelGGL(k_pair_scan<false>, dim3((unsigned)tp), dim3(kPairTile), 0, s, qx, qy, qz, n,
+                               (const float*)nullptr, w, first, tmax);
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
         uint32_t* hw = (uint32_t*)ctx->pinned("ax_w", 16);

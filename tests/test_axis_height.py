@@ -104,7 +104,7 @@ def test_oracle_axis_height_edges():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,seed,mode", [(2, 11, 0), (3, 12, 1), (255, 13, 0), (256, 14, 1), (257, 15, 0),
-                                         (1000, 16, 1), (4097, 17, 0), (20000, 18, 1)])
+                                         (1000, 16, 1), (4097, 17, 0), (20000, 18, 1), (30000, 19, 0)])
 def test_hip_axis_height_matches_oracle(ctx, n, seed, mode):
     import torch
     p, coef = cylinder_cloud(n, seed)
