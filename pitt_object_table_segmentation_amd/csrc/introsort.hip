@@ -121,17 +121,19 @@ __device__ __forceinline__ void is_grid_sync(uint32_t* bar, uint32_t& target) {
     __syncthreads();
 }
 
-// All levels of segments longer than kIsSmall in one launch of a resident grid; a level is six grid-wide
+// All levels of segments longer than kIsSmall in one launch of a resident grid; a level is five grid-wide
 // phases (grid barriers between them):
-//   1 pivot   per segment: median of (first + 1, mid, last - 1) to first; depth 0 -> the heap list;
+//   1 pivot   per segment: median of (first + 1, mid, last - 1) to first; depth 0 -> the heap list
+//             (beside it, the previous level's step 7);
 //   2 flags   per element: left stop (key >= p) / right stop (key <= p) of its segment, block-local
 //             exclusive ranks over the block's contiguous chunk, block totals;
-//   3 offsets the chunk prefix of the block totals added: global exclusive ranks SL / SR;
-//   4 ranks   per element: posL[first + 1 + k] = the k-th left stop, posR[first + 1 + k] = the k-th
+//   4 ranks   global rank = block-local rank + the prefix of the block totals (each block forms it);
+//             per element: posL[first + 1 + k] = the k-th left stop, posR[first + 1 + k] = the k-th
 //             right stop from the end; per segment nL / nR;
 //   5 K       per segment: the swaps __unguarded_partition makes (posL[k] < posR[k] holds on a prefix);
 //   6 swap    per element k < K: swap posL[k] <-> posR[k]; per segment: the cut, the children;
-//   7 segid   per element: its child segment (or -1), then every block reads the next level's count.
+//   7 segid   per element: its child segment (or -1) -- run with the next level's step 1, after every
+//             block has read the next level's segment count.
 __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, ISeg* __restrict__ segB,
                                                    ISeg* __restrict__ heap, ISmall* __restrict__ small,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ segid,
@@ -141,6 +143,7 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
                                                    uint32_t* __restrict__ key, uint32_t* __restrict__ val, int64_t n,
                                                    int64_t chunk, int levels, uint32_t* __restrict__ bar) {
     __shared__ int sh[2 * kIsLvW];
+    __shared__ int preL[513], preR[513];  // G <= 512
     uint32_t target = 0;
     const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
     const int64_t gt = (int64_t)b * kIsLvT + tid, gstride = (int64_t)G * kIsLvT;
@@ -148,7 +151,16 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
     ISeg* cur = segA;
     ISeg* nxt = segB;
     for (int v = 0; v < levels; ++v) {
-        const int nseg = is_load_count(cnt + 2 + v);
+        const int nseg = is_load_count(cnt + 2 + v);  // the same value in every block (after a barrier)
+        if (nseg == 0) break;
+        if (v > 0) {  // 7 (of the previous level) next segment ids -- beside this level's pivots
+            for (int64_t i = gt; i < n; i += gstride) {
+                const int s = segid[i];
+                if (s < 0) continue;
+                const ISeg& g = nxt[s];
+                segid[i] = !g.active ? -1 : (i < g.cut ? g.childL : g.childR);
+            }
+        }
         // 1 pivot
         for (int64_t s = gt; s < nseg; s += gstride) {
             ISeg g = cur[s];
@@ -201,39 +213,30 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             bsum[G + b] = carR;
         }
         is_grid_sync(bar, target);
-        // 3 global ranks
-        {
+        // 4 stop positions; stop counts.  Global ranks = block-local rank + the prefix of the block
+        // totals (every block forms the prefix itself: no separate pass)
+        for (int j = tid; j <= G; j += kIsLvT) {
             int a = 0, r = 0;
-            for (int j = tid; j < b; j += kIsLvT) {
-                a += bsum[j];
-                r += bsum[G + j];
-            }
-            int ea, er, offL, offR;
-            is_block_scan2(a, r, ea, er, offL, offR, sh);
-            for (int64_t i = c0 + tid; i < c1; i += kIsLvT) {
-                SL[i] += offL;
-                SR[i] += offR;
-            }
-            if (b == G - 1 && tid == 0) {
-                SL[n] = offL + carL;
-                SR[n] = offR + carR;
-            }
+            for (int q = 0; q < j; ++q) a += bsum[q], r += bsum[G + q];
+            preL[j] = a;
+            preR[j] = r;
         }
-        is_grid_sync(bar, target);
-        // 4 stop positions; stop counts
+        __syncthreads();
+        auto gl = [&](int64_t i) { return i >= n ? preL[G] : SL[i] + preL[i / chunk]; };
+        auto gr = [&](int64_t i) { return i >= n ? preR[G] : SR[i] + preR[i / chunk]; };
         for (int64_t s = gt; s < nseg; s += gstride) {
             if (!cur[s].active) continue;
             const int bb = cur[s].f + 1, l = cur[s].l;
-            cur[s].nL = SL[l] - SL[bb];
-            cur[s].nR = SR[l] - SR[bb];
+            cur[s].nL = gl(l) - gl(bb);
+            cur[s].nR = gr(l) - gr(bb);
         }
         for (int64_t i = gt; i < n; i += gstride) {
             const int fb = F[i];
             if (!fb) continue;
             const ISeg& g = cur[segid[i]];
             const int bb = g.f + 1;
-            if (fb & 1) posL[bb + (SL[i] - SL[bb])] = (int32_t)i;
-            if (fb & 2) posR[bb + (SR[g.l] - SR[i + 1])] = (int32_t)i;
+            if (fb & 1) posL[bb + (gl(i) - gl(bb))] = (int32_t)i;
+            if (fb & 2) posR[bb + (gr(g.l) - gr(i + 1))] = (int32_t)i;
         }
         is_grid_sync(bar, target);
         // 5 K by bisection
@@ -270,18 +273,9 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             cur[s].childR = is_child(cut, g.l, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
         }
         is_grid_sync(bar, target);
-        // 7 next segment ids
-        for (int64_t i = gt; i < n; i += gstride) {
-            const int s = segid[i];
-            if (s < 0) continue;
-            const ISeg& g = cur[s];
-            segid[i] = !g.active ? -1 : (i < g.cut ? g.childL : g.childR);
-        }
-        ISeg* t = cur;
+        ISeg* t = cur;  // phase 7 runs at the top of the next level, over nxt (= this level's segments)
         cur = nxt;
         nxt = t;
-        if (is_load_count(cnt + 3 + v) == 0) break;  // the same value in every block (after the barrier)
-        is_grid_sync(bar, target);
     }
 }
 
