@@ -39,7 +39,10 @@ struct ISmall {
 };
 
 constexpr int kIsThreshold = 16;  // _S_threshold
-constexpr int kIsSmall = 2048;
+#ifndef PITT_IS_SMALL
+#define PITT_IS_SMALL 2048
+#endif
+constexpr int kIsSmall = PITT_IS_SMALL;  // segments this short finish in one wave, in LDS
 #ifndef PITT_IS_COOP_MAX
 #define PITT_IS_COOP_MAX 64
 #endif    // segments this short finish in one wave, in LDS

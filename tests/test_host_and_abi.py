@@ -141,14 +141,15 @@ def test_ros_adapters_use_only_declared_abi():
         declared |= set(re.findall(r"\b(pitt_\w+)\s*\(", open(h).read()))
     srcs = glob.glob(os.path.join(root, "adapters", "ros", "*.cpp")) + \
         glob.glob(os.path.join(root, "adapters", "ros", "*.hpp"))
-    assert len(srcs) == 5
+    assert len(srcs) == 6
     used = set()
     for s in srcs:
         used |= set(re.findall(r"\b(pitt_(?!ros\b)\w+)\s*\(", open(s).read()))
     assert used and used <= declared, sorted(used - declared)
     names = {"plane_segmentation_node.cpp": "plane_segmentation_srv", "deep_filter_node.cpp": "deep_filter_srv",
              "supports_segmentation_node.cpp": "support_segmentation_srv",
-             "cluster_segmentation_node.cpp": "cluster_Segmentation_srv"}
+             "cluster_segmentation_node.cpp": "cluster_Segmentation_srv",
+             "sphere_segmentation_node.cpp": "sphere_segmentation_srv"}
     for f, name in names.items():
         assert f'advertiseService("{name}"' in open(os.path.join(root, "adapters", "ros", f)).read(), f
 
