@@ -25,6 +25,7 @@
  *   pitt_normal_estimation        replaces  NormalEstimation<PointXYZ, Normal>::compute (estimateNormal)
  *        src/point_cloud_library/pc_manager.cpp:68-78
  *   pitt_sphere_segment           replaces  seg.segment in src/segmentation_services/sphere_segmentation_srv.cpp:57-73
+ *   pitt_cylinder_segment         replaces  seg.segment in src/segmentation_services/cylinder_segmentation_srv.cpp:110-126
  *   pitt_axis_height              replaces  the projection + O(n^2) height loop after seg.segment in
  *        src/segmentation_services/cylinder_segmentation_srv.cpp:129-189 and
  *        src/segmentation_services/cone_segmentation_srv.cpp:129-189
@@ -294,6 +295,28 @@ int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y, const flo
 /* The same on a host PointXYZ cloud (x, y, z, pad: 16-byte stride); inliers in host memory. */
 int pitt_sphere_segment_host(pitt_ctx* ctx, const float* xyz16, int64_t n, const pitt_sphere_params* params,
                              int32_t* inliers, int64_t* n_inliers, float coef[4], int32_t* hypotheses);
+
+/* The cylinder service's seg.segment (cylinder_segmentation_srv.cpp:110-126): SampleConsensusModelCylinder
+ * with normals (2-point samples; the model from the two normal lines' closest points), the radius limits,
+ * the normal-weighted distance |w * angle + (1 - w) * |axis distance - r|| < threshold, PCL's
+ * computeModel loop with w^2; optimize: the least-squares refinement of sqrPointToLineDistance - r^2
+ * (PCL: Eigen's float Levenberg-Marquardt -- the axis and radius equal within its tolerance, the point
+ * on the axis may slide along it), the direction normalised, the final selection.  x/y/z and the
+ * normals nx/ny/nz: device SoA of n points; inliers (device, capacity n) ascending; coef[7] = point on
+ * the axis, direction, radius.  PITT_OK with a model, PITT_NO_MODEL without. */
+typedef struct {
+    double   threshold;               /* 0.008 (cylinder_segmentation_srv.cpp:24) */
+    int32_t  max_iterations;          /* 1000 (:27) */
+    int32_t  optimize;                /* 1 (:114) */
+    double   probability;             /* 0.99 */
+    double   radius_min, radius_max;  /* 0.005, 0.5 (:25-26) */
+    double   normal_distance_weight;  /* 0.001 (:23) */
+    uint32_t seed;                    /* 12345 */
+    int32_t  pad;
+} pitt_cylinder_params;
+int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
+                          const float* ny, const float* nz, int64_t n, const pitt_cylinder_params* params,
+                          int32_t* inliers, int64_t* n_inliers, float coef[7], int32_t* hypotheses);
 
 /* The post-processing of the cylinder and cone services once PCL has fitted the model
  * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).

@@ -1347,3 +1347,261 @@ int orc_sphere_segment(const float* x, const float* y, const float* z, int64_t n
     return 1;
 }
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Cylinder (PCL 1.7 sample_consensus/impl/sac_model_cylinder.hpp, common/distances.h, common.hpp).
+// Eigen::Vector4f arithmetic: element-wise float ops, dot / squaredNorm reduced in SSE2 order (A3),
+// normalize() multiplies by 1 / norm (A9), normalized() divides by it.
+namespace {
+struct V4 {
+    float v[4];
+};
+inline V4 v4(float a, float b, float c, float d = 0.0f) { return V4{{a, b, c, d}}; }
+inline V4 add(V4 a, V4 b) { return v4(a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]); }
+inline V4 sub(V4 a, V4 b) { return v4(a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2], a.v[3] - b.v[3]); }
+inline V4 mul(float s, V4 a) { return v4(s * a.v[0], s * a.v[1], s * a.v[2], s * a.v[3]); }
+inline float dot(V4 a, V4 b) { return red4(a.v[0] * b.v[0], a.v[1] * b.v[1], a.v[2] * b.v[2], a.v[3] * b.v[3], 0); }
+inline V4 cross3(V4 l, V4 r) {  // Eigen's SSE cross3: lane 3 = l3 r3 - l3 r3
+    return v4(l.v[1] * r.v[2] - l.v[2] * r.v[1], l.v[2] * r.v[0] - l.v[0] * r.v[2], l.v[0] * r.v[1] - l.v[1] * r.v[0],
+              l.v[3] * r.v[3] - l.v[3] * r.v[3]);
+}
+inline V4 normalize(V4 a) {  // *this /= norm(): times 1 / norm (A9)
+    const float r = 1.0f / std::sqrt(dot(a, a));
+    return v4(a.v[0] * r, a.v[1] * r, a.v[2] * r, a.v[3] * r);
+}
+inline V4 normalized(V4 a) {  // *this / norm()
+    const float nn = std::sqrt(dot(a, a));
+    return v4(a.v[0] / nn, a.v[1] / nn, a.v[2] / nn, a.v[3] / nn);
+}
+// sqrPointToLineDistance: |line_dir x (line_pt - pt)|^2 / |line_dir|^2 (float quotient, as double)
+inline double sqr_pt_line(V4 pt, V4 lp, V4 ld) {
+    const V4 c = cross3(ld, sub(lp, pt));
+    return (double)(dot(c, c) / dot(ld, ld));
+}
+// getAngle3D: acos of the clamped dot of the normalized vectors (double)
+inline double angle3d(V4 a, V4 b) {
+    double rad = dot(normalized(a), normalized(b));
+    if (rad < -1.0) rad = -1.0;
+    else if (rad > 1.0) rad = 1.0;
+    return std::acos(rad);
+}
+
+bool cyl_from2(const float* x, const float* y, const float* z, const float* nx, const float* ny, const float* nz,
+               const int s[2], double rmin, double rmax, float c[7]) {
+    const int a = s[0], b = s[1];
+    const float eps = std::numeric_limits<float>::epsilon();
+    if (std::fabs(x[a] - x[b]) <= eps && std::fabs(y[a] - y[b]) <= eps && std::fabs(z[a] - z[b]) <= eps) return false;
+    const V4 p1 = v4(x[a], y[a], z[a]), p2 = v4(x[b], y[b], z[b]);
+    const V4 n1 = v4(nx[a], ny[a], nz[a]), n2 = v4(nx[b], ny[b], nz[b]);
+    const V4 w = sub(add(n1, p1), p2);
+    const float A = dot(n1, n1), B = dot(n1, n2), C = dot(n2, n2), D = dot(n1, w), E = dot(n2, w);
+    const float den = A * C - B * B;
+    float sc, tc;
+    if (den < 1e-8) {
+        sc = 0.0f;
+        tc = (B > C ? D / B : E / C);
+    } else {
+        sc = (B * E - C * D) / den;
+        tc = (A * E - B * D) / den;
+    }
+    const V4 lp = add(add(p1, n1), mul(sc, n1));
+    const V4 ld = normalize(sub(add(p2, mul(tc, n2)), lp));
+    for (int k = 0; k < 3; ++k) c[k] = lp.v[k], c[3 + k] = ld.v[k];
+    c[6] = (float)std::sqrt(sqr_pt_line(p1, lp, ld));
+    if (c[6] > rmax || c[6] < rmin) return false;
+    return true;
+}
+
+bool cyl_valid(const float c[7], double rmin, double rmax) {
+    if (rmin != -DBL_MAX && c[6] < rmin) return false;
+    if (rmax != DBL_MAX && c[6] > rmax) return false;
+    return true;
+}
+
+inline bool cyl_in(const float* x, const float* y, const float* z, const float* nx, const float* ny, const float* nz,
+                   int64_t i, const float c[7], double w, double th) {
+    const V4 lp = v4(c[0], c[1], c[2]), ld = v4(c[3], c[4], c[5]);
+    const float ptdotdir = dot(lp, ld), dirdotdir = 1.0f / dot(ld, ld);
+    const V4 pt = v4(x[i], y[i], z[i]), nn = v4(nx[i], ny[i], nz[i]);
+    const double d_euclid = std::fabs(std::sqrt(sqr_pt_line(pt, lp, ld)) - (double)c[6]);
+    const float k = (dot(pt, ld) - ptdotdir) * dirdotdir;
+    const V4 proj = add(lp, mul(k, ld));
+    const V4 dir = normalize(sub(pt, proj));
+    double d_normal = std::fabs(angle3d(nn, dir));
+    d_normal = std::min(d_normal, M_PI - d_normal);
+    return std::fabs(w * d_normal + (1 - w) * d_euclid) < th;
+}
+
+// f = |u x (c - p)|^2 / |u|^2 - r^2 and its gradient in (c, u, r)
+inline void cyl_residual(const double* v, float px, float py, float pz, double J[7], double* f) {
+    const double vx = v[0] - px, vy = v[1] - py, vz = v[2] - pz;  // c - p
+    const double ux = v[3], uy = v[4], uz = v[5];
+    const double wx = uy * vz - uz * vy, wy = uz * vx - ux * vz, wz = ux * vy - uy * vx;  // u x v
+    const double s = ux * ux + uy * uy + uz * uz, w2 = wx * wx + wy * wy + wz * wz;
+    *f = w2 / s - v[6] * v[6];
+    // d|w|^2/dv = 2 (w x u); d|w|^2/du = 2 (v x w)
+    J[0] = 2.0 * (wy * uz - wz * uy) / s;
+    J[1] = 2.0 * (wz * ux - wx * uz) / s;
+    J[2] = 2.0 * (wx * uy - wy * ux) / s;
+    J[3] = 2.0 * (vy * wz - vz * wy) / s - 2.0 * w2 * ux / (s * s);
+    J[4] = 2.0 * (vz * wx - vx * wz) / s - 2.0 * w2 * uy / (s * s);
+    J[5] = 2.0 * (vx * wy - vy * wx) / s - 2.0 * w2 * uz / (s * s);
+    J[6] = -2.0 * v[6];
+}
+
+// Levenberg-Marquardt (Marquardt damping lambda * diag, x10 / x0.1) over N parameters; sums(v, jtj
+// (upper triangle, row major), jtr, cost).  Stops when no damping lowers the cost or the step is
+// below 1e-12 relative.
+template <int N, class Sums>
+void lm_solve(double* x, Sums sums) {
+    double jtj[N * (N + 1) / 2], jtr[N], cost;
+    sums(x, jtj, jtr, &cost);
+    double lambda = 1e-3;
+    for (int it = 0; it < 200; ++it) {
+        bool moved = false;
+        double step = 0;
+        while (lambda < 1e10) {
+            double M[N][N + 1];
+            int t = 0;
+            for (int a = 0; a < N; ++a)
+                for (int b = a; b < N; ++b) M[a][b] = M[b][a] = jtj[t++];
+            for (int a = 0; a < N; ++a) M[a][a] += lambda * M[a][a] + 1e-30, M[a][N] = -jtr[a];
+            bool ok = true;
+            for (int col = 0; col < N && ok; ++col) {
+                int piv = col;
+                for (int r = col + 1; r < N; ++r)
+                    if (std::fabs(M[r][col]) > std::fabs(M[piv][col])) piv = r;
+                if (M[piv][col] == 0) { ok = false; break; }
+                if (piv != col)
+                    for (int k = 0; k <= N; ++k) std::swap(M[col][k], M[piv][k]);
+                for (int r = col + 1; r < N; ++r) {
+                    const double f = M[r][col] / M[col][col];
+                    for (int k = col; k <= N; ++k) M[r][k] -= f * M[col][k];
+                }
+            }
+            if (!ok) break;
+            double dl[N];
+            for (int r = N - 1; r >= 0; --r) {
+                double acc = M[r][N];
+                for (int k = r + 1; k < N; ++k) acc -= M[r][k] * dl[k];
+                dl[r] = acc / M[r][r];
+            }
+            double xn[N], jn[N * (N + 1) / 2], rn[N], cn;
+            for (int a = 0; a < N; ++a) xn[a] = x[a] + dl[a];
+            sums(xn, jn, rn, &cn);
+            if (cn < cost) {
+                double nx = 0;
+                for (int a = 0; a < N; ++a) step += dl[a] * dl[a], nx += xn[a] * xn[a];
+                step = std::sqrt(step / (nx + 1e-300));
+                for (int a = 0; a < N; ++a) x[a] = xn[a];
+                std::memcpy(jtj, jn, sizeof jtj);
+                std::memcpy(jtr, rn, sizeof jtr);
+                cost = cn;
+                lambda *= 0.1;
+                moved = true;
+                break;
+            }
+            lambda *= 10;
+        }
+        if (!moved || step < 1e-12) break;
+    }
+}
+
+// Levenberg-Marquardt in double on f_i = |u x (c - p_i)|^2 / |u|^2 - r^2 (OptimizationFunctor's
+// residual), parameters (c, u, r); then u normalised.
+void cyl_refine(const float* x, const float* y, const float* z, const std::vector<int>& inl, const float in[7],
+                float out[7]) {
+    double q[7];
+    for (int k = 0; k < 7; ++k) q[k] = in[k];
+    auto sums = [&](const double* v, double* jtj /*28*/, double* jtr /*7*/, double* cost) {
+        for (int k = 0; k < 28; ++k) jtj[k] = 0;
+        for (int k = 0; k < 7; ++k) jtr[k] = 0;
+        *cost = 0;
+        for (int id : inl) {
+            double J[7], f;
+            cyl_residual(v, x[id], y[id], z[id], J, &f);
+            int t = 0;
+            for (int a = 0; a < 7; ++a)
+                for (int b = a; b < 7; ++b) jtj[t++] += J[a] * J[b];
+            for (int a = 0; a < 7; ++a) jtr[a] += J[a] * f;
+            *cost += f * f;
+        }
+    };
+    lm_solve<7>(q, sums);
+    const double nu = std::sqrt(q[3] * q[3] + q[4] * q[4] + q[5] * q[5]);
+    for (int k = 0; k < 3; ++k) out[k] = (float)q[k];
+    // Eigen::Vector3f line_dir(...).normalize() on the float coefficients
+    // Vector3f: fixed size 3, not vectorised: a0 + (a1 + a2)
+    const float u0 = (float)q[3], u1 = (float)q[4], u2 = (float)q[5];
+    const float r = 1.0f / std::sqrt(u0 * u0 + (u1 * u1 + u2 * u2));
+    out[3] = u0 * r;
+    out[4] = u1 * r;
+    out[5] = u2 * r;
+    out[6] = (float)q[6];
+    (void)nu;
+}
+}  // namespace
+
+extern "C" int orc_cylinder_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
+                                    const float* nz, int64_t n, const orc_cylinder_params* p, int32_t* inliers,
+                                    int64_t* n_inliers, float coef[7], float best_out[7], int32_t* hypotheses) {
+    *n_inliers = 0;
+    *hypotheses = 0;
+    if (n < 2) return 0;  // getSamples: "Can not select 2 unique points"
+    std::mt19937 mt(p->seed);
+    std::vector<int> sh((size_t)n);
+    std::iota(sh.begin(), sh.end(), 0);
+    int iterations = 0, n_best = -std::numeric_limits<int>::max();
+    double k = 1.0;
+    const double log_probability = std::log(1.0 - p->probability);
+    const double one_over_indices = 1.0 / (double)n;
+    unsigned skipped = 0;
+    const unsigned max_skip = (unsigned)p->max_iterations * 10u;
+    bool have = false;
+    float best[7] = {0, 0, 0, 0, 0, 0, 0};
+    while (iterations < k && skipped < max_skip) {
+        for (unsigned i = 0; i < 2; ++i) std::swap(sh[i], sh[i + ((size_t)(mt() >> 1) % ((size_t)n - i))]);
+        const int smp[2] = {sh[0], sh[1]};
+        float m[7];
+        if (!cyl_from2(x, y, z, nx, ny, nz, smp, p->radius_min, p->radius_max, m)) {
+            ++skipped;
+            continue;
+        }
+        int n_in = 0;
+        if (cyl_valid(m, p->radius_min, p->radius_max))
+            for (int64_t i = 0; i < n; ++i) n_in += cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold);
+        if (n_in > n_best) {
+            n_best = n_in;
+            have = true;
+            std::memcpy(best, m, sizeof m);
+            const double w = (double)n_best * one_over_indices;
+            double p_no = 1.0 - std::pow(w, 2.0);
+            p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
+            p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
+            k = log_probability / std::log(p_no);
+        }
+        ++iterations;
+        if (iterations > p->max_iterations) break;
+    }
+    *hypotheses = iterations;
+    if (!have) return 0;
+    std::memcpy(best_out, best, sizeof best);
+    std::vector<int> inl;
+    auto select = [&](const float* m) {
+        inl.clear();
+        if (!cyl_valid(m, p->radius_min, p->radius_max)) return;
+        for (int64_t i = 0; i < n; ++i)
+            if (cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold)) inl.push_back((int)i);
+    };
+    select(best);
+    float out[7];
+    std::memcpy(out, best, sizeof out);
+    if (p->optimize && !inl.empty()) {  // optimizeModelCoefficients: any inliers
+        cyl_refine(x, y, z, inl, best, out);
+        select(out);
+    }
+    std::memcpy(coef, out, sizeof out);
+    for (size_t i = 0; i < inl.size(); ++i) inliers[i] = inl[i];
+    *n_inliers = (int64_t)inl.size();
+    return 1;
+}

@@ -150,6 +150,22 @@ int     orc_sphere_segment(const float* x, const float* y, const float* z, int64
                            int32_t* hypotheses, int32_t* counts, int32_t counts_cap, int32_t* n_counts);
 // SampleConsensusModelSphere::computeModelCoefficients on 4 points (xyz[4][3]); returns 0 when m11 == 0
 int     orc_sphere_from4(const float xyz[12], float coef[4]);
+// The cylinder service's seg.segment (cylinder_segmentation_srv.cpp:110-126): SampleConsensusModelCylinder
+// with normals (2-point samples, the normal-weighted distance), radius limits, optimize (Levenberg-
+// Marquardt on sqrPointToLineDistance - r^2, restated in double; PCL: Eigen's float LM).
+typedef struct {
+    double  threshold;
+    int32_t max_iterations;
+    int32_t optimize;
+    double  probability;
+    double  radius_min, radius_max;
+    double  normal_distance_weight;
+    uint32_t seed;
+    int32_t pad;
+} orc_cylinder_params;
+int     orc_cylinder_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
+                             const float* nz, int64_t n, const orc_cylinder_params* p, int32_t* inliers,
+                             int64_t* n_inliers, float coef[7], float best[7], int32_t* hypotheses);
 // The axis "height" post-processing of the cylinder / cone services (cylinder_segmentation_srv.cpp:129-189,
 // cone_segmentation_srv.cpp:129-189): every point projected on the axis of coef[0..5], the pair (i > j)
 // of projected points farthest apart (first maximum in loop order), and the centroid (mode 0 cylinder:

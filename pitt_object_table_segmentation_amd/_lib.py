@@ -77,6 +77,13 @@ class SphereParams(ctypes.Structure):
                 ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
 
 
+class CylinderParams(ctypes.Structure):
+    """pitt_cylinder_params (include/pitt_seg.h)."""
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("radius_min", ctypes.c_double), ("radius_max", ctypes.c_double),
+                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+
+
 class SupportParams(ctypes.Structure):
     _fields_ = [
         ("min_iterative_cloud_percentage", ctypes.c_float),
@@ -160,6 +167,7 @@ SIGNATURES = {
                                _vp, _vp, _i64p, _i32p]),
     "pitt_sort_pairs": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "pitt_sphere_segment_host": (_i32, [_vp, _f32p, _i64, ctypes.POINTER(SphereParams), _i32p, _i64p, _f32p, _i32p]),
+    "pitt_cylinder_segment": (_i32, [_vp] * 7 + [_i64, ctypes.POINTER(CylinderParams), _vp, _i64p, _f32p, _i32p]),
     "pitt_sphere_segment": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SphereParams), _vp, _i64p, _f32p, _i32p]),
     "pitt_axis_height": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32p, _i32, _vp, _vp, _vp, _f32p, _i32p, _i32p, _f32p]),
     "pitt_support_params_default": (None, [ctypes.POINTER(SupportParams)]),

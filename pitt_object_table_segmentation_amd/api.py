@@ -377,6 +377,26 @@ class Context:
         self._check(rc, "pitt_sphere_segment")
         return inl[:ni.value], coef, hyp.value
 
+    def cylinder_segment(self, x, y, z, nx, ny, nz, threshold: float = 0.008, max_iterations: int = 1000,
+                         optimize: bool = True, radius_min: float = 0.005, radius_max: float = 0.5,
+                         normal_distance_weight: float = 0.001, probability: float = 0.99, seed: int = 12345):
+        """The cylinder service's seg.segment (cylinder_segmentation_srv.cpp:110-126; defaults :23-30) on
+        device tensors (points and normals): (inliers device int32, coefficients[7] or None, hypotheses)."""
+        import torch
+        n = x.numel()
+        prm = L.CylinderParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max,
+                               normal_distance_weight, seed, 0)
+        inl = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
+        ni = ctypes.c_int64()
+        coef = np.zeros(7, np.float32)
+        hyp = ctypes.c_int32()
+        rc = lib.pitt_cylinder_segment(self.h, *(t.data_ptr() for t in (x, y, z, nx, ny, nz)), n, ctypes.byref(prm),
+                                       inl.data_ptr(), ctypes.byref(ni), _fp(coef), ctypes.byref(hyp))
+        if rc == L.PITT_NO_MODEL:
+            return inl[:0], None, hyp.value
+        self._check(rc, "pitt_cylinder_segment")
+        return inl[:ni.value], coef, hyp.value
+
     def axis_height(self, x, y, z, coefficients, mode: int = L.PITT_AXIS_CYLINDER, projected: bool = False):
         """The cylinder / cone services' post-processing (cylinder_segmentation_srv.cpp:129-189,
         cone_segmentation_srv.cpp:129-189) on device tensors: (height, idx1, idx2, centroid[3])

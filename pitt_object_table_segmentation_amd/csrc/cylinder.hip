@@ -1,0 +1,452 @@
+// cylinder.hip -- the cylinder service's seg.segment (cylinder_segmentation_srv.cpp:110-126; SURVEY.md
+// s8f row 4): SampleConsensusModelCylinder with normals, RANSAC over 2-point samples, the radius limits,
+// the normal-weighted distance, optimize, the final selection.  The axis "height" post-processing that
+// follows in the service is pitt_axis_height (primitives.hip).
+//
+// PCL 1.7 semantics (restated in oracle/pitt_oracle.cpp: orc_cylinder_segment); Eigen::Vector4f math is
+// element-wise float, dot / squaredNorm reduced in SSE2 order (A3), normalize() times 1 / norm (A9),
+// normalized() divided by it:
+//   computeModel...    identical points (|dx|, |dy|, |dz| <= FLT_EPSILON) -> skip; the closest points of
+//                      the two normal lines (a, b, c, d, e; den < 1e-8 -> the parallel case), line_pt =
+//                      p1 + n1 + sc n1, line_dir = normalize(p2 + tc n2 - line_pt), r = sqrt of
+//                      sqrPointToLineDistance(p1) (double sqrt of the float quotient), outside the radius
+//                      limits -> skip;
+//   countWithinDistance |w * d_normal + (1 - w) * d_euclid| < threshold in double, d_euclid = |point-to-axis
+//                      distance - r|, d_normal = min(angle, pi - angle) between the normal and the radial
+//                      direction (getAngle3D: acos of the clamped dot of the normalized vectors);
+//   computeModel       the plane loop with w^2;
+//   optimize           Levenberg-Marquardt on OptimizationFunctor's residual sqrPointToLineDistance - r^2 over
+//                      the inliers, the direction normalised as a Vector3f afterwards.  PCL runs Eigen's
+//                      float LM with numerical differences; this runs a double LM (one block, deterministic
+//                      sums) to the least-squares optimum: the axis and radius match PCL's within that
+//                      tolerance, not bit for bit (the point on the axis may slide along it).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "compact.hpp"
+#include "ctx.hpp"
+#include "device_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pitt {
+
+struct CV4 {
+    float v[4];
+};
+__device__ __forceinline__ CV4 cv4(float a, float b, float c, float d = 0.0f) { return CV4{{a, b, c, d}}; }
+__device__ __forceinline__ CV4 cadd(CV4 a, CV4 b) {
+    return cv4(a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]);
+}
+__device__ __forceinline__ CV4 csub(CV4 a, CV4 b) {
+    return cv4(a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2], a.v[3] - b.v[3]);
+}
+__device__ __forceinline__ CV4 cmul(float s, CV4 a) { return cv4(s * a.v[0], s * a.v[1], s * a.v[2], s * a.v[3]); }
+__device__ __forceinline__ float cdot(CV4 a, CV4 b) {  // SSE2 predux: (a0 + a2) + (a1 + a3)
+    return (a.v[0] * b.v[0] + a.v[2] * b.v[2]) + (a.v[1] * b.v[1] + a.v[3] * b.v[3]);
+}
+__device__ __forceinline__ CV4 ccross3(CV4 l, CV4 r) {
+    return cv4(l.v[1] * r.v[2] - l.v[2] * r.v[1], l.v[2] * r.v[0] - l.v[0] * r.v[2], l.v[0] * r.v[1] - l.v[1] * r.v[0],
+               l.v[3] * r.v[3] - l.v[3] * r.v[3]);
+}
+__device__ __forceinline__ CV4 cnormalize(CV4 a) {
+    const float r = 1.0f / sqrtf(cdot(a, a));
+    return cv4(a.v[0] * r, a.v[1] * r, a.v[2] * r, a.v[3] * r);
+}
+__device__ __forceinline__ CV4 cnormalized(CV4 a) {
+    const float nn = sqrtf(cdot(a, a));
+    return cv4(a.v[0] / nn, a.v[1] / nn, a.v[2] / nn, a.v[3] / nn);
+}
+__device__ __forceinline__ double csqr_pt_line(CV4 pt, CV4 lp, CV4 ld) {
+    const CV4 c = ccross3(ld, csub(lp, pt));
+    return (double)(cdot(c, c) / cdot(ld, ld));
+}
+
+struct CylCoef {
+    float c[7];
+    float pad;
+};
+
+__global__ void k_cyl_model(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+                            const float* __restrict__ NX, const float* __restrict__ NY, const float* __restrict__ NZ,
+                            const int32_t* __restrict__ table, int A, double rmin, double rmax,
+                            CylCoef* __restrict__ coef, int32_t* __restrict__ flag) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A) return;
+    const int a = table[2 * t], b = table[2 * t + 1];
+    const float eps = FLT_EPSILON;
+    CylCoef out = {};
+    int ok = 1;
+    if (fabsf(X[a] - X[b]) <= eps && fabsf(Y[a] - Y[b]) <= eps && fabsf(Z[a] - Z[b]) <= eps) {
+        ok = 0;
+    } else {
+        const CV4 p1 = cv4(X[a], Y[a], Z[a]), p2 = cv4(X[b], Y[b], Z[b]);
+        const CV4 n1 = cv4(NX[a], NY[a], NZ[a]), n2 = cv4(NX[b], NY[b], NZ[b]);
+        const CV4 w = csub(cadd(n1, p1), p2);
+        const float A_ = cdot(n1, n1), B = cdot(n1, n2), C = cdot(n2, n2), D = cdot(n1, w), E = cdot(n2, w);
+        const float den = A_ * C - B * B;
+        float sc, tc;
+        if (den < 1e-8) {
+            sc = 0.0f;
+            tc = (B > C ? D / B : E / C);
+        } else {
+            sc = (B * E - C * D) / den;
+            tc = (A_ * E - B * D) / den;
+        }
+        const CV4 lp = cadd(cadd(p1, n1), cmul(sc, n1));
+        const CV4 ld = cnormalize(csub(cadd(p2, cmul(tc, n2)), lp));
+        for (int k = 0; k < 3; ++k) out.c[k] = lp.v[k], out.c[3 + k] = ld.v[k];
+        out.c[6] = (float)sqrt(csqr_pt_line(p1, lp, ld));
+        if (out.c[6] > rmax || out.c[6] < rmin) ok = 0;
+    }
+    coef[t] = out;
+    flag[t] = ok;
+}
+
+__device__ __forceinline__ bool cyl_in(float x, float y, float z, float nx, float ny, float nz, const CylCoef& m,
+                                       double w, double th) {
+    const CV4 lp = cv4(m.c[0], m.c[1], m.c[2]), ld = cv4(m.c[3], m.c[4], m.c[5]);
+    const float ptdotdir = cdot(lp, ld), dirdotdir = 1.0f / cdot(ld, ld);
+    const CV4 pt = cv4(x, y, z), nn = cv4(nx, ny, nz);
+    const double d_euclid = fabs(sqrt(csqr_pt_line(pt, lp, ld)) - (double)m.c[6]);
+    const float k = (cdot(pt, ld) - ptdotdir) * dirdotdir;
+    const CV4 dir = cnormalize(csub(pt, cadd(lp, cmul(k, ld))));
+    double rad = cdot(cnormalized(nn), cnormalized(dir));
+    if (rad < -1.0) rad = -1.0;
+    else if (rad > 1.0) rad = 1.0;
+    double d_normal = fabs(acos(rad));
+    const double alt = M_PI - d_normal;
+    d_normal = alt < d_normal ? alt : d_normal;  // std::min
+    return fabs(w * d_normal + (1 - w) * d_euclid) < th;
+}
+
+__device__ __forceinline__ bool cyl_valid(const CylCoef& m, double rmin, double rmax) {
+    return !((rmin != -DBL_MAX && m.c[6] < rmin) || (rmax != DBL_MAX && m.c[6] > rmax));
+}
+
+__global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, const float* __restrict__ NX,
+                                                   const float* __restrict__ NY, const float* __restrict__ NZ,
+                                                   int64_t n, const CylCoef* __restrict__ coef,
+                                                   const int32_t* __restrict__ flag, int a0, double w, double th,
+                                                   double rmin, double rmax, int32_t* __restrict__ counts) {
+    const int a = a0 + blockIdx.y;
+    if (flag[a] != 1) return;
+    const CylCoef m = coef[a];
+    if (!cyl_valid(m, rmin, rmax)) return;
+    __shared__ int part[4];
+    int cnt = 0;
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        const bool in = i < n && cyl_in(X[i], Y[i], Z[i], NX[i], NY[i], NZ[i], m, w, th);
+        cnt += __popcll(__ballot(in));
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(counts + blockIdx.y, part[0] + part[1] + part[2] + part[3]);
+}
+
+struct CylIn {
+    const float *x, *y, *z, *nx, *ny, *nz;
+    CylCoef m;
+    double w, th;
+    __device__ bool operator()(int64_t i) const { return cyl_in(x[i], y[i], z[i], nx[i], ny[i], nz[i], m, w, th); }
+};
+struct CylWriteIdx {
+    int32_t* out;
+    __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = (int32_t)i; }
+};
+
+// f = |u x (c - p)|^2 / |u|^2 - r^2 and its gradient in (c, u, r)
+__device__ __forceinline__ void cyl_residual(const double* v, float px, float py, float pz, double J[7], double* f) {
+    const double vx = v[0] - px, vy = v[1] - py, vz = v[2] - pz;
+    const double ux = v[3], uy = v[4], uz = v[5];
+    const double wx = uy * vz - uz * vy, wy = uz * vx - ux * vz, wz = ux * vy - uy * vx;
+    const double s = ux * ux + uy * uy + uz * uz, w2 = wx * wx + wy * wy + wz * wz;
+    *f = w2 / s - v[6] * v[6];
+    J[0] = 2.0 * (wy * uz - wz * uy) / s;
+    J[1] = 2.0 * (wz * ux - wx * uz) / s;
+    J[2] = 2.0 * (wx * uy - wy * ux) / s;
+    J[3] = 2.0 * (vy * wz - vz * wy) / s - 2.0 * w2 * ux / (s * s);
+    J[4] = 2.0 * (vz * wx - vx * wz) / s - 2.0 * w2 * uy / (s * s);
+    J[5] = 2.0 * (vx * wy - vy * wx) / s - 2.0 * w2 * uz / (s * s);
+    J[6] = -2.0 * v[6];
+}
+
+constexpr int kCylLmThreads = 1024;
+constexpr int kCylSums = 28 + 7 + 1;
+
+__device__ void cyl_lm_sums(const float* X, const float* Y, const float* Z, const int32_t* inl, int64_t m,
+                            const double* v, double (*red)[kCylSums], double* out) {
+    double acc[kCylSums];
+    for (int q = 0; q < kCylSums; ++q) acc[q] = 0;
+    for (int64_t k = threadIdx.x; k < m; k += kCylLmThreads) {
+        const int id = inl[k];
+        double J[7], f;
+        cyl_residual(v, X[id], Y[id], Z[id], J, &f);
+        int t = 0;
+        for (int a = 0; a < 7; ++a)
+            for (int b = a; b < 7; ++b) acc[t++] += J[a] * J[b];
+        for (int a = 0; a < 7; ++a) acc[28 + a] += J[a] * f;
+        acc[35] += f * f;
+    }
+    for (int q = 0; q < kCylSums; ++q) {
+        double t = acc[q];
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < kCylSums) {
+        double t = 0;
+        for (int w = 0; w < kCylLmThreads / 64; ++w) t += red[w][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+// the oracle's lm_solve<7>: Marquardt damping, the damped 7 x 7 system solved by thread 0
+__global__ __launch_bounds__(kCylLmThreads) void k_cyl_lm(const float* __restrict__ X, const float* __restrict__ Y,
+                                                          const float* __restrict__ Z, const int32_t* __restrict__ inl,
+                                                          int64_t m, CylCoef init, CylCoef* __restrict__ out) {
+    __shared__ double red[kCylLmThreads / 64][kCylSums];
+    __shared__ double cur[kCylSums], trial[kCylSums];
+    __shared__ double xv[7], xn[7];
+    __shared__ int state;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 7; ++k) xv[k] = init.c[k];
+    __syncthreads();
+    cyl_lm_sums(X, Y, Z, inl, m, xv, red, cur);
+    double lambda = 1e-3;
+    for (int it = 0; it < 200; ++it) {
+        bool moved = false, stop = false;
+        for (;;) {
+            if (threadIdx.x == 0) {
+                state = 0;
+                if (!(lambda < 1e10)) state = 3;
+                else {
+                    double M[7][8];
+                    int t = 0;
+                    for (int a = 0; a < 7; ++a)
+                        for (int b = a; b < 7; ++b) M[a][b] = M[b][a] = cur[t++];
+                    for (int a = 0; a < 7; ++a) M[a][a] += lambda * M[a][a] + 1e-30, M[a][7] = -cur[28 + a];
+                    for (int col = 0; col < 7 && state == 0; ++col) {
+                        int piv = col;
+                        for (int r = col + 1; r < 7; ++r)
+                            if (fabs(M[r][col]) > fabs(M[piv][col])) piv = r;
+                        if (M[piv][col] == 0) {
+                            state = 3;
+                            break;
+                        }
+                        if (piv != col)
+                            for (int k = 0; k < 8; ++k) {
+                                const double tt = M[col][k];
+                                M[col][k] = M[piv][k];
+                                M[piv][k] = tt;
+                            }
+                        for (int r = col + 1; r < 7; ++r) {
+                            const double f = M[r][col] / M[col][col];
+                            for (int k = col; k < 8; ++k) M[r][k] -= f * M[col][k];
+                        }
+                    }
+                    if (state == 0) {
+                        double dl[7];
+                        for (int r = 6; r >= 0; --r) {
+                            double acc = M[r][7];
+                            for (int k = r + 1; k < 7; ++k) acc -= M[r][k] * dl[k];
+                            dl[r] = acc / M[r][r];
+                        }
+                        for (int r = 0; r < 7; ++r) xn[r] = xv[r] + dl[r];
+                    }
+                }
+            }
+            __syncthreads();
+            const int st0 = state;
+            __syncthreads();
+            if (st0 == 3) {
+                stop = true;
+                break;
+            }
+            cyl_lm_sums(X, Y, Z, inl, m, xn, red, trial);
+            if (threadIdx.x == 0) {
+                if (trial[35] < cur[35]) {
+                    double step = 0, nx = 0;
+                    for (int r = 0; r < 7; ++r) {
+                        const double d = xn[r] - xv[r];
+                        step += d * d;
+                        nx += xn[r] * xn[r];
+                        xv[r] = xn[r];
+                    }
+                    for (int q = 0; q < kCylSums; ++q) cur[q] = trial[q];
+                    lambda *= 0.1;
+                    state = sqrt(step / (nx + 1e-300)) < 1e-12 ? 3 : 1;
+                } else {
+                    lambda *= 10;
+                    state = 2;
+                }
+            }
+            __syncthreads();
+            const int st1 = state;
+            __syncthreads();
+            if (st1 == 2) continue;
+            moved = true;
+            stop = st1 == 3;
+            break;
+        }
+        __syncthreads();
+        if (!moved || stop) break;
+    }
+    if (threadIdx.x == 0) {
+        CylCoef o = {};
+        for (int k = 0; k < 3; ++k) o.c[k] = (float)xv[k];
+        // Eigen::Vector3f line_dir(...).normalize(): fixed size 3, a0 + (a1 + a2), times 1 / norm
+        const float u0 = (float)xv[3], u1 = (float)xv[4], u2 = (float)xv[5];
+        const float r = 1.0f / sqrtf(u0 * u0 + (u1 * u1 + u2 * u2));
+        o.c[3] = u0 * r;
+        o.c[4] = u1 * r;
+        o.c[5] = u2 * r;
+        o.c[6] = (float)xv[6];
+        *out = o;
+    }
+}
+
+}  // namespace pitt
+
+extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
+                                     const float* ny, const float* nz, int64_t n, const pitt_cylinder_params* p,
+                                     int32_t* inliers, int64_t* n_inliers, float coef_out[7], int32_t* hypotheses) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (!p || !n_inliers || !coef_out || n < 0 || (n > 0 && (!x || !y || !z || !nx || !ny || !nz || !inliers)))
+        return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
+    if (p->max_iterations < 0 || !(p->probability > 0 && p->probability < 1))
+        return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    *n_inliers = 0;
+    if (hypotheses) *hypotheses = 0;
+    for (int k = 0; k < 7; ++k) coef_out[k] = 0;
+    if (n < 2) return PITT_NO_MODEL;  // getSamples: "Can not select 2 unique points"
+    hipStream_t s = ctx->stream;
+    const int64_t max_skip = (int64_t)p->max_iterations * 10;
+    const int64_t A = (int64_t)p->max_iterations + 1 + max_skip;
+    if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
+    const std::vector<int32_t>& tab = sampler_table(ctx, n, p->seed, A, 2);
+    int32_t* dtab = (int32_t*)ctx->buf("cyl_table", (size_t)A * 8);
+    CylCoef* dcoef = (CylCoef*)ctx->buf("cyl_coef", (size_t)A * sizeof(CylCoef));
+    int32_t* dflag = (int32_t*)ctx->buf("cyl_flag", (size_t)A * 4);
+    int32_t* dcnt = (int32_t*)ctx->buf("cyl_cnt", (size_t)A * 4);
+    const int64_t nt = ctiles(n);
+    int32_t* tc = (int32_t*)ctx->buf("cyl_tc", (size_t)(nt + 1) * 4);
+    int32_t* to = (int32_t*)ctx->buf("cyl_to", (size_t)(nt + 1) * 4);
+    CylCoef* dref = (CylCoef*)ctx->buf("cyl_ref", sizeof(CylCoef));
+    if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref) return ctx->fail(PITT_E_NOMEM, "cylinder scratch");
+    PITT_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), (size_t)A * 8, hipMemcpyHostToDevice, s));
+    int rec = ctx->prof_begin("k_cyl_model", (double)A * 48.0);
+    hipLaunchKernelGGL(k_cyl_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, x, y, z, nx, ny, nz, dtab, (int)A,
+                       p->radius_min, p->radius_max, dcoef, dflag);
+    ctx->prof_end(rec);
+    PITT_HIP_TRY(hipGetLastError());
+    std::vector<int32_t> hflag((size_t)A), hcnt;
+    PITT_HIP_TRY(hipMemcpyAsync(hflag.data(), dflag, (size_t)A * 4, hipMemcpyDeviceToHost, s));
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    int iterations = 0, n_best = -INT32_MAX;
+    double k = 1.0;
+    const double log_probability = std::log(1.0 - p->probability);
+    const double one_over_indices = 1.0 / (double)n;
+    int64_t skipped = 0;
+    int best = -1;
+    int64_t a = 0;
+    int chunk = 32;
+    bool done = false;
+    const int64_t ntc = (n + 1023) / 1024;
+    while (!done && a < A) {
+        const int64_t a1 = std::min<int64_t>(A, a + chunk);
+        const int nh = (int)(a1 - a);
+        PITT_HIP_TRY(hipMemsetAsync(dcnt + a, 0, (size_t)nh * 4, s));
+        rec = ctx->prof_begin("k_cyl_count", (double)nh * (double)n * 24.0);
+        hipLaunchKernelGGL(k_cyl_count, dim3((unsigned)ntc, (unsigned)nh), dim3(256), 0, s, x, y, z, nx, ny, nz, n, dcoef,
+                           dflag, (int)a, p->normal_distance_weight, p->threshold, p->radius_min, p->radius_max,
+                           dcnt + a);
+        ctx->prof_end(rec);
+        PITT_HIP_TRY(hipGetLastError());
+        hcnt.resize((size_t)nh);
+        PITT_HIP_TRY(hipMemcpyAsync(hcnt.data(), dcnt + a, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        for (int64_t i = a; i < a1; ++i) {
+            if (!(iterations < k && skipped < max_skip)) {
+                done = true;
+                break;
+            }
+            if (hflag[(size_t)i] == 0) {
+                ++skipped;
+                continue;
+            }
+            const int n_in = hcnt[(size_t)(i - a)];
+            if (n_in > n_best) {
+                n_best = n_in;
+                best = (int)i;
+                const double w = (double)n_best * one_over_indices;
+                double p_no = 1.0 - std::pow(w, 2.0);
+                p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
+                p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
+                k = log_probability / std::log(p_no);
+            }
+            ++iterations;
+            if (iterations > p->max_iterations) {
+                done = true;
+                break;
+            }
+        }
+        a = a1;
+        chunk = std::min(chunk * 2, 256);
+    }
+    if (hypotheses) *hypotheses = iterations;
+    if (best < 0) return PITT_NO_MODEL;
+    CylCoef bc;
+    PITT_HIP_TRY(hipMemcpy(&bc, dcoef + best, sizeof bc, hipMemcpyDeviceToHost));
+    int32_t* hto = (int32_t*)ctx->pinned("cyl_to_h", 16);
+    CylCoef* href = (CylCoef*)ctx->pinned("cyl_ref_h", sizeof(CylCoef));
+    if (!hto || !href) return ctx->fail(PITT_E_NOMEM, "cylinder pinned");
+    const int g = grid_for_tiles(nt);
+    auto select = [&](const CylCoef& m) -> int {
+        const bool valid = !((p->radius_min != -DBL_MAX && m.c[6] < p->radius_min) ||
+                             (p->radius_max != DBL_MAX && m.c[6] > p->radius_max));
+        if (!valid) {
+            *n_inliers = 0;
+            return PITT_OK;
+        }
+        CylIn pred{x, y, z, nx, ny, nz, m, p->normal_distance_weight, p->threshold};
+        hipLaunchKernelGGL(k_pred_count<CylIn>, dim3(g), dim3(kBlock), 0, s, pred, n, tc);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, nt, to);
+        hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, CylWriteIdx{inliers}, n,
+                           to);
+        PITT_HIP_TRY(hipGetLastError());
+        PITT_HIP_TRY(hipMemcpyAsync(hto, to + nt, 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        *n_inliers = hto[0];
+        return PITT_OK;
+    };
+    int rc = select(bc);
+    if (rc != PITT_OK) return rc;
+    CylCoef outc = bc;
+    if (p->optimize && *n_inliers > 0) {
+        rec = ctx->prof_begin("k_cyl_lm", (double)*n_inliers * 12.0);
+        hipLaunchKernelGGL(k_cyl_lm, dim3(1), dim3(kCylLmThreads), 0, s, x, y, z, inliers, *n_inliers, bc, dref);
+        ctx->prof_end(rec);
+        PITT_HIP_TRY(hipGetLastError());
+        PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(CylCoef), hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        outc = *href;
+        rc = select(outc);
+        if (rc != PITT_OK) return rc;
+    }
+    for (int r = 0; r < 7; ++r) coef_out[r] = outc.c[r];
+    return PITT_OK;
+}

@@ -335,3 +335,36 @@ def sphere_segment(x, y, z, params=None, counts_cap=20000):
                               _fp(best), ctypes.byref(hyp), _ip(cnt), counts_cap, ctypes.byref(nc))
     return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value,
             "counts": cnt[:min(nc.value, counts_cap)].copy()}
+
+
+class CylinderParams(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("radius_min", ctypes.c_double), ("radius_max", ctypes.c_double),
+                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+
+
+def cylinder_params(threshold=0.008, max_iterations=1000, optimize=True, radius_min=0.005, radius_max=0.5,
+                    normal_distance_weight=0.001, probability=0.99, seed=12345):
+    """cylinder_segmentation_srv.cpp:23-30 defaults."""
+    return CylinderParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max,
+                          normal_distance_weight, seed, 0)
+
+
+O.orc_cylinder_segment.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.POINTER(CylinderParams)] + \
+    [ctypes.c_void_p] * 5
+
+
+def cylinder_segment(xyz, nrm, params=None):
+    """The cylinder service's seg.segment restated: dict(ok, inliers, coef[7], best[7], hypotheses)."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    nrm = np.ascontiguousarray(nrm, np.float32)
+    cols = [np.ascontiguousarray(a[:, k]) for a in (xyz, nrm) for k in range(3)]
+    n = len(xyz)
+    p = params or cylinder_params()
+    inl = np.empty(max(n, 1), np.int32)
+    ni = ctypes.c_int64()
+    coef, best = np.zeros(7, np.float32), np.zeros(7, np.float32)
+    hyp = ctypes.c_int32()
+    ok = O.orc_cylinder_segment(*(_fp(c) for c in cols), n, ctypes.byref(p), _ip(inl), ctypes.byref(ni), _fp(coef),
+                                _fp(best), ctypes.byref(hyp))
+    return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value}
