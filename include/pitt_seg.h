@@ -317,6 +317,10 @@ typedef struct {
 int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
                           const float* ny, const float* nz, int64_t n, const pitt_cylinder_params* params,
                           int32_t* inliers, int64_t* n_inliers, float coef[7], int32_t* hypotheses);
+/* The same on host memory: points as PointXYZ (16-byte stride), normals as (nx, ny, nz) triples. */
+int pitt_cylinder_segment_host(pitt_ctx* ctx, const float* xyz16, const float* normals3, int64_t n,
+                               const pitt_cylinder_params* params, int32_t* inliers, int64_t* n_inliers,
+                               float coef[7], int32_t* hypotheses);
 
 /* The post-processing of the cylinder and cone services once PCL has fitted the model
  * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).
@@ -332,6 +336,9 @@ enum { PITT_AXIS_CYLINDER = 0, PITT_AXIS_CONE = 1 };
 int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                      const float coef[6], int32_t mode, float* px, float* py, float* pz, float* height,
                      int32_t* idx1, int32_t* idx2, float centroid[3]);
+/* The same on a host PointXYZ cloud (16-byte stride). */
+int pitt_axis_height_host(pitt_ctx* ctx, const float* xyz16, int64_t n, const float coef[6], int32_t mode,
+                          float* height, int32_t* idx1, int32_t* idx2, float centroid[3]);
 
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };

@@ -9,6 +9,7 @@
  *   pitt_srv_clusterize       <-> clusterize            cluster_segmentation_srv.cpp:38
  *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
  *   pitt_srv_ransac_sphere    <-> ransacSphereDetection sphere_segmentation_srv.cpp:29
+ *   pitt_srv_ransac_cylinder  <-> ransacCylinderDetaction cylinder_segmentation_srv.cpp:82
  *   pitt_srv_call_ransac_plane <-> callRansacPlaneSegmentation  ransac_segmentation.cpp:175-199
  *   pitt_srv_arbitrate        <-> clustersAcquisition's arbitration  ransac_segmentation.cpp:265-302
  * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
@@ -59,6 +60,13 @@ int pitt_srv_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int64_t 
 int pitt_srv_ransac_sphere(pitt_srv* srv, const float* xyz16, int64_t n, int64_t n_normals,
                            int32_t* inliers_out /* cap n */, int64_t* n_inliers,
                            float* coefficients_out /* cap 4 */, int32_t* n_coefficients, float centroid_out[3]);
+
+/* The cylinder service: normals3 = (nx, ny, nz) per point (needed when n_normals == n); inliers (index 0
+ * dropped, Q1); coefficients = the 7 model values (none without a model) followed by the axis height
+ * (-1 without inliers); centroid_out = the midpoint of the farthest projected pair (0 without inliers). */
+int pitt_srv_ransac_cylinder(pitt_srv* srv, const float* xyz16, int64_t n, const float* normals3, int64_t n_normals,
+                             int32_t* inliers_out /* cap n */, int64_t* n_inliers,
+                             float* coefficients_out /* cap 8 */, int32_t* n_coefficients, float centroid_out[3]);
 
 /* callRansacPlaneSegmentation, ransac_segmentation.cpp:175-199: the plane service, accepted (1) only
  * when its response holds more than 0 inliers (Q2: the min-inliers parameter is read but unused);

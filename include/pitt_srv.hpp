@@ -34,6 +34,7 @@ struct PointCloud {
 // sensor_msgs/PointCloud2 carrying pcl::Normal (only its size matters on the plane path, A1).
 struct NormalCloud {
     size_t n = 0;
+    std::vector<float> data;  // (nx, ny, nz) per point when the handler reads the normals (cylinder)
     size_t size() const { return n; }
 };
 
@@ -122,6 +123,15 @@ const std::string PARAM_NAME_PLANE_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_s
 const std::string PARAM_NAME_PLANE_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/plane_segmentation/max_opening_angle_deg";
 const std::string PARAM_NAME_PLANE_MIN_INLIERS = "/pitt/srv/plane_segmentation/min_inliers";
 const std::string SRV_NAME_RANSAC_SPHERE_FILTER = "sphere_segmentation_srv";
+const std::string SRV_NAME_RANSAC_CYLINDER_FILTER = "cylinder_segmentation_srv";
+const std::string PARAM_NAME_CYLINDER_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/cylinder_segmentation/normal_distance_weight";
+const std::string PARAM_NAME_CYLINDER_DISTANCE_TH = "/pitt/srv/cylinder_segmentation/distance_th";
+const std::string PARAM_NAME_CYLINDER_MAX_ITERATION_LIMIT = "/pitt/srv/cylinder_segmentation/max_iter_limit";
+const std::string PARAM_NAME_CYLINDER_MIN_RADIUS_LIMIT = "/pitt/srv/cylinder_segmentation/min_radius_limit";
+const std::string PARAM_NAME_CYLINDER_MAX_RADIUS_LIMIT = "/pitt/srv/cylinder_segmentation/max_radius_limit";
+const std::string PARAM_NAME_CYLINDER_EPS_ANGLE_TH = "/pitt/srv/cylinder_segmentation/eps_angle_th";
+const std::string PARAM_NAME_CYLINDER_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/cylinder_segmentation/min_opening_angle_deg";
+const std::string PARAM_NAME_CYLINDER_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/cylinder_segmentation/max_opening_angle_deg";
 const std::string PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/sphere_segmentation/normal_distance_weight";
 const std::string PARAM_NAME_SPHERE_DISTANCE_TH = "/pitt/srv/sphere_segmentation/distance_th";
 const std::string PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT = "/pitt/srv/sphere_segmentation/max_iter_limit";
@@ -200,6 +210,9 @@ public:
     // plane_segmentation_srv.cpp:27
     bool ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
                               pitt_msgs::PrimitiveSegmentation::Response& res);
+    // cylinder_segmentation_srv.cpp:82-216 (the model, then the axis height and centroid)
+    bool ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                                 pitt_msgs::PrimitiveSegmentation::Response& res);
     // sphere_segmentation_srv.cpp:29-96
     bool ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
                                pitt_msgs::PrimitiveSegmentation::Response& res);

@@ -210,6 +210,10 @@ SIGNATURES.update({
     "pitt_srv_param_set_list": (_i32, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i32]),
     "pitt_srv_param_erase": (_i32, [_vp, ctypes.c_char_p]),
     "pitt_srv_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_srv_ransac_cylinder": (_i32, [_vp, _f32p, _i64, _f32p, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_cylinder_segment_host": (_i32, [_vp, _f32p, _f32p, _i64, ctypes.POINTER(CylinderParams), _i32p, _i64p, _f32p,
+                                          _i32p]),
+    "pitt_axis_height_host": (_i32, [_vp, _f32p, _i64, _f32p, _i32, _f32p, _i32p, _i32p, _f32p]),
     "pitt_srv_ransac_sphere": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
     "pitt_srv_call_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p]),
     "pitt_srv_arbitrate": (_i32, [_i64, _i64, _i64, _i64]),

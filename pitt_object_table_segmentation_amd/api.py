@@ -534,6 +534,21 @@ class Services:
                                                  ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)), "ransac_sphere")
         return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
 
+    def ransac_cylinder(self, cloud: np.ndarray, normals: np.ndarray, n_normals: Optional[int] = None):
+        """ransacCylinderDetaction (cylinder_segmentation_srv.cpp:82-216): (ok, inliers (index 0 dropped),
+        coefficients (7 model values, then the height), centroid)."""
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        nrm = np.ascontiguousarray(np.asarray(normals, np.float32).reshape(-1, 3))
+        inl = np.empty(max(n, 1), np.int32)
+        ni, nc = ctypes.c_int64(), ctypes.c_int32()
+        co = np.zeros(8, np.float32)
+        ce = np.zeros(3, np.float32)
+        ok = self._rc(lib.pitt_srv_ransac_cylinder(self.h, _fp(c), n, _fp(nrm), n if n_normals is None else n_normals,
+                                                   _ip(inl), ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)),
+                      "ransac_cylinder")
+        return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
+
     def call_ransac_plane(self, cloud: np.ndarray, n_normals: Optional[int] = None):
         """callRansacPlaneSegmentation (ransac_segmentation.cpp:175-199): (accepted, inliers, coefficients)."""
         c = _cloud16(cloud)

@@ -450,3 +450,35 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
     for (int r = 0; r < 7; ++r) coef_out[r] = outc.c[r];
     return PITT_OK;
 }
+
+// Host-memory form (the service handlers' clouds): points as PointXYZ (16-byte stride), normals as
+// (nx, ny, nz) triples; staged into the context's device buffers, the inliers copied back.
+extern "C" int pitt_cylinder_segment_host(pitt_ctx* ctx, const float* xyz16, const float* normals3, int64_t n,
+                                          const pitt_cylinder_params* params, int32_t* inliers, int64_t* n_inliers,
+                                          float coef[7], int32_t* hypotheses) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (n < 0 || (n > 0 && (!xyz16 || !normals3 || !inliers)) || !n_inliers || !coef)
+        return ctx->fail(PITT_E_INVALID, "null argument");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    const size_t nb = (size_t)std::max<int64_t>(n, 1) * 4;
+    float* d = (float*)ctx->buf("cyl_hsoa", nb * 6);
+    int32_t* di = (int32_t*)ctx->buf("cyl_hi", nb);
+    if (!d || !di) return ctx->fail(PITT_E_NOMEM, "cylinder staging");
+    std::vector<float> soa((size_t)std::max<int64_t>(n, 1) * 6);
+    for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            soa[(size_t)(k * n + i)] = xyz16[4 * i + k];
+            soa[(size_t)((3 + k) * n + i)] = normals3[3 * i + k];
+        }
+    hipStream_t s = ctx->stream;
+    if (n > 0) PITT_HIP_TRY(hipMemcpyAsync(d, soa.data(), (size_t)n * 24, hipMemcpyHostToDevice, s));
+    const int rc = pitt_cylinder_segment(ctx, d, d + n, d + 2 * n, d + 3 * n, d + 4 * n, d + 5 * n, n, params, di,
+                                         n_inliers, coef, hypotheses);
+    if (rc < 0) return rc;
+    if (*n_inliers > 0) {
+        PITT_HIP_TRY(hipMemcpyAsync(inliers, di, (size_t)*n_inliers * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+    }
+    return rc;
+}

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "ctx.hpp"
 #include "device_common.hpp"
@@ -320,4 +321,22 @@ extern "C" int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, c
     *idx2 = hout->idx2;
     for (int k = 0; k < 3; ++k) centroid[k] = hout->centroid[k];
     return PITT_OK;
+}
+
+// Host-memory form: a PointXYZ cloud (16-byte stride) staged into the context's device buffers.
+extern "C" int pitt_axis_height_host(pitt_ctx* ctx, const float* xyz16, int64_t n, const float coef[6], int32_t mode,
+                                     float* height, int32_t* idx1, int32_t* idx2, float centroid[3]) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (n < 0 || (n > 0 && !xyz16)) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    const size_t nb = (size_t)std::max<int64_t>(n, 1) * 4;
+    float* d = (float*)ctx->buf("ax_hsoa", nb * 3);
+    if (!d) return ctx->fail(PITT_E_NOMEM, "axis height staging");
+    std::vector<float> soa((size_t)std::max<int64_t>(n, 1) * 3);
+    for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) soa[(size_t)(k * n + i)] = xyz16[4 * i + k];
+    if (n > 0) PITT_HIP_TRY(hipMemcpyAsync(d, soa.data(), (size_t)n * 12, hipMemcpyHostToDevice, ctx->stream));
+    return pitt_axis_height(ctx, d, d + n, d + 2 * n, n, coef, mode, nullptr, nullptr, nullptr, height, idx1, idx2,
+                            centroid);
 }

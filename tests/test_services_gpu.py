@@ -167,3 +167,23 @@ def test_sphere_handler(srv):
     # normals of the wrong size: PCL clears the outputs
     ok, inl, coef, centroid = srv.ransac_sphere(xyz, n_normals=len(xyz) - 1)
     assert ok and len(inl) == 0 and len(coef) == 0 and not centroid.any()
+
+
+def test_cylinder_handler(srv):
+    """ransacCylinderDetaction (cylinder_segmentation_srv.cpp:82-216): the model, then the axis height
+    pushed after the 7 coefficients and the centroid of the farthest projected pair (:129-200)."""
+    from test_cylinder import cylinder_scene, same_line
+    P, N, _ = cylinder_scene(1500, 500, 11)
+    ok, inl, coef, centroid = srv.ransac_cylinder(P, N)
+    want = orc.cylinder_segment(P, N)
+    assert ok and want["ok"] and len(coef) == 8
+    assert same_line(coef[:7].astype(np.float64), want["coef"].astype(np.float64), ang=1e-9, dist=1e-6, rad=1e-6)
+    # the post-processing on the handler's own coefficients: bit-exact against the restatement
+    h, i1, i2, cen, _ = orc.axis_height(*P.T, coef[:6], 0)
+    assert np.float32(coef[7]).view(np.int32) == np.float32(h).view(np.int32)
+    assert np.array_equal(centroid.view(np.int32), cen.view(np.int32))
+    ref = want["inliers"][want["inliers"] != 0]
+    assert len(np.setxor1d(inl, ref)) <= max(2, len(ref) // 2000) and 0 not in inl
+    # normals of the wrong size: PCL clears the outputs; the height stays -1 (:132, :195)
+    ok, inl, coef, centroid = srv.ransac_cylinder(P, N, n_normals=len(P) - 1)
+    assert ok and len(inl) == 0 and list(coef) == [-1.0] and not centroid.any()
