@@ -1605,3 +1605,210 @@ extern "C" int orc_cylinder_segment(const float* x, const float* y, const float*
     *n_inliers = (int64_t)inl.size();
     return 1;
 }
+
+// ------------------------------------------------------------------------------------------
+// Cone (PCL 1.7 sample_consensus/impl/sac_model_cone.hpp; SACSegmentationFromNormals::initSACModel sets
+// the opening-angle limits and the eps angle, not the radius limits).  Vector4f arithmetic as for the
+// cylinder.  A7: acosf / sinf / cosf taken as correctly rounded (float)f((double)x); tan(angle) in
+// double.
+namespace {
+inline float acosf_cr(float a) { return (float)std::acos((double)a); }
+inline float sinf_cr(float a) { return (float)std::sin((double)a); }
+inline float cosf_cr(float a) { return (float)std::cos((double)a); }
+
+// getAngle3D with Eigen's normalized(): 3.2 divides by the norm (0 / 0 = NaN); >= 3.3 keeps a zero vector
+inline V4 normalized_e(V4 a, int eigen33) {
+    if (eigen33 && !(dot(a, a) > 0.0f)) return a;
+    return normalized(a);
+}
+inline double angle3d_e(V4 a, V4 b, int eigen33) {
+    double rad = dot(normalized_e(a, eigen33), normalized_e(b, eigen33));
+    if (rad < -1.0) rad = -1.0;
+    else if (rad > 1.0) rad = 1.0;
+    return std::acos(rad);
+}
+
+bool cone_from3(const V4 p[3], const V4 nn[3], double amin, double amax, float c[7]) {
+    const V4 o12 = cross3(nn[0], nn[1]), o23 = cross3(nn[1], nn[2]), o31 = cross3(nn[2], nn[0]);
+    const float den = dot(nn[0], o23);
+    const float d1 = dot(p[0], nn[0]), d2 = dot(p[1], nn[1]), d3 = dot(p[2], nn[2]);
+    const V4 num = add(add(mul(d1, o23), mul(d2, o31)), mul(d3, o12));
+    const V4 apex = v4(num.v[0] / den, num.v[1] / den, num.v[2] / den, num.v[3] / den);
+    V4 ap[3], np[3];
+    for (int k = 0; k < 3; ++k) {
+        ap[k] = sub(p[k], apex);
+        const V4 u = normalized(ap[k]);  // ap / ap.norm()
+        np[k] = add(apex, u);
+    }
+    const V4 axis = normalize(cross3(sub(np[1], np[0]), sub(np[2], np[0])));
+    float acc = 0.0f;
+    for (int k = 0; k < 3; ++k) acc = acc + acosf_cr(dot(normalize(ap[k]), axis));
+    const float ang = acc / 3.0f;
+    for (int k = 0; k < 3; ++k) c[k] = apex.v[k], c[3 + k] = axis.v[k];
+    c[6] = ang;
+    if (c[6] != -DBL_MAX && c[6] < amin) return false;
+    if (c[6] != DBL_MAX && c[6] > amax) return false;
+    return true;
+}
+
+bool cone_valid(const float c[7], const orc_cone_params* p) {
+    if (p->eps_angle > 0.0) {
+        const V4 coeff = v4(c[3], c[4], c[5]), ax = v4(p->axis[0], p->axis[1], p->axis[2]);
+        double d = std::fabs(angle3d_e(ax, coeff, p->eigen33));
+        d = std::min(d, M_PI - d);
+        if (d > p->eps_angle) return false;
+    }
+    if (c[6] != -DBL_MAX && c[6] < p->min_angle) return false;
+    if (c[6] != DBL_MAX && c[6] > p->max_angle) return false;
+    return true;
+}
+
+inline bool cone_in(const float* x, const float* y, const float* z, const float* nx, const float* ny, const float* nz,
+                    int64_t i, const float c[7], const orc_cone_params* p) {
+    const V4 apex = v4(c[0], c[1], c[2]), ad = v4(c[3], c[4], c[5]);
+    const float ang = c[6];
+    const float apexdotdir = dot(apex, ad), dirdotdir = 1.0f / dot(ad, ad);
+    const V4 pt = v4(x[i], y[i], z[i]), nn = v4(nx[i], ny[i], nz[i]);
+    const float k = (dot(pt, ad) - apexdotdir) * dirdotdir;
+    const V4 proj = add(apex, mul(k, ad));
+    const V4 dir = normalize(sub(pt, proj));
+    V4 h = sub(apex, proj);
+    const double radius = std::tan((double)ang) * (double)std::sqrt(dot(h, h));
+    h = normalize(h);
+    const V4 cn = add(mul(sinf_cr(ang), h), mul(cosf_cr(ang), dir));
+    const double d_euclid = std::fabs(std::sqrt(sqr_pt_line(pt, apex, ad)) - radius);
+    double d_normal = std::fabs(angle3d_e(nn, cn, p->eigen33));
+    d_normal = std::min(d_normal, M_PI - d_normal);
+    const double w = p->normal_distance_weight;
+    return std::fabs(w * d_normal + (1 - w) * d_euclid) < p->threshold;
+}
+
+// f = |v|^2 - (1 + tan^2 a) (u.v)^2 / |u|^2 with v = apex - p: the functor's sqrPointToLineDistance -
+// (tan(a) |apex - proj|)^2 (Lagrange's identity), and its gradient in (apex, u, a)
+inline void cone_residual(const double* q, float px, float py, float pz, double J[7], double* f) {
+    const double vx = q[0] - px, vy = q[1] - py, vz = q[2] - pz;
+    const double ux = q[3], uy = q[4], uz = q[5];
+    const double s = ux * ux + uy * uy + uz * uz, g = ux * vx + uy * vy + uz * vz;
+    const double t = std::tan(q[6]), K = 1.0 + t * t;
+    *f = (vx * vx + vy * vy + vz * vz) - K * g * g / s;
+    const double a = 2.0 * K * g / s;
+    J[0] = 2.0 * vx - a * ux;
+    J[1] = 2.0 * vy - a * uy;
+    J[2] = 2.0 * vz - a * uz;
+    J[3] = -a * (vx - g * ux / s);
+    J[4] = -a * (vy - g * uy / s);
+    J[5] = -a * (vz - g * uz / s);
+    J[6] = -(g * g / s) * 2.0 * t * K;
+}
+
+// optimizeModelCoefficients: Eigen's LM refuses fewer residuals than parameters (m < n:
+// ImproperInputParameters, the coefficients unchanged); the direction is normalised either way.
+void cone_refine(const float* x, const float* y, const float* z, const std::vector<int>& inl, const float in[7],
+                 float out[7]) {
+    double q[7];
+    for (int k = 0; k < 7; ++k) q[k] = in[k];
+    if (inl.size() >= 7) {
+        auto sums = [&](const double* v, double* jtj, double* jtr, double* cost) {
+            for (int k = 0; k < 28; ++k) jtj[k] = 0;
+            for (int k = 0; k < 7; ++k) jtr[k] = 0;
+            *cost = 0;
+            for (int id : inl) {
+                double J[7], f;
+                cone_residual(v, x[id], y[id], z[id], J, &f);
+                int t = 0;
+                for (int a = 0; a < 7; ++a)
+                    for (int b = a; b < 7; ++b) jtj[t++] += J[a] * J[b];
+                for (int a = 0; a < 7; ++a) jtr[a] += J[a] * f;
+                *cost += f * f;
+            }
+        };
+        lm_solve<7>(q, sums);
+    }
+    for (int k = 0; k < 3; ++k) out[k] = (float)q[k];
+    const float u0 = (float)q[3], u1 = (float)q[4], u2 = (float)q[5];
+    const float r = 1.0f / std::sqrt(u0 * u0 + (u1 * u1 + u2 * u2));
+    out[3] = u0 * r;
+    out[4] = u1 * r;
+    out[5] = u2 * r;
+    out[6] = (float)q[6];
+}
+}  // namespace
+
+extern "C" int orc_cone_from3(const float xyz[9], const float nrm[9], double min_angle, double max_angle,
+                              float coef[7]) {
+    V4 p[3], nn[3];
+    for (int k = 0; k < 3; ++k) {
+        p[k] = v4(xyz[3 * k], xyz[3 * k + 1], xyz[3 * k + 2]);
+        nn[k] = v4(nrm[3 * k], nrm[3 * k + 1], nrm[3 * k + 2]);
+    }
+    return cone_from3(p, nn, min_angle, max_angle, coef) ? 1 : 0;
+}
+
+extern "C" int orc_cone_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
+                                const float* nz, int64_t n, const orc_cone_params* p, int32_t* inliers,
+                                int64_t* n_inliers, float coef[7], float best_out[7], int32_t* hypotheses) {
+    *n_inliers = 0;
+    *hypotheses = 0;
+    if (n < 3) return 0;  // getSamples: "Can not select 3 unique points"
+    std::mt19937 mt(p->seed);
+    std::vector<int> sh((size_t)n);
+    std::iota(sh.begin(), sh.end(), 0);
+    int iterations = 0, n_best = -std::numeric_limits<int>::max();
+    double k = 1.0;
+    const double log_probability = std::log(1.0 - p->probability);
+    const double one_over_indices = 1.0 / (double)n;
+    unsigned skipped = 0;
+    const unsigned max_skip = (unsigned)p->max_iterations * 10u;
+    bool have = false;
+    float best[7] = {0, 0, 0, 0, 0, 0, 0};
+    while (iterations < k && skipped < max_skip) {
+        for (unsigned i = 0; i < 3; ++i) std::swap(sh[i], sh[i + ((size_t)(mt() >> 1) % ((size_t)n - i))]);
+        V4 ps[3], ns[3];
+        for (int q = 0; q < 3; ++q) {
+            const int id = sh[q];
+            ps[q] = v4(x[id], y[id], z[id]);
+            ns[q] = v4(nx[id], ny[id], nz[id]);
+        }
+        float m[7];
+        if (!cone_from3(ps, ns, p->min_angle, p->max_angle, m)) {
+            ++skipped;
+            continue;
+        }
+        int n_in = 0;
+        if (cone_valid(m, p))
+            for (int64_t i = 0; i < n; ++i) n_in += cone_in(x, y, z, nx, ny, nz, i, m, p);
+        if (n_in > n_best) {
+            n_best = n_in;
+            have = true;
+            std::memcpy(best, m, sizeof m);
+            const double w = (double)n_best * one_over_indices;
+            double p_no = 1.0 - std::pow(w, 3.0);
+            p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
+            p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
+            k = log_probability / std::log(p_no);
+        }
+        ++iterations;
+        if (iterations > p->max_iterations) break;
+    }
+    *hypotheses = iterations;
+    if (!have) return 0;
+    std::memcpy(best_out, best, sizeof best);
+    std::vector<int> inl;
+    auto select = [&](const float* m) {
+        inl.clear();
+        if (!cone_valid(m, p)) return;
+        for (int64_t i = 0; i < n; ++i)
+            if (cone_in(x, y, z, nx, ny, nz, i, m, p)) inl.push_back((int)i);
+    };
+    select(best);
+    float out[7];
+    std::memcpy(out, best, sizeof out);
+    if (p->optimize && !inl.empty()) {  // optimizeModelCoefficients: "Inliers vector empty" returns unchanged
+        cone_refine(x, y, z, inl, best, out);
+        select(out);
+    }
+    std::memcpy(coef, out, sizeof out);
+    for (size_t i = 0; i < inl.size(); ++i) inliers[i] = inl[i];
+    *n_inliers = (int64_t)inl.size();
+    return 1;
+}

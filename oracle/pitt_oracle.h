@@ -166,6 +166,32 @@ typedef struct {
 int     orc_cylinder_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
                              const float* nz, int64_t n, const orc_cylinder_params* p, int32_t* inliers,
                              int64_t* n_inliers, float coef[7], float best[7], int32_t* hypotheses);
+// The cone service's seg.segment (cone_segmentation_srv.cpp:111-127): SampleConsensusModelCone with
+// normals (3-point samples: the apex as the intersection of the three tangent planes, the axis as the
+// normal of the plane through the unit apex-to-sample offsets, the opening angle as the mean of their
+// angles to it), the opening-angle limits, isModelValid's eps angle against axis[3] (the service sets
+// none: the zero vector), the normal-weighted distance, optimize (Levenberg-Marquardt in double on
+// OptimizationFunctor's residual sqrPointToLineDistance - (tan(angle) |apex - proj|)^2; PCL: Eigen's
+// float LM).  eigen33: 0 = Eigen 3.2's normalized() (a zero vector gives NaN, so the eps check against
+// a zero axis never rejects); 1 = Eigen >= 3.3 (a zero vector stays zero: the angle is pi/2).
+typedef struct {
+    double  threshold;
+    int32_t max_iterations;
+    int32_t optimize;
+    double  probability;
+    double  normal_distance_weight;
+    double  min_angle, max_angle;  // radians
+    double  eps_angle;
+    float   axis[3];
+    int32_t eigen33;
+    uint32_t seed;
+    int32_t pad;
+} orc_cone_params;
+int     orc_cone_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
+                         const float* nz, int64_t n, const orc_cone_params* p, int32_t* inliers,
+                         int64_t* n_inliers, float coef[7], float best[7], int32_t* hypotheses);
+// SampleConsensusModelCone::computeModelCoefficients on 3 points + normals; returns 0 outside the angle limits
+int     orc_cone_from3(const float xyz[9], const float nrm[9], double min_angle, double max_angle, float coef[7]);
 // The axis "height" post-processing of the cylinder / cone services (cylinder_segmentation_srv.cpp:129-189,
 // cone_segmentation_srv.cpp:129-189): every point projected on the axis of coef[0..5], the pair (i > j)
 // of projected points farthest apart (first maximum in loop order), and the centroid (mode 0 cylinder:
