@@ -26,6 +26,7 @@
  *        src/point_cloud_library/pc_manager.cpp:68-78
  *   pitt_sphere_segment           replaces  seg.segment in src/segmentation_services/sphere_segmentation_srv.cpp:57-73
  *   pitt_cylinder_segment         replaces  seg.segment in src/segmentation_services/cylinder_segmentation_srv.cpp:110-126
+ *   pitt_cone_segment             replaces  seg.segment in src/segmentation_services/cone_segmentation_srv.cpp:111-127
  *   pitt_axis_height              replaces  the projection + O(n^2) height loop after seg.segment in
  *        src/segmentation_services/cylinder_segmentation_srv.cpp:129-189 and
  *        src/segmentation_services/cone_segmentation_srv.cpp:129-189
@@ -321,6 +322,40 @@ int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const f
 int pitt_cylinder_segment_host(pitt_ctx* ctx, const float* xyz16, const float* normals3, int64_t n,
                                const pitt_cylinder_params* params, int32_t* inliers, int64_t* n_inliers,
                                float coef[7], int32_t* hypotheses);
+
+/* The cone service's seg.segment (cone_segmentation_srv.cpp:111-127): SampleConsensusModelCone with normals
+ * (3-point samples: the apex where the three tangent planes meet, the axis normal to the plane through the
+ * unit apex-to-sample offsets, the opening angle the mean of their acosf to it), the opening-angle limits,
+ * isModelValid's eps angle against `axis` (the service sets none: zero), the normal-weighted distance
+ * |w * angle(normal, cone normal) + (1 - w) * |axis distance - tan(angle) * height|| < threshold, PCL's
+ * computeModel loop with w^3; optimize: the least-squares refinement of OptimizationFunctor's residual
+ * sqrPointToLineDistance - (tan(angle) |apex - proj|)^2 (PCL: Eigen's float Levenberg-Marquardt -- equal
+ * within its tolerance; fewer than 7 inliers leave the model unchanged, as Eigen's LM refuses m < n), the
+ * direction normalised, the final selection.  SACSegmentation's radius limits do not reach SACMODEL_CONE.
+ * x/y/z, nx/ny/nz: device SoA of n points; inliers (device, capacity n) ascending; coef[7] = apex,
+ * axis direction, opening angle.  PITT_OK with a model, PITT_NO_MODEL without. */
+typedef struct {
+    double   threshold;               /* 0.0055 (cone_segmentation_srv.cpp:25) */
+    int32_t  max_iterations;          /* 1000 (:28) */
+    int32_t  optimize;                /* 1 (:115) */
+    double   probability;             /* 0.99 */
+    double   normal_distance_weight;  /* 0.0006 (:24) */
+    double   min_angle, max_angle;    /* radians: 10 and 170 degrees (:30-31, converted at :124) */
+    double   eps_angle;               /* 0.4 (:29, set at :125) */
+    float    axis[3];                 /* 0, 0, 0: the service sets no axis */
+    int32_t  eigen33;                 /* 0: Eigen 3.2's normalized() (0 / 0 = NaN: the eps check against the
+                                         zero axis never rejects); 1: Eigen >= 3.3 (a zero vector stays zero:
+                                         the angle is pi/2, so eps_angle 0.4 rejects every model) */
+    uint32_t seed;                    /* 12345 */
+    int32_t  pad;
+} pitt_cone_params;
+int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
+                      const float* ny, const float* nz, int64_t n, const pitt_cone_params* params,
+                      int32_t* inliers, int64_t* n_inliers, float coef[7], int32_t* hypotheses);
+/* The same on host memory: points as PointXYZ (16-byte stride), normals as (nx, ny, nz) triples. */
+int pitt_cone_segment_host(pitt_ctx* ctx, const float* xyz16, const float* normals3, int64_t n,
+                           const pitt_cone_params* params, int32_t* inliers, int64_t* n_inliers, float coef[7],
+                           int32_t* hypotheses);
 
 /* The post-processing of the cylinder and cone services once PCL has fitted the model
  * (cylinder_segmentation_srv.cpp:129-189, cone_segmentation_srv.cpp:129-189; the helpers :53-79).

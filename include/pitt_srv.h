@@ -10,6 +10,7 @@
  *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
  *   pitt_srv_ransac_sphere    <-> ransacSphereDetection sphere_segmentation_srv.cpp:29
  *   pitt_srv_ransac_cylinder  <-> ransacCylinderDetaction cylinder_segmentation_srv.cpp:82
+ *   pitt_srv_ransac_cone      <-> ransacConeDetaction     cone_segmentation_srv.cpp:83
  *   pitt_srv_call_ransac_plane <-> callRansacPlaneSegmentation  ransac_segmentation.cpp:175-199
  *   pitt_srv_arbitrate        <-> clustersAcquisition's arbitration  ransac_segmentation.cpp:265-302
  * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
@@ -67,6 +68,13 @@ int pitt_srv_ransac_sphere(pitt_srv* srv, const float* xyz16, int64_t n, int64_t
 int pitt_srv_ransac_cylinder(pitt_srv* srv, const float* xyz16, int64_t n, const float* normals3, int64_t n_normals,
                              int32_t* inliers_out /* cap n */, int64_t* n_inliers,
                              float* coefficients_out /* cap 8 */, int32_t* n_coefficients, float centroid_out[3]);
+
+/* The cone service: as the cylinder's; coefficients = apex, axis direction, opening angle (none without
+ * a model) followed by the axis height (-1 without inliers); centroid_out = apex + 3/4 height along the
+ * unit axis (0 without inliers). */
+int pitt_srv_ransac_cone(pitt_srv* srv, const float* xyz16, int64_t n, const float* normals3, int64_t n_normals,
+                         int32_t* inliers_out /* cap n */, int64_t* n_inliers, float* coefficients_out /* cap 8 */,
+                         int32_t* n_coefficients, float centroid_out[3]);
 
 /* callRansacPlaneSegmentation, ransac_segmentation.cpp:175-199: the plane service, accepted (1) only
  * when its response holds more than 0 inliers (Q2: the min-inliers parameter is read but unused);

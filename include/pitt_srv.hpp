@@ -132,6 +132,16 @@ const std::string PARAM_NAME_CYLINDER_MAX_RADIUS_LIMIT = "/pitt/srv/cylinder_seg
 const std::string PARAM_NAME_CYLINDER_EPS_ANGLE_TH = "/pitt/srv/cylinder_segmentation/eps_angle_th";
 const std::string PARAM_NAME_CYLINDER_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/cylinder_segmentation/min_opening_angle_deg";
 const std::string PARAM_NAME_CYLINDER_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/cylinder_segmentation/max_opening_angle_deg";
+const std::string SRV_NAME_RANSAC_CONE_FILTER = "cone_segmentation_srv";
+const std::string PARAM_NAME_CONE_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/cone_segmentation/normal_distance_weight";
+const std::string PARAM_NAME_CONE_DISTANCE_TH = "/pitt/srv/cone_segmentation/distance_th";
+const std::string PARAM_NAME_CONE_MAX_ITERATION_LIMIT = "/pitt/srv/cone_segmentation/max_iter_limit";
+const std::string PARAM_NAME_CONE_MIN_RADIUS_LIMIT = "/pitt/srv/cone_segmentation/min_radius_limit";
+const std::string PARAM_NAME_CONE_MAX_RADIUS_LIMIT = "/pitt/srv/cone_segmentation/max_radius_limit";
+const std::string PARAM_NAME_CONE_EPS_ANGLE_TH = "/pitt/srv/cone_segmentation/eps_angle_th";
+const std::string PARAM_NAME_CONE_MIN_OPENING_ANGLE_DEGREE = "/pitt/srv/cone_segmentation/min_opening_angle_deg";
+const std::string PARAM_NAME_CONE_MAX_OPENING_ANGLE_DEGREE = "/pitt/srv/cone_segmentation/max_opening_angle_deg";
+const std::string PARAM_NAME_CONE_MIN_INLIERS = "/pitt/srv/cone_segmentation/min_inliers";
 const std::string PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT = "/pitt/srv/sphere_segmentation/normal_distance_weight";
 const std::string PARAM_NAME_SPHERE_DISTANCE_TH = "/pitt/srv/sphere_segmentation/distance_th";
 const std::string PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT = "/pitt/srv/sphere_segmentation/max_iter_limit";
@@ -213,6 +223,9 @@ public:
     // cylinder_segmentation_srv.cpp:82-216 (the model, then the axis height and centroid)
     bool ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
                                  pitt_msgs::PrimitiveSegmentation::Response& res);
+    // cone_segmentation_srv.cpp:83-216 (the model, then the axis height and the 3/4-height centroid)
+    bool ransacConeDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                             pitt_msgs::PrimitiveSegmentation::Response& res);
     // sphere_segmentation_srv.cpp:29-96
     bool ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
                                pitt_msgs::PrimitiveSegmentation::Response& res);

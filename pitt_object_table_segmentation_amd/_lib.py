@@ -84,6 +84,15 @@ class CylinderParams(ctypes.Structure):
                 ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
 
 
+class ConeParams(ctypes.Structure):
+    """pitt_cone_params (include/pitt_seg.h)."""
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("normal_distance_weight", ctypes.c_double),
+                ("min_angle", ctypes.c_double), ("max_angle", ctypes.c_double), ("eps_angle", ctypes.c_double),
+                ("axis", ctypes.c_float * 3), ("eigen33", ctypes.c_int32), ("seed", ctypes.c_uint32),
+                ("pad", ctypes.c_int32)]
+
+
 class SupportParams(ctypes.Structure):
     _fields_ = [
         ("min_iterative_cloud_percentage", ctypes.c_float),
@@ -210,9 +219,12 @@ SIGNATURES.update({
     "pitt_srv_param_set_list": (_i32, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i32]),
     "pitt_srv_param_erase": (_i32, [_vp, ctypes.c_char_p]),
     "pitt_srv_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
+    "pitt_srv_ransac_cone": (_i32, [_vp, _f32p, _i64, _f32p, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
     "pitt_srv_ransac_cylinder": (_i32, [_vp, _f32p, _i64, _f32p, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
     "pitt_cylinder_segment_host": (_i32, [_vp, _f32p, _f32p, _i64, ctypes.POINTER(CylinderParams), _i32p, _i64p, _f32p,
                                           _i32p]),
+    "pitt_cone_segment": (_i32, [_vp] * 7 + [_i64, ctypes.POINTER(ConeParams), _vp, _i64p, _f32p, _i32p]),
+    "pitt_cone_segment_host": (_i32, [_vp, _f32p, _f32p, _i64, ctypes.POINTER(ConeParams), _i32p, _i64p, _f32p, _i32p]),
     "pitt_axis_height_host": (_i32, [_vp, _f32p, _i64, _f32p, _i32, _f32p, _i32p, _i32p, _f32p]),
     "pitt_srv_ransac_sphere": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p, _f32p]),
     "pitt_srv_call_ransac_plane": (_i32, [_vp, _f32p, _i64, _i64, _i32p, _i64p, _f32p, _i32p]),

@@ -397,6 +397,29 @@ class Context:
         self._check(rc, "pitt_cylinder_segment")
         return inl[:ni.value], coef, hyp.value
 
+    def cone_segment(self, x, y, z, nx, ny, nz, threshold: float = 0.0055, max_iterations: int = 1000,
+                     optimize: bool = True, normal_distance_weight: float = 0.0006, min_angle_deg: float = 10.0,
+                     max_angle_deg: float = 170.0, eps_angle: float = 0.4, axis=(0.0, 0.0, 0.0), eigen33: int = 0,
+                     probability: float = 0.99, seed: int = 12345):
+        """The cone service's seg.segment (cone_segmentation_srv.cpp:111-127; defaults :24-31, the angles
+        converted as :124 does) on device tensors (points and normals): (inliers device int32,
+        coefficients[7] = apex, axis, opening angle, or None, hypotheses)."""
+        import torch
+        n = x.numel()
+        prm = L.ConeParams(threshold, max_iterations, int(optimize), probability, normal_distance_weight,
+                           min_angle_deg / 180.0 * np.pi, max_angle_deg / 180.0 * np.pi, eps_angle,
+                           (ctypes.c_float * 3)(*axis), eigen33, seed, 0)
+        inl = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
+        ni = ctypes.c_int64()
+        coef = np.zeros(7, np.float32)
+        hyp = ctypes.c_int32()
+        rc = lib.pitt_cone_segment(self.h, *(t.data_ptr() for t in (x, y, z, nx, ny, nz)), n, ctypes.byref(prm),
+                                   inl.data_ptr(), ctypes.byref(ni), _fp(coef), ctypes.byref(hyp))
+        if rc == L.PITT_NO_MODEL:
+            return inl[:0], None, hyp.value
+        self._check(rc, "pitt_cone_segment")
+        return inl[:ni.value], coef, hyp.value
+
     def axis_height(self, x, y, z, coefficients, mode: int = L.PITT_AXIS_CYLINDER, projected: bool = False):
         """The cylinder / cone services' post-processing (cylinder_segmentation_srv.cpp:129-189,
         cone_segmentation_srv.cpp:129-189) on device tensors: (height, idx1, idx2, centroid[3])
@@ -547,6 +570,21 @@ class Services:
         ok = self._rc(lib.pitt_srv_ransac_cylinder(self.h, _fp(c), n, _fp(nrm), n if n_normals is None else n_normals,
                                                    _ip(inl), ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)),
                       "ransac_cylinder")
+        return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
+
+    def ransac_cone(self, cloud: np.ndarray, normals: np.ndarray, n_normals: Optional[int] = None):
+        """ransacConeDetaction (cone_segmentation_srv.cpp:83-216): (ok, inliers (index 0 dropped),
+        coefficients (apex, axis, opening angle, then the height), centroid)."""
+        c = _cloud16(cloud)
+        n = c.shape[0]
+        nrm = np.ascontiguousarray(np.asarray(normals, np.float32).reshape(-1, 3))
+        inl = np.empty(max(n, 1), np.int32)
+        ni, nc = ctypes.c_int64(), ctypes.c_int32()
+        co = np.zeros(8, np.float32)
+        ce = np.zeros(3, np.float32)
+        ok = self._rc(lib.pitt_srv_ransac_cone(self.h, _fp(c), n, _fp(nrm), n if n_normals is None else n_normals,
+                                               _ip(inl), ctypes.byref(ni), _fp(co), ctypes.byref(nc), _fp(ce)),
+                      "ransac_cone")
         return ok, inl[:ni.value].copy(), co[:nc.value].copy(), ce
 
     def call_ransac_plane(self, cloud: np.ndarray, n_normals: Optional[int] = None):

@@ -31,46 +31,14 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
+#include "lm7.hpp"
+#include "vec4.hpp"
 
 #pragma clang fp contract(off)
 
 namespace pitt {
 
-struct CV4 {
-    float v[4];
-};
-__device__ __forceinline__ CV4 cv4(float a, float b, float c, float d = 0.0f) { return CV4{{a, b, c, d}}; }
-__device__ __forceinline__ CV4 cadd(CV4 a, CV4 b) {
-    return cv4(a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]);
-}
-__device__ __forceinline__ CV4 csub(CV4 a, CV4 b) {
-    return cv4(a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2], a.v[3] - b.v[3]);
-}
-__device__ __forceinline__ CV4 cmul(float s, CV4 a) { return cv4(s * a.v[0], s * a.v[1], s * a.v[2], s * a.v[3]); }
-__device__ __forceinline__ float cdot(CV4 a, CV4 b) {  // SSE2 predux: (a0 + a2) + (a1 + a3)
-    return (a.v[0] * b.v[0] + a.v[2] * b.v[2]) + (a.v[1] * b.v[1] + a.v[3] * b.v[3]);
-}
-__device__ __forceinline__ CV4 ccross3(CV4 l, CV4 r) {
-    return cv4(l.v[1] * r.v[2] - l.v[2] * r.v[1], l.v[2] * r.v[0] - l.v[0] * r.v[2], l.v[0] * r.v[1] - l.v[1] * r.v[0],
-               l.v[3] * r.v[3] - l.v[3] * r.v[3]);
-}
-__device__ __forceinline__ CV4 cnormalize(CV4 a) {
-    const float r = 1.0f / sqrtf(cdot(a, a));
-    return cv4(a.v[0] * r, a.v[1] * r, a.v[2] * r, a.v[3] * r);
-}
-__device__ __forceinline__ CV4 cnormalized(CV4 a) {
-    const float nn = sqrtf(cdot(a, a));
-    return cv4(a.v[0] / nn, a.v[1] / nn, a.v[2] / nn, a.v[3] / nn);
-}
-__device__ __forceinline__ double csqr_pt_line(CV4 pt, CV4 lp, CV4 ld) {
-    const CV4 c = ccross3(ld, csub(lp, pt));
-    return (double)(cdot(c, c) / cdot(ld, ld));
-}
-
-struct CylCoef {
-    float c[7];
-    float pad;
-};
+using CylCoef = Coef7;
 
 __global__ void k_cyl_model(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
                             const float* __restrict__ NX, const float* __restrict__ NY, const float* __restrict__ NZ,
@@ -179,142 +147,11 @@ __device__ __forceinline__ void cyl_residual(const double* v, float px, float py
     J[5] = 2.0 * (vx * wy - vy * wx) / s - 2.0 * w2 * uz / (s * s);
     J[6] = -2.0 * v[6];
 }
-
-constexpr int kCylLmThreads = 1024;
-constexpr int kCylSums = 28 + 7 + 1;
-
-__device__ void cyl_lm_sums(const float* X, const float* Y, const float* Z, const int32_t* inl, int64_t m,
-                            const double* v, double (*red)[kCylSums], double* out) {
-    double acc[kCylSums];
-    for (int q = 0; q < kCylSums; ++q) acc[q] = 0;
-    for (int64_t k = threadIdx.x; k < m; k += kCylLmThreads) {
-        const int id = inl[k];
-        double J[7], f;
-        cyl_residual(v, X[id], Y[id], Z[id], J, &f);
-        int t = 0;
-        for (int a = 0; a < 7; ++a)
-            for (int b = a; b < 7; ++b) acc[t++] += J[a] * J[b];
-        for (int a = 0; a < 7; ++a) acc[28 + a] += J[a] * f;
-        acc[35] += f * f;
+struct CylResidual {
+    __device__ void operator()(const double* v, float px, float py, float pz, double J[7], double* f) const {
+        cyl_residual(v, px, py, pz, J, f);
     }
-    for (int q = 0; q < kCylSums; ++q) {
-        double t = acc[q];
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x < kCylSums) {
-        double t = 0;
-        for (int w = 0; w < kCylLmThreads / 64; ++w) t += red[w][threadIdx.x];
-        out[threadIdx.x] = t;
-    }
-    __syncthreads();
-}
-
-// the oracle's lm_solve<7>: Marquardt damping, the damped 7 x 7 system solved by thread 0
-__global__ __launch_bounds__(kCylLmThreads) void k_cyl_lm(const float* __restrict__ X, const float* __restrict__ Y,
-                                                          const float* __restrict__ Z, const int32_t* __restrict__ inl,
-                                                          int64_t m, CylCoef init, CylCoef* __restrict__ out) {
-    __shared__ double red[kCylLmThreads / 64][kCylSums];
-    __shared__ double cur[kCylSums], trial[kCylSums];
-    __shared__ double xv[7], xn[7];
-    __shared__ int state;
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 7; ++k) xv[k] = init.c[k];
-    __syncthreads();
-    cyl_lm_sums(X, Y, Z, inl, m, xv, red, cur);
-    double lambda = 1e-3;
-    for (int it = 0; it < 200; ++it) {
-        bool moved = false, stop = false;
-        for (;;) {
-            if (threadIdx.x == 0) {
-                state = 0;
-                if (!(lambda < 1e10)) state = 3;
-                else {
-                    double M[7][8];
-                    int t = 0;
-                    for (int a = 0; a < 7; ++a)
-                        for (int b = a; b < 7; ++b) M[a][b] = M[b][a] = cur[t++];
-                    for (int a = 0; a < 7; ++a) M[a][a] += lambda * M[a][a] + 1e-30, M[a][7] = -cur[28 + a];
-                    for (int col = 0; col < 7 && state == 0; ++col) {
-                        int piv = col;
-                        for (int r = col + 1; r < 7; ++r)
-                            if (fabs(M[r][col]) > fabs(M[piv][col])) piv = r;
-                        if (M[piv][col] == 0) {
-                            state = 3;
-                            break;
-                        }
-                        if (piv != col)
-                            for (int k = 0; k < 8; ++k) {
-                                const double tt = M[col][k];
-                                M[col][k] = M[piv][k];
-                                M[piv][k] = tt;
-                            }
-                        for (int r = col + 1; r < 7; ++r) {
-                            const double f = M[r][col] / M[col][col];
-                            for (int k = col; k < 8; ++k) M[r][k] -= f * M[col][k];
-                        }
-                    }
-                    if (state == 0) {
-                        double dl[7];
-                        for (int r = 6; r >= 0; --r) {
-                            double acc = M[r][7];
-                            for (int k = r + 1; k < 7; ++k) acc -= M[r][k] * dl[k];
-                            dl[r] = acc / M[r][r];
-                        }
-                        for (int r = 0; r < 7; ++r) xn[r] = xv[r] + dl[r];
-                    }
-                }
-            }
-            __syncthreads();
-            const int st0 = state;
-            __syncthreads();
-            if (st0 == 3) {
-                stop = true;
-                break;
-            }
-            cyl_lm_sums(X, Y, Z, inl, m, xn, red, trial);
-            if (threadIdx.x == 0) {
-                if (trial[35] < cur[35]) {
-                    double step = 0, nx = 0;
-                    for (int r = 0; r < 7; ++r) {
-                        const double d = xn[r] - xv[r];
-                        step += d * d;
-                        nx += xn[r] * xn[r];
-                        xv[r] = xn[r];
-                    }
-                    for (int q = 0; q < kCylSums; ++q) cur[q] = trial[q];
-                    lambda *= 0.1;
-                    state = sqrt(step / (nx + 1e-300)) < 1e-12 ? 3 : 1;
-                } else {
-                    lambda *= 10;
-                    state = 2;
-                }
-            }
-            __syncthreads();
-            const int st1 = state;
-            __syncthreads();
-            if (st1 == 2) continue;
-            moved = true;
-            stop = st1 == 3;
-            break;
-        }
-        __syncthreads();
-        if (!moved || stop) break;
-    }
-    if (threadIdx.x == 0) {
-        CylCoef o = {};
-        for (int k = 0; k < 3; ++k) o.c[k] = (float)xv[k];
-        // Eigen::Vector3f line_dir(...).normalize(): fixed size 3, a0 + (a1 + a2), times 1 / norm
-        const float u0 = (float)xv[3], u1 = (float)xv[4], u2 = (float)xv[5];
-        const float r = 1.0f / sqrtf(u0 * u0 + (u1 * u1 + u2 * u2));
-        o.c[3] = u0 * r;
-        o.c[4] = u1 * r;
-        o.c[5] = u2 * r;
-        o.c[6] = (float)xv[6];
-        *out = o;
-    }
-}
+};
 
 }  // namespace pitt
 
@@ -438,7 +275,8 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
     CylCoef outc = bc;
     if (p->optimize && *n_inliers > 0) {
         rec = ctx->prof_begin("k_cyl_lm", (double)*n_inliers * 12.0);
-        hipLaunchKernelGGL(k_cyl_lm, dim3(1), dim3(kCylLmThreads), 0, s, x, y, z, inliers, *n_inliers, bc, dref);
+        hipLaunchKernelGGL(k_lm7<CylResidual>, dim3(1), dim3(kLmThreads), 0, s, CylResidual{}, x, y, z, inliers, *n_inliers,
+                           bc, dref);
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
         PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(CylCoef), hipMemcpyDeviceToHost, s));

@@ -162,6 +162,74 @@ bool SegmentationServices::ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentat
     return true;
 }
 
+// cone_segmentation_srv.cpp:83-216.  The radius limits are read and set (:121) but SACMODEL_CONE does not
+// use them; the opening angles (degrees, converted at :124) and the eps angle (:125, against no axis)
+// constrain the model.  After the fit, the cloud's projection on the axis gives the height (pushed after
+// the 7 coefficients) and the centroid, apex + 3/4 height along the unit axis (:129-200).
+bool SegmentationServices::ransacConeDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                                                   pitt_msgs::PrimitiveSegmentation::Response& res) {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
+        maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_CONE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.0006);
+    params_.param(srvm::PARAM_NAME_CONE_DISTANCE_TH, distanceThreshold, 0.0055);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_CONE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.001);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
+    params_.param(srvm::PARAM_NAME_CONE_EPS_ANGLE_TH, epsAngleTh, 0.4);
+    params_.param(srvm::PARAM_NAME_CONE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 10.0);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 170.0);
+    (void)minRadiusLimit; (void)maxRadiusLimit;
+
+    pitt_cone_params p;
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    p.optimize = 1;
+    p.probability = 0.99;
+    p.normal_distance_weight = normalDistanceWeight;
+    p.min_angle = minOpeningAngle / 180.0 * M_PI;
+    p.max_angle = maxOpeningAngle / 180.0 * M_PI;
+    p.eps_angle = epsAngleTh;
+    p.axis[0] = p.axis[1] = p.axis[2] = 0.0f;
+    p.eigen33 = 0;
+    p.seed = 12345u;
+    p.pad = 0;
+    const size_t n = req.cloud.size();
+    std::vector<int32_t> inl(n + 1);
+    int64_t n_inl = 0;
+    float coef[7] = {0, 0, 0, 0, 0, 0, 0};
+    int32_t n_coef = 0;
+    status_ = PITT_OK;
+    if (req.normals.size() == n) {  // initSACModel: normals must match the cloud
+        if (req.normals.data.size() != 3 * n) {
+            status_ = PITT_E_INVALID;  // the normal vectors themselves are needed here
+            return false;
+        }
+        status_ = pitt_cone_segment_host(ctx_, req.cloud.data.data(), req.normals.data.data(), (int64_t)n, &p,
+                                         inl.data(), &n_inl, coef, nullptr);
+        if (status_ == PITT_OK) n_coef = 7;
+        if (status_ != PITT_OK) n_inl = 0;
+        if (status_ == PITT_NO_MODEL) status_ = PITT_OK;
+        if (status_ < 0) return false;
+    }
+    float height = -1.0f, centroid[3] = {0, 0, 0};  // the reference leaves the centroid unset without inliers
+    if (n_inl > 0) {
+        int32_t i1 = -1, i2 = -1;
+        status_ = pitt_axis_height_host(ctx_, req.cloud.data.data(), (int64_t)n, coef, PITT_AXIS_CONE, &height,
+                                        &i1, &i2, centroid);
+        if (status_ < 0) return false;
+    }
+    res.inliers.clear();  // inlierToVectorMsg drops index 0 (Q1)
+    for (int64_t i = 0; i < n_inl; ++i)
+        if (inl[(size_t)i] != 0) res.inliers.push_back(inl[(size_t)i]);
+    res.coefficients.assign(coef, coef + n_coef);
+    res.coefficients.push_back(height);  // :195
+    res.x_centroid = centroid[0];
+    res.y_centroid = centroid[1];
+    res.z_centroid = centroid[2];
+    return true;
+}
+
 // sphere_segmentation_srv.cpp:29-96.  SACSegmentationFromNormals with SACMODEL_SPHERE falls through to
 // the plain sphere model: the normal weight, eps angle and opening angles are read but unused.
 bool SegmentationServices::ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
@@ -482,6 +550,31 @@ int pitt_srv_ransac_cylinder(pitt_srv* s, const float* xyz16, int64_t n, const f
     srv.request.normals.n = (size_t)n_normals;
     if (normals3 && n_normals == n) srv.request.normals.data.assign(normals3, normals3 + 3 * n);
     bool ok = s->svc.ransacCylinderDetaction(srv.request, srv.response);
+    if (s->svc.last_status() < 0) return s->svc.last_status();
+    *n_inliers = (int64_t)srv.response.inliers.size();
+    *n_coefficients = (int32_t)srv.response.coefficients.size();
+    if (inliers_out && !srv.response.inliers.empty())
+        std::memcpy(inliers_out, srv.response.inliers.data(), srv.response.inliers.size() * 4);
+    if (coefficients_out && !srv.response.coefficients.empty())
+        std::memcpy(coefficients_out, srv.response.coefficients.data(), srv.response.coefficients.size() * 4);
+    if (centroid_out) {
+        centroid_out[0] = srv.response.x_centroid;
+        centroid_out[1] = srv.response.y_centroid;
+        centroid_out[2] = srv.response.z_centroid;
+    }
+    return ok ? 1 : 0;
+}
+
+int pitt_srv_ransac_cone(pitt_srv* s, const float* xyz16, int64_t n, const float* normals3, int64_t n_normals,
+                         int32_t* inliers_out, int64_t* n_inliers, float* coefficients_out, int32_t* n_coefficients,
+                         float centroid_out[3]) {
+    if (!s || (n > 0 && !xyz16) || n < 0 || !n_inliers || !n_coefficients) return PITT_E_INVALID;
+    if (n_normals == n && n > 0 && !normals3) return PITT_E_INVALID;
+    pitt_msgs::PrimitiveSegmentation srv;
+    srv.request.cloud = cloud_from(xyz16, n);
+    srv.request.normals.n = (size_t)n_normals;
+    if (normals3 && n_normals == n) srv.request.normals.data.assign(normals3, normals3 + 3 * n);
+    bool ok = s->svc.ransacConeDetaction(srv.request, srv.response);
     if (s->svc.last_status() < 0) return s->svc.last_status();
     *n_inliers = (int64_t)srv.response.inliers.size();
     *n_coefficients = (int32_t)srv.response.coefficients.size();

@@ -368,3 +368,48 @@ def cylinder_segment(xyz, nrm, params=None):
     ok = O.orc_cylinder_segment(*(_fp(c) for c in cols), n, ctypes.byref(p), _ip(inl), ctypes.byref(ni), _fp(coef),
                                 _fp(best), ctypes.byref(hyp))
     return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value}
+
+
+class ConeParams(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
+                ("probability", ctypes.c_double), ("normal_distance_weight", ctypes.c_double),
+                ("min_angle", ctypes.c_double), ("max_angle", ctypes.c_double), ("eps_angle", ctypes.c_double),
+                ("axis", ctypes.c_float * 3), ("eigen33", ctypes.c_int32), ("seed", ctypes.c_uint32),
+                ("pad", ctypes.c_int32)]
+
+
+def cone_params(threshold=0.0055, max_iterations=1000, optimize=True, normal_distance_weight=0.0006,
+                min_angle_deg=10.0, max_angle_deg=170.0, eps_angle=0.4, axis=(0.0, 0.0, 0.0), eigen33=0,
+                probability=0.99, seed=12345):
+    """cone_segmentation_srv.cpp:24-31 defaults; the angles converted as :124 does (deg / 180 * M_PI)."""
+    return ConeParams(threshold, max_iterations, int(optimize), probability, normal_distance_weight,
+                      min_angle_deg / 180.0 * np.pi, max_angle_deg / 180.0 * np.pi, eps_angle,
+                      (ctypes.c_float * 3)(*axis), eigen33, seed, 0)
+
+
+O.orc_cone_segment.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.POINTER(ConeParams)] + \
+    [ctypes.c_void_p] * 5
+O.orc_cone_from3.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+
+
+def cone_from3(p3, n3, min_angle=-np.finfo(np.float64).max, max_angle=np.finfo(np.float64).max):
+    c = np.zeros(7, np.float32)
+    ok = O.orc_cone_from3(_fp(np.ascontiguousarray(p3, np.float32)), _fp(np.ascontiguousarray(n3, np.float32)),
+                          min_angle, max_angle, _fp(c))
+    return bool(ok), c
+
+
+def cone_segment(xyz, nrm, params=None):
+    """The cone service's seg.segment restated: dict(ok, inliers, coef[7], best[7], hypotheses)."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    nrm = np.ascontiguousarray(nrm, np.float32)
+    cols = [np.ascontiguousarray(a[:, k]) for a in (xyz, nrm) for k in range(3)]
+    n = len(xyz)
+    p = params or cone_params()
+    inl = np.empty(max(n, 1), np.int32)
+    ni = ctypes.c_int64()
+    coef, best = np.zeros(7, np.float32), np.zeros(7, np.float32)
+    hyp = ctypes.c_int32()
+    ok = O.orc_cone_segment(*(_fp(c) for c in cols), n, ctypes.byref(p), _ip(inl), ctypes.byref(ni), _fp(coef),
+                            _fp(best), ctypes.byref(hyp))
+    return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value}

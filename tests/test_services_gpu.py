@@ -187,3 +187,35 @@ def test_cylinder_handler(srv):
     # normals of the wrong size: PCL clears the outputs; the height stays -1 (:132, :195)
     ok, inl, coef, centroid = srv.ransac_cylinder(P, N, n_normals=len(P) - 1)
     assert ok and len(inl) == 0 and list(coef) == [-1.0] and not centroid.any()
+
+
+def test_cone_handler(srv):
+    """ransacConeDetaction (cone_segmentation_srv.cpp:83-216): the parameter-server defaults (:24-31, the
+    opening angles converted at :124), the model, then the axis height pushed after the 7 coefficients and
+    the centroid apex + 3/4 height along the axis (:129-200)."""
+    from test_cone import cone_scene, same_cone
+    P, N, _ = cone_scene(1500, 500, 11)
+    ok, inl, coef, centroid = srv.ransac_cone(P, N)
+    want = orc.cone_segment(P, N)
+    assert ok and want["ok"] and len(coef) == 8
+    assert same_cone(coef[:7].astype(np.float64), want["coef"].astype(np.float64), pos=1e-5, ang=1e-9, opening=1e-6)
+    # the post-processing on the handler's own coefficients: bit-exact against the restatement
+    h, i1, i2, cen, _ = orc.axis_height(*P.T, coef[:6], 1)
+    assert np.float32(coef[7]).view(np.int32) == np.float32(h).view(np.int32)
+    assert np.array_equal(centroid.view(np.int32), cen.view(np.int32))
+    ref = want["inliers"][want["inliers"] != 0]
+    assert len(np.setxor1d(inl, ref)) <= max(2, len(ref) // 2000) and 0 not in inl
+    # a parameter on the server reaches the model: opening angles 60-120 degrees exclude this 25-degree cone
+    srv.set_param("/pitt/srv/cone_segmentation/min_opening_angle_deg", 60.0)
+    srv.set_param("/pitt/srv/cone_segmentation/max_opening_angle_deg", 120.0)
+    try:
+        ok, inl, coef, centroid = srv.ransac_cone(P, N)
+        want = orc.cone_segment(P, N, orc.cone_params(min_angle_deg=60.0, max_angle_deg=120.0))
+        ref = want["inliers"][want["inliers"] != 0]
+        assert ok and abs(len(inl) - len(ref)) <= max(2, len(ref) // 2000)
+    finally:
+        srv.erase_param("/pitt/srv/cone_segmentation/min_opening_angle_deg")
+        srv.erase_param("/pitt/srv/cone_segmentation/max_opening_angle_deg")
+    # normals of the wrong size: PCL clears the outputs; the height stays -1 (:132, :195)
+    ok, inl, coef, centroid = srv.ransac_cone(P, N, n_normals=len(P) - 1)
+    assert ok and len(inl) == 0 and list(coef) == [-1.0] and not centroid.any()
