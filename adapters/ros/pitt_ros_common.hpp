@@ -130,6 +130,27 @@ inline sensor_msgs::PointCloud2 from_xyz16(const float* xyz16, int64_t n, bool i
     return m;
 }
 
+// fromROSMsg into PointCloud<Normal> (PCManager::normForRosMsg, pc_manager.cpp:92-97), keeping the
+// (normal_x, normal_y, normal_z) triples: fields located by name, FLOAT32 only; a missing field leaves
+// pcl::Normal's default 0.
+inline std::vector<float> to_normals3(const sensor_msgs::PointCloud2& msg) {
+    int off[3] = {-1, -1, -1};
+    const char* names[3] = {"normal_x", "normal_y", "normal_z"};
+    for (const sensor_msgs::PointField& f : msg.fields)
+        for (int k = 0; k < 3; ++k)
+            if (f.name == names[k] && f.datatype == sensor_msgs::PointField::FLOAT32) off[k] = (int)f.offset;
+    const size_t n = (size_t)msg.width * msg.height;
+    std::vector<float> out(3 * n, 0.0f);
+    for (uint32_t r = 0; r < msg.height; ++r)
+        for (uint32_t c = 0; c < msg.width; ++c) {
+            const uint8_t* p = &msg.data[(size_t)r * msg.row_step + (size_t)c * msg.point_step];
+            float* o = &out[3 * ((size_t)r * msg.width + c)];
+            for (int k = 0; k < 3; ++k)
+                if (off[k] >= 0) std::memcpy(&o[k], p + off[k], 4);
+        }
+    return out;
+}
+
 inline int64_t n_points(const sensor_msgs::PointCloud2& msg) { return (int64_t)msg.width * msg.height; }
 
 }  // namespace pitt_ros

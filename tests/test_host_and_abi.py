@@ -141,7 +141,7 @@ def test_ros_adapters_use_only_declared_abi():
         declared |= set(re.findall(r"\b(pitt_\w+)\s*\(", open(h).read()))
     srcs = glob.glob(os.path.join(root, "adapters", "ros", "*.cpp")) + \
         glob.glob(os.path.join(root, "adapters", "ros", "*.hpp"))
-    assert len(srcs) == 6
+    assert len(srcs) == 8
     used = set()
     for s in srcs:
         used |= set(re.findall(r"\b(pitt_(?!ros\b)\w+)\s*\(", open(s).read()))
@@ -149,7 +149,9 @@ def test_ros_adapters_use_only_declared_abi():
     names = {"plane_segmentation_node.cpp": "plane_segmentation_srv", "deep_filter_node.cpp": "deep_filter_srv",
              "supports_segmentation_node.cpp": "support_segmentation_srv",
              "cluster_segmentation_node.cpp": "cluster_Segmentation_srv",
-             "sphere_segmentation_node.cpp": "sphere_segmentation_srv"}
+             "sphere_segmentation_node.cpp": "sphere_segmentation_srv",
+             "cylinder_segmentation_node.cpp": "cylinder_segmentation_srv",
+             "cone_segmentation_node.cpp": "cone_segmentation_srv"}
     for f, name in names.items():
         assert f'advertiseService("{name}"' in open(os.path.join(root, "adapters", "ros", f)).read(), f
 
