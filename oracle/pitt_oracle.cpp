@@ -1527,7 +1527,7 @@ void cyl_refine(const float* x, const float* y, const float* z, const std::vecto
             *cost += f * f;
         }
     };
-    lm_solve<7>(q, sums);
+    if (inl.size() >= 7) lm_solve<7>(q, sums);  // Eigen's LM refuses m < n (ImproperInputParameters)
     const double nu = std::sqrt(q[3] * q[3] + q[4] * q[4] + q[5] * q[5]);
     for (int k = 0; k < 3; ++k) out[k] = (float)q[k];
     // Eigen::Vector3f line_dir(...).normalize() on the float coefficients

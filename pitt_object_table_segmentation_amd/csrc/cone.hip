@@ -204,16 +204,6 @@ struct ConeResidual {
     }
 };
 
-// fewer than 7 inliers: Eigen's LM returns ImproperInputParameters; only the direction is normalised
-__global__ void k_cone_normalize_dir(Coef7 m, Coef7* out) {
-    const float u0 = m.c[3], u1 = m.c[4], u2 = m.c[5];
-    const float r = 1.0f / sqrtf(u0 * u0 + (u1 * u1 + u2 * u2));
-    m.c[3] = u0 * r;
-    m.c[4] = u1 * r;
-    m.c[5] = u2 * r;
-    *out = m;
-}
-
 }  // namespace pitt
 
 extern "C" int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
@@ -346,7 +336,7 @@ extern "C" int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, 
                                *n_inliers, bc, dref);
             ctx->prof_end(rec);
         } else {
-            hipLaunchKernelGGL(k_cone_normalize_dir, dim3(1), dim3(1), 0, s, bc, dref);
+            hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, dref);
         }
         PITT_HIP_TRY(hipGetLastError());
         PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(Coef7), hipMemcpyDeviceToHost, s));

@@ -156,4 +156,16 @@ __global__ __launch_bounds__(kLmThreads) void k_lm7(R res, const float* __restri
     }
 }
 
+// fewer residuals than parameters (m < 7): Eigen's LM returns ImproperInputParameters and leaves the model;
+// optimizeModelCoefficients still normalises the direction
+template <int = 0>  // a template, so the header can be included by several translation units
+__global__ void k_lm7_normalize_dir(Coef7 m, Coef7* out) {
+    const float u0 = m.c[3], u1 = m.c[4], u2 = m.c[5];
+    const float r = 1.0f / sqrtf(u0 * u0 + (u1 * u1 + u2 * u2));
+    m.c[3] = u0 * r;
+    m.c[4] = u1 * r;
+    m.c[5] = u2 * r;
+    *out = m;
+}
+
 }  // namespace pitt

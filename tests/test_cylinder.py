@@ -112,3 +112,16 @@ def test_hip_cylinder_edges(ctx):
     want = orc.cylinder_segment(P, N, orc.cylinder_params(optimize=False, max_iterations=20))
     inl, coef, hyp = _gpu(ctx, P, N, optimize=False, max_iterations=20)
     assert (coef is not None) == want["ok"] and hyp == want["hypotheses"]
+
+
+@pytest.mark.gpu
+def test_hip_cylinder_few_inliers(ctx):
+    """Fewer than 7 inliers: Eigen's LM refuses m < n, the model stays and only the direction is normalised."""
+    P, N, _ = cylinder_scene(5, 0, 5)
+    want = orc.cylinder_segment(P, N)
+    inl, coef, hyp = _gpu(ctx, P, N)
+    assert (coef is not None) == want["ok"] and hyp == want["hypotheses"]
+    if coef is not None:
+        assert len(want["inliers"]) < 7
+        assert np.array_equal(coef.view(np.int32), want["coef"].view(np.int32))
+        assert np.array_equal(inl, want["inliers"])

@@ -162,6 +162,34 @@ def main():
                     e["kernels"][kname] = {"launches_per_call": launches / 5, "avg_us": round(ms / launches * 1e3, 1)}
             ctx.profile(False)
             sph[str(ns + no)] = e
+        # cylinder / cone services: RANSAC with normals + refinement on object-sized clusters with clutter
+        from test_cylinder import cylinder_scene
+        from test_cone import cone_scene
+        prim = {}
+        for name, scene, fn, knames in (
+                ("cylinder_segment", cylinder_scene, ctx.cylinder_segment, ("k_cyl_model", "k_cyl_count", "k_cyl_lm")),
+                ("cone_segment", cone_scene, ctx.cone_segment, ("k_cone_model", "k_cone_count", "k_cone_lm"))):
+            prim[name] = {}
+            for ns, no in ((4000, 1000), (40000, 10000)):
+                P, N, _ = scene(ns, no, 7)
+                ts = [torch.from_numpy(np.ascontiguousarray(a[:, k])).cuda() for a in (P, N) for k in range(3)]
+                fn(*ts)
+                torch.cuda.synchronize()
+                ctx.profile(True)
+                ctx.profile_reset()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    inl_c, coef_c, hyp_c = fn(*ts)
+                torch.cuda.synchronize()
+                e = {"ms_per_call_wall": round((time.perf_counter() - t0) * 1e3 / 5, 3), "points": ns + no,
+                     "hypotheses": hyp_c, "inliers": int(inl_c.numel()), "kernels": {}}
+                for kname in knames:
+                    launches, ms, algo = ctx.profile_get(kname)
+                    if launches:
+                        e["kernels"][kname] = {"launches_per_call": launches / 5,
+                                               "avg_us": round(ms / launches * 1e3, 1)}
+                ctx.profile(False)
+                prim[name][str(ns + no)] = e
     import oracle_binding as orc
     t0 = time.perf_counter()
     k = 0
@@ -187,10 +215,17 @@ def main():
     t0 = time.perf_counter()
     orc.sphere_segment(*ps.T)
     sph["5000"]["cpu_oracle_ms_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
+    for name, scene, fn in (("cylinder_segment", cylinder_scene, orc.cylinder_segment),
+                            ("cone_segment", cone_scene, orc.cone_segment)):
+        for ns, no in ((4000, 1000), (40000, 10000)):
+            P, N, _ = scene(ns, no, 7)
+            t0 = time.perf_counter()
+            fn(P, N)
+            prim[name][str(ns + no)]["cpu_oracle_ms_1thread"] = round((time.perf_counter() - t0) * 1e3, 1)
     print(json.dumps({"workload": f"{args.frames} x 640x480 synthetic camera clouds ({n} points), deep filter "
                                   f"(th {used}) + transform, PointXYZ unpack, {args.reps} reps", "points": n, "kept": kept,
                       "kernels": res, "cpu_oracle_points_per_s_1thread": round(cpu), "voxel_grid": vox, "normal_estimation": nrm,
-                      "axis_height": axis, "sphere_segment": sph,
+                      "axis_height": axis, "sphere_segment": sph, **prim,
                       "gpu_points_per_s": round(n / (sum(r["avg_us"] for r in res.values()) * 1e-6))}))
 
 
