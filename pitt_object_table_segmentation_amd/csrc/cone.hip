@@ -13,7 +13,7 @@
 //                      distance - tan(angle) |apex - proj||, d_normal = min(a, pi - a) of the angle between
 //                      the normal and sinf(angle) * unit(apex - proj) + cosf(angle) * unit(p - proj);
 //   computeModel       the plane loop with w^3;
-//   optimize           the double Levenberg-Marquardt of lm7.hpp on f = |v|^2 - (1 + tan^2 a) (u.v)^2 / |u|^2
+//   optimize           the double Levenberg-Marquardt of lm.hpp on f = |v|^2 - (1 + tan^2 a) (u.v)^2 / |u|^2
 //                      (v = apex - p: the functor's residual by Lagrange's identity); PCL runs Eigen's float
 //                      LM: equal within its tolerance, not bit for bit.
 // A7: acosf / sinf / cosf are taken as correctly rounded -- (float) of the double function, here and in
@@ -29,7 +29,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
-#include "lm7.hpp"
+#include "lm.hpp"
 #include "vec4.hpp"
 
 #pragma clang fp contract(off)
@@ -332,8 +332,8 @@ extern "C" int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, 
     if (p->optimize && *n_inliers > 0) {
         if (*n_inliers >= 7) {
             rec = ctx->prof_begin("k_cone_lm", (double)*n_inliers * 12.0);
-            hipLaunchKernelGGL(k_lm7<ConeResidual>, dim3(1), dim3(kLmThreads), 0, s, ConeResidual{}, x, y, z, inliers,
-                               *n_inliers, bc, dref);
+            const int lrc = launch_lm7(ctx, s, ConeResidual{}, x, y, z, inliers, *n_inliers, bc, dref);
+            if (lrc != PITT_OK) return lrc;
             ctx->prof_end(rec);
         } else {
             hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, dref);

@@ -31,7 +31,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
-#include "lm7.hpp"
+#include "lm.hpp"
 #include "vec4.hpp"
 
 #pragma clang fp contract(off)
@@ -275,11 +275,12 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
     CylCoef outc = bc;
     if (p->optimize && *n_inliers > 0) {
         rec = ctx->prof_begin("k_cyl_lm", (double)*n_inliers * 12.0);
-        if (*n_inliers >= 7)
-            hipLaunchKernelGGL(k_lm7<CylResidual>, dim3(1), dim3(kLmThreads), 0, s, CylResidual{}, x, y, z, inliers,
-                               *n_inliers, bc, dref);
-        else  // Eigen's LM refuses m < n: the model stays, the direction is normalised
+        if (*n_inliers >= 7) {
+            const int lrc = launch_lm7(ctx, s, CylResidual{}, x, y, z, inliers, *n_inliers, bc, dref);
+            if (lrc != PITT_OK) return lrc;
+        } else {  // Eigen's LM refuses m < n: the model stays, the direction is normalised
             hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, dref);
+        }
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
         PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(CylCoef), hipMemcpyDeviceToHost, s));

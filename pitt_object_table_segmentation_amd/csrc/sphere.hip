@@ -18,7 +18,8 @@
 // Device pipeline: k_sph_model (one thread per attempt: the 4 x 4 determinants), k_sph_count per
 // chunk of attempts (one 2048-point tile x one hypothesis per block, ballot counts), the RANSAC replay
 // on the host over the chunk's counts (scalar control), compaction of the inliers, and for the
-// refinement k_sph_lm: the whole Levenberg-Marquardt iteration in one block (deterministic sums).
+// refinement k_lm<SphLmModel> (lm.hpp): the whole Levenberg-Marquardt iteration in one resident grid
+// (deterministic sums).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,6 +31,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
+#include "lm.hpp"
 
 #pragma clang fp contract(off)
 
@@ -123,134 +125,30 @@ struct WriteIdx {
     __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = (int32_t)i; }
 };
 
-// Levenberg-Marquardt over the inliers' residuals ||p - c|| - r in double, one block: every thread
-// sums its strided inliers (J^T J upper triangle, J^T r, r^T r), a fixed shuffle + LDS tree combines
-// them, thread 0 solves the damped 4 x 4 system and decides; control is uniform through LDS.
-constexpr int kLmThreads = 1024;
-
-__device__ void sph_lm_sums(const float* X, const float* Y, const float* Z, const int32_t* inl, int64_t m,
-                            const double* v, double (*red)[15], double* out) {
-    double acc[15];
-    for (int q = 0; q < 15; ++q) acc[q] = 0;
-    for (int64_t k = threadIdx.x; k < m; k += kLmThreads) {
-        const int id = inl[k];
-        const double dx = (double)X[id] - v[0], dy = (double)Y[id] - v[1], dz = (double)Z[id] - v[2];
+// Levenberg-Marquardt over the inliers' residuals ||p - c|| - r in double (lm.hpp's resident grid, 100
+// iterations, no diagonal floor), the coefficients written back as floats.
+struct SphLmModel {
+    static constexpr int N = 4;
+    static constexpr int kMaxIt = 100;
+    static constexpr double kDiagEps = 0.0;
+    using Out = float4;
+    float4 start;
+    __device__ void init(double* v) const {
+        v[0] = start.x, v[1] = start.y, v[2] = start.z, v[3] = start.w;
+    }
+    __device__ void residual(const double* v, float px, float py, float pz, double* J, double* f) const {
+        const double dx = (double)px - v[0], dy = (double)py - v[1], dz = (double)pz - v[2];
         const double d = sqrt(dx * dx + dy * dy + dz * dz);
-        const double r = d - v[3];
-        const double j[4] = {d > 0 ? -dx / d : 0.0, d > 0 ? -dy / d : 0.0, d > 0 ? -dz / d : 0.0, -1.0};
-        int q = 0;
-        for (int a = 0; a < 4; ++a)
-            for (int b = a; b < 4; ++b) acc[q++] += j[a] * j[b];
-        for (int a = 0; a < 4; ++a) acc[10 + a] += j[a] * r;
-        acc[14] += r * r;
+        *f = d - v[3];
+        J[0] = d > 0 ? -dx / d : 0.0;
+        J[1] = d > 0 ? -dy / d : 0.0;
+        J[2] = d > 0 ? -dz / d : 0.0;
+        J[3] = -1.0;
     }
-    for (int q = 0; q < 15; ++q) {
-        double t = acc[q];
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = t;
+    __device__ void finish(const double* xv, float4* out) const {
+        *out = make_float4((float)xv[0], (float)xv[1], (float)xv[2], (float)xv[3]);
     }
-    __syncthreads();
-    if (threadIdx.x < 15) {
-        double t = 0;
-        for (int w = 0; w < kLmThreads / 64; ++w) t += red[w][threadIdx.x];
-        out[threadIdx.x] = t;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(kLmThreads) void k_sph_lm(const float* __restrict__ X, const float* __restrict__ Y,
-                                                       const float* __restrict__ Z, const int32_t* __restrict__ inl,
-                                                       int64_t m, float4 init, float4* __restrict__ out) {
-    __shared__ double red[kLmThreads / 64][15];
-    __shared__ double cur[15], trial[15];
-    __shared__ double xv[4], xn[4];
-    __shared__ int state;  // 0 go on, 1 accepted, 2 rejected (more damping), 3 stop
-    if (threadIdx.x == 0) {
-        xv[0] = init.x, xv[1] = init.y, xv[2] = init.z, xv[3] = init.w;
-    }
-    __syncthreads();
-    sph_lm_sums(X, Y, Z, inl, m, xv, red, cur);
-    double lambda = 1e-3;  // thread 0's
-    for (int it = 0; it < 100; ++it) {
-        bool moved = false, stop = false;
-        for (;;) {
-            if (threadIdx.x == 0) {
-                state = 0;
-                if (!(lambda < 1e10)) state = 3;
-                else {
-                    double M[4][5];
-                    int q = 0;
-                    for (int r = 0; r < 4; ++r)
-                        for (int c = r; c < 4; ++c) M[r][c] = M[c][r] = cur[q++];
-                    for (int r = 0; r < 4; ++r) M[r][r] += lambda * M[r][r], M[r][4] = -cur[10 + r];
-                    for (int col = 0; col < 4 && state == 0; ++col) {
-                        int piv = col;
-                        for (int r = col + 1; r < 4; ++r)
-                            if (fabs(M[r][col]) > fabs(M[piv][col])) piv = r;
-                        if (M[piv][col] == 0) {
-                            state = 3;
-                            break;
-                        }
-                        if (piv != col)
-                            for (int c = 0; c < 5; ++c) {
-                                const double t = M[col][c];
-                                M[col][c] = M[piv][c];
-                                M[piv][c] = t;
-                            }
-                        for (int r = col + 1; r < 4; ++r) {
-                            const double f = M[r][col] / M[col][col];
-                            for (int c = col; c < 5; ++c) M[r][c] -= f * M[col][c];
-                        }
-                    }
-                    if (state == 0) {
-                        double dl[4];
-                        for (int r = 3; r >= 0; --r) {
-                            double acc = M[r][4];
-                            for (int c = r + 1; c < 4; ++c) acc -= M[r][c] * dl[c];
-                            dl[r] = acc / M[r][r];
-                        }
-                        for (int r = 0; r < 4; ++r) xn[r] = xv[r] + dl[r];
-                    }
-                }
-            }
-            __syncthreads();
-            const int st0 = state;
-            __syncthreads();  // every thread has read state before thread 0 writes it again
-            if (st0 == 3) {
-                stop = true;
-                break;
-            }
-            sph_lm_sums(X, Y, Z, inl, m, xn, red, trial);
-            if (threadIdx.x == 0) {
-                if (trial[14] < cur[14]) {
-                    double step = 0, nx = 0;
-                    for (int r = 0; r < 4; ++r) {
-                        const double d = xn[r] - xv[r];
-                        step += d * d;
-                        nx += xn[r] * xn[r];
-                        xv[r] = xn[r];
-                    }
-                    for (int q = 0; q < 15; ++q) cur[q] = trial[q];
-                    lambda *= 0.1;
-                    state = sqrt(step / (nx + 1e-300)) < 1e-12 ? 3 : 1;
-                } else {
-                    lambda *= 10;
-                    state = 2;
-                }
-            }
-            __syncthreads();
-            const int st1 = state;
-            __syncthreads();
-            if (st1 == 2) continue;
-            moved = true;
-            stop = st1 == 3;
-            break;
-        }
-        __syncthreads();
-        if (!moved || stop) break;
-    }
-    if (threadIdx.x == 0) *out = make_float4((float)xv[0], (float)xv[1], (float)xv[2], (float)xv[3]);
-}
+};
 
 }  // namespace pitt
 
@@ -377,7 +275,8 @@ extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y
         // sphere_refine; fixed reduction order, so the same bits on every run)
         float4* dref = (float4*)part;
         rec = ctx->prof_begin("k_sph_lm", (double)*n_inliers * 12.0);
-        hipLaunchKernelGGL(k_sph_lm, dim3(1), dim3(kLmThreads), 0, s, x, y, z, inliers, *n_inliers, bc, dref);
+        const int lrc = launch_lm(ctx, s, SphLmModel{bc}, x, y, z, inliers, *n_inliers, dref);
+        if (lrc != PITT_OK) return lrc;
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
         float4* hr = (float4*)ctx->pinned("sph_ref_h", 16);
