@@ -187,11 +187,13 @@ __global__ void k_cone_prepare(Coef7 m, ConeCfg cfg, ConePrep* out) {
 }
 
 struct ConeResidual {
+    static constexpr int64_t kSmall = 6144;
+    __device__ static double aux(const double* q) { return tan(q[6]); }  // q[7] below
     __device__ void operator()(const double* q, float px, float py, float pz, double J[7], double* f) const {
         const double vx = q[0] - px, vy = q[1] - py, vz = q[2] - pz;
         const double ux = q[3], uy = q[4], uz = q[5];
         const double s = ux * ux + uy * uy + uz * uz, g = ux * vx + uy * vy + uz * vz;
-        const double t = tan(q[6]), K = 1.0 + t * t;
+        const double t = q[7], K = 1.0 + t * t;
         *f = (vx * vx + vy * vy + vz * vz) - K * g * g / s;
         const double a = 2.0 * K * g / s;
         J[0] = 2.0 * vx - a * ux;

@@ -148,6 +148,8 @@ __device__ __forceinline__ void cyl_residual(const double* v, float px, float py
     J[6] = -2.0 * v[6];
 }
 struct CylResidual {
+    static constexpr int64_t kSmall = 6144;
+    __device__ static double aux(const double*) { return 0.0; }
     __device__ void operator()(const double* v, float px, float py, float pz, double J[7], double* f) const {
         cyl_residual(v, px, py, pz, J, f);
     }

@@ -4,8 +4,10 @@
 // small resident grid (deterministic sums: per lane, then a fixed wave, block and grid order).  Used by the
 // sphere (sphere.hip, 4 parameters), cylinder (cylinder.hip) and cone (cone.hip) services (7 parameters).
 //
-// A model P provides: N, kMaxIt, kDiagEps (added to the damped diagonal), init(v), residual(v, px, py, pz,
-// J[N], &f) and finish(xv, out) -- the float coefficients as PCL's optimizeModelCoefficients writes them.
+// A model P provides: N, kMaxIt, kDiagEps (added to the damped diagonal), kSmall (inlier counts up to it
+// run as one block, measured per model), init(v), aux(v) (a per-evaluation constant handed to the
+// residual as v[N]), residual(v, px, py, pz, J[N], &f) and finish(xv, out) -- the float coefficients as
+// PCL's optimizeModelCoefficients writes them.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -61,10 +63,14 @@ __device__ void lm_partial(const P& prm, const float* X, const float* Y, const f
     double acc[S];
 #pragma unroll
     for (int q = 0; q < S; ++q) acc[q] = 0;
+    double w[N + 1];  // the point, then the model's per-evaluation constant (aux: e.g. the cone's tan)
+#pragma unroll
+    for (int q = 0; q < N; ++q) w[q] = v[q];
+    w[N] = prm.aux(v);
     for (int64_t k = (int64_t)blockIdx.x * kLmThreads + threadIdx.x; k < m; k += (int64_t)gridDim.x * kLmThreads) {
         const int id = inl[k];
         double J[N], f;
-        prm.residual(v, X[id], Y[id], Z[id], J, &f);
+        prm.residual(w, X[id], Y[id], Z[id], J, &f);
         int t = 0;
 #pragma unroll
         for (int a = 0; a < N; ++a)
@@ -173,13 +179,19 @@ __global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restric
     __shared__ double stage[kLmMaxBlocks * S];
     __shared__ double cur[S], trial[S];
     __shared__ double xv[N], xn[N];  // block 0's copy of the trial point it publishes in g->xn
+    __shared__ int32_t st_s;
+    // one block (small inlier sets): partial sums straight into cur / trial, __syncthreads for the
+    // barriers, the trial point and the state in LDS -- no device-memory round trips per evaluation
+    const bool one = gridDim.x == 1;
     double v0[N];
     prm.init(v0);
     uint32_t target = 0;
-    lm_partial(prm, X, Y, Z, inl, m, v0, red, g->part[blockIdx.x]);
-    lm_grid_sync(&g->bar, target);
+    lm_partial(prm, X, Y, Z, inl, m, v0, red, one ? cur : g->part[blockIdx.x]);
     const bool ctl = blockIdx.x == 0;
-    if (ctl) lm_reduce_grid<S>(g, stage, cur);
+    if (!one) {
+        lm_grid_sync(&g->bar, target);
+        if (ctl) lm_reduce_grid<S>(g, stage, cur);
+    }
     if (ctl && threadIdx.x < N) xv[threadIdx.x] = v0[threadIdx.x];
     // control state (block 0, thread 0)
     double lambda = 1e-3;
@@ -212,18 +224,27 @@ __global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restric
             if (!stop)
                 for (int r = 0; r < N; ++r) {
                     xn[r] = xv[r] + dl[r];
-                    g->xn[r] = xn[r];
+                    if (!one) g->xn[r] = xn[r];
                 }
-            g->state = stop ? 3 : 0;
+            st_s = stop ? 3 : 0;
+            if (!one) g->state = st_s;
         }
-        lm_grid_sync(&g->bar, target);
-        if (__hip_atomic_load(&g->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) break;
         double vn[N];
+        if (one) {
+            __syncthreads();
+            if (st_s == 3) break;
 #pragma unroll
-        for (int k = 0; k < N; ++k) vn[k] = __hip_atomic_load(&g->xn[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lm_partial(prm, X, Y, Z, inl, m, vn, red, g->part[blockIdx.x]);
-        lm_grid_sync(&g->bar, target);
-        if (ctl) lm_reduce_grid<S>(g, stage, trial);
+            for (int k = 0; k < N; ++k) vn[k] = xn[k];
+            lm_partial(prm, X, Y, Z, inl, m, vn, red, trial);
+        } else {
+            lm_grid_sync(&g->bar, target);
+            if (__hip_atomic_load(&g->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) break;
+#pragma unroll
+            for (int k = 0; k < N; ++k) vn[k] = __hip_atomic_load(&g->xn[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lm_partial(prm, X, Y, Z, inl, m, vn, red, g->part[blockIdx.x]);
+            lm_grid_sync(&g->bar, target);
+            if (ctl) lm_reduce_grid<S>(g, stage, trial);
+        }
         have_trial = true;
     }
     if (ctl && threadIdx.x == 0) prm.finish(xv, out);
@@ -235,7 +256,9 @@ inline int launch_lm(pitt_ctx* ctx, hipStream_t s, const P& prm, const float* x,
                      const int32_t* inl, int64_t m, typename P::Out* out) {
     LmGlobal* g = (LmGlobal*)ctx->buf("lm_global", sizeof(LmGlobal));
     if (!g) return ctx->fail(PITT_E_NOMEM, "lm scratch");
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kLmMaxBlocks, (m + 1023) / 1024));
+    // up to P::kSmall inliers one block (no grid barrier: two device-memory round trips per evaluation
+    // cost more than the 256 threads' extra points), above that one block per 1024 inliers
+    const int G = m <= P::kSmall ? 1 : (int)std::min<int64_t>(kLmMaxBlocks, (m + 1023) / 1024);
     PITT_HIP_TRY(hipMemsetAsync(&g->bar, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_lm<P>, dim3(G), dim3(kLmThreads), 0, s, prm, x, y, z, inl, m, g, out);
     PITT_HIP_TRY(hipGetLastError());
@@ -250,11 +273,13 @@ struct Lm7Model {
     static constexpr int N = 7;
     static constexpr int kMaxIt = 200;
     static constexpr double kDiagEps = 1e-30;
+    static constexpr int64_t kSmall = R::kSmall;
     using Out = Coef7;
     Coef7 start;
     __device__ void init(double* v) const {
         for (int k = 0; k < 7; ++k) v[k] = start.c[k];
     }
+    __device__ double aux(const double* v) const { return R::aux(v); }
     __device__ void residual(const double* v, float px, float py, float pz, double* J, double* f) const {
         R{}(v, px, py, pz, J, f);
     }

@@ -131,7 +131,9 @@ struct SphLmModel {
     static constexpr int N = 4;
     static constexpr int kMaxIt = 100;
     static constexpr double kDiagEps = 0.0;
+    static constexpr int64_t kSmall = 2048;
     using Out = float4;
+    __device__ double aux(const double*) const { return 0.0; }
     float4 start;
     __device__ void init(double* v) const {
         v[0] = start.x, v[1] = start.y, v[2] = start.z, v[3] = start.w;
