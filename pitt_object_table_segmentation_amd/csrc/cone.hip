@@ -187,7 +187,7 @@ __global__ void k_cone_prepare(Coef7 m, ConeCfg cfg, ConePrep* out) {
 }
 
 struct ConeResidual {
-    static constexpr int64_t kSmall = 6144;
+    static constexpr int64_t kSmall = 2048;  // one block measured slower than the grid at 4k inliers
     __device__ static double aux(const double* q) { return tan(q[6]); }  // q[7] below
     __device__ void operator()(const double* q, float px, float py, float pz, double J[7], double* f) const {
         const double vx = q[0] - px, vy = q[1] - py, vz = q[2] - pz;
