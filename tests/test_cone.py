@@ -166,3 +166,23 @@ def test_hip_cone_edges(ctx):
     if coef is not None:
         assert np.array_equal(coef.view(np.int32), want["coef"].view(np.int32))
         assert np.array_equal(inl, want["inliers"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", ["points", "normals"])
+def test_hip_cone_nan_inputs(ctx, what):
+    """NaN coordinates or normals (a camera cloud's invalid pixels): NaN distances never count, a sample that
+    draws one gives a NaN model that counts no point; the RANSAC stage stays bit-exact."""
+    P, N, _ = cone_scene(3000, 800, 9)
+    rng = np.random.default_rng(9)
+    bad = rng.random(len(P)) < 0.05
+    (P if what == "points" else N)[bad] = np.nan
+    raw = orc.cone_segment(P, N, orc.cone_params(optimize=False))
+    inl, coef, hyp = _gpu(ctx, P, N, optimize=False)
+    assert hyp == raw["hypotheses"] and (coef is not None) == raw["ok"]
+    assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
+    assert np.array_equal(inl, raw["inliers"]) and not bad[inl].any()
+    want = orc.cone_segment(P, N)
+    inl, coef, hyp = _gpu(ctx, P, N)
+    assert same_cone(coef.astype(np.float64), want["coef"].astype(np.float64), pos=1e-5, ang=1e-9, opening=1e-6)
+    assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)

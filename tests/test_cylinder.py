@@ -125,3 +125,22 @@ def test_hip_cylinder_few_inliers(ctx):
         assert len(want["inliers"]) < 7
         assert np.array_equal(coef.view(np.int32), want["coef"].view(np.int32))
         assert np.array_equal(inl, want["inliers"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", ["points", "normals"])
+def test_hip_cylinder_nan_inputs(ctx, what):
+    """NaN coordinates or normals: NaN distances never count; the RANSAC stage stays bit-exact."""
+    P, N, _ = cylinder_scene(3000, 800, 9)
+    rng = np.random.default_rng(9)
+    bad = rng.random(len(P)) < 0.05
+    (P if what == "points" else N)[bad] = np.nan
+    raw = orc.cylinder_segment(P, N, orc.cylinder_params(optimize=False))
+    inl, coef, hyp = _gpu(ctx, P, N, optimize=False)
+    assert hyp == raw["hypotheses"] and (coef is not None) == raw["ok"]
+    assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
+    assert np.array_equal(inl, raw["inliers"]) and not bad[inl].any()
+    want = orc.cylinder_segment(P, N)
+    inl, coef, hyp = _gpu(ctx, P, N)
+    assert same_line(coef.astype(np.float64), want["coef"].astype(np.float64), ang=1e-9, dist=1e-6, rad=1e-6)
+    assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)
