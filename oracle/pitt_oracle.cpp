@@ -1257,9 +1257,14 @@ void sphere_refine(const Cloud& c, const std::vector<int>& inl, const float in[4
                 moved = true;
                 break;
             }
+            // rejected: a step already below 1e-10 relative cannot change the float result -- stop
+            // (instead of raising the damping to 1e10 through the summation noise)
+            double rs = 0, rx = 0;
+            for (int a = 0; a < 4; ++a) rs += dlt[a] * dlt[a], rx += xn[a] * xn[a];
+            if (std::sqrt(rs / (rx + 1e-300)) < 1e-10) break;
             lambda *= 10;
         }
-        if (!moved || step < 1e-12) break;
+        if (!moved || step < 1e-10) break;
     }
     for (int a = 0; a < 4; ++a) out[a] = (float)x[a];
 }
@@ -1450,8 +1455,9 @@ inline void cyl_residual(const double* v, float px, float py, float pz, double J
 }
 
 // Levenberg-Marquardt (Marquardt damping lambda * diag, x10 / x0.1) over N parameters; sums(v, jtj
-// (upper triangle, row major), jtr, cost).  Stops when no damping lowers the cost or the step is
-// below 1e-12 relative.
+// (upper triangle, row major), jtr, cost).  Stops when no damping lowers the cost, or an accepted or
+// rejected step is below 1e-10 relative (below the float coefficients' resolution; past it the damping
+// would only climb through the summation noise).
 template <int N, class Sums>
 void lm_solve(double* x, Sums sums) {
     double jtj[N * (N + 1) / 2], jtr[N], cost;
@@ -1501,9 +1507,13 @@ void lm_solve(double* x, Sums sums) {
                 moved = true;
                 break;
             }
+            // rejected: a step already below 1e-10 relative cannot change the float result -- stop
+            double rs = 0, rx = 0;
+            for (int a = 0; a < N; ++a) rs += dl[a] * dl[a], rx += xn[a] * xn[a];
+            if (std::sqrt(rs / (rx + 1e-300)) < 1e-10) break;
             lambda *= 10;
         }
-        if (!moved || step < 1e-12) break;
+        if (!moved || step < 1e-10) break;
     }
 }
 

@@ -1,6 +1,6 @@
 // lm.hpp -- the oracle's lm_solve<N> (oracle/pitt_oracle.cpp) on the device: Levenberg-Marquardt in double
 // with Marquardt damping (lambda * diag, x10 / x0.1, stop when no damping lowers the cost, the step falls
-// below 1e-12 relative or the iteration cap passes) over a model's residual summed over an inlier list by a
+// below 1e-10 relative, accepted or rejected, or the iteration cap passes) over a model's residual summed over an inlier list by a
 // small resident grid (deterministic sums: per lane, then a fixed wave, block and grid order).  Used by the
 // sphere (sphere.hip, 4 parameters), cylinder (cylinder.hip) and cone (cone.hip) services (7 parameters).
 //
@@ -167,7 +167,7 @@ __device__ __forceinline__ bool lm_solve_dev(const double* sums, double lambda, 
 
 // The oracle's lm_solve<N> on a grid of G <= kLmMaxBlocks resident blocks.  Block 0's thread 0 runs the
 // scalar control (Marquardt damping x10 / x0.1, accept on a lower cost, stop when no damping lowers it, the
-// step falls below 1e-12 relative or P::kMaxIt iterations pass); every block sums its share of the
+// step (accepted or rejected) falls below 1e-10 relative or P::kMaxIt iterations pass); every block sums its share of the
 // residuals at each trial point.  Two grid barriers per evaluation: after the trial point is published, and
 // after the partial sums are written (block 0 then reduces them over the blocks in order: deterministic).
 template <class P>
@@ -213,8 +213,15 @@ __global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restric
                     for (int q = 0; q < S; ++q) cur[q] = trial[q];
                     lambda *= 0.1;
                     ++it;
-                    stop = sqrt(step / (nx + 1e-300)) < 1e-12 || it >= P::kMaxIt;
-                } else {
+                    stop = sqrt(step / (nx + 1e-300)) < 1e-10 || it >= P::kMaxIt;
+                } else {  // a rejected step below 1e-10 relative cannot change the float result: stop
+                    double rs = 0, rx = 0;
+                    for (int r = 0; r < N; ++r) {
+                        const double d = xn[r] - xv[r];
+                        rs += d * d;
+                        rx += xn[r] * xn[r];
+                    }
+                    stop = sqrt(rs / (rx + 1e-300)) < 1e-10;
                     lambda *= 10;
                 }
             }
