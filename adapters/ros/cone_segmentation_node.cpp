@@ -27,7 +27,7 @@ bool ransacConeDetaction(pitt_msgs::PrimitiveSegmentation::Request& req, pitt_ms
     float coef[8] = {0, 0, 0, 0, 0, 0, 0, 0}, centroid[3] = {0, 0, 0};
     int32_t n_coef = 0;
     const int rc = pitt_srv_ransac_cone(pitt_ros::node().srv, cloud.data(), n, normals.data(),
-                                         pitt_ros::n_points(req.normals), inl.data(), &n_inl, coef, &n_coef, centroid);
+                                         (int64_t)normals.size() / 3, inl.data(), &n_inl, coef, &n_coef, centroid);
     if (rc < 0) {
         ROS_ERROR_STREAM("cone segmentation (MI355X) failed: " << pitt_last_error(pitt_ros::node().ctx));
         return false;

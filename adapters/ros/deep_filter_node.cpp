@@ -18,7 +18,7 @@ struct DevBuf {
     size_t bytes = 0;
     void* get(size_t b) {
         if (b > bytes) {
-            if (p) hipFree(p);
+            if (p) (void)hipFree(p);
             p = nullptr;
             bytes = 0;
             if (hipMalloc(&p, b) != hipSuccess) return nullptr;
@@ -29,18 +29,26 @@ struct DevBuf {
 };
 DevBuf g_payload, g_planes, g_out;
 
-std::vector<float> download_xyz16(const float* x, const float* y, const float* z, int64_t n) {
-    std::vector<float> sx((size_t)n), sy((size_t)n), sz((size_t)n), out((size_t)n * 4);
-    hipMemcpy(sx.data(), x, (size_t)n * 4, hipMemcpyDeviceToHost);
-    hipMemcpy(sy.data(), y, (size_t)n * 4, hipMemcpyDeviceToHost);
-    hipMemcpy(sz.data(), z, (size_t)n * 4, hipMemcpyDeviceToHost);
+bool copy_ok(hipError_t e) {
+    if (e != hipSuccess) ROS_ERROR_STREAM("deep filter: HIP copy failed: " << hipGetErrorString(e));
+    return e == hipSuccess;
+}
+
+bool download_xyz16(const float* x, const float* y, const float* z, int64_t n, std::vector<float>& out) {
+    std::vector<float> sx((size_t)n), sy((size_t)n), sz((size_t)n);
+    out.assign((size_t)n * 4, 0.0f);
+    if (n == 0) return true;
+    if (!copy_ok(hipMemcpy(sx.data(), x, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
+        !copy_ok(hipMemcpy(sy.data(), y, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
+        !copy_ok(hipMemcpy(sz.data(), z, (size_t)n * 4, hipMemcpyDeviceToHost)))
+        return false;
     for (int64_t i = 0; i < n; ++i) {
         out[4 * i] = sx[i];
         out[4 * i + 1] = sy[i];
         out[4 * i + 2] = sz[i];
         out[4 * i + 3] = 1.0f;
     }
-    return out;
+    return true;
 }
 }  // namespace
 
@@ -62,7 +70,7 @@ bool deepFiltering(pitt_msgs::DeepFilter::Request& req, pitt_msgs::DeepFilter::R
     if (!planes || !outp || !payload) return false;
     float *x = planes, *y = planes + n, *z = planes + 2 * n;
     if (n > 0) {
-        hipMemcpy(payload, m.data.data(), m.data.size(), hipMemcpyHostToDevice);
+        if (!copy_ok(hipMemcpy(payload, m.data.data(), m.data.size(), hipMemcpyHostToDevice))) return false;
         if (pitt_unpack_pointcloud2(ctx, payload, (int64_t)m.data.size(), (int32_t)m.width, (int32_t)m.height,
                                     (int32_t)m.point_step, (int64_t)m.row_step, off[0], off[1], off[2], x, y,
                                     z) != PITT_OK) {
@@ -76,9 +84,10 @@ bool deepFiltering(pitt_msgs::DeepFilter::Request& req, pitt_msgs::DeepFilter::R
             if (pitt_voxel_grid(ctx, x, y, z, n, (float)g_leaf, (float)g_leaf, (float)g_leaf, PITT_VOXEL_ORDER_PCL, v,
                                 v + n, v + 2 * n, &nv, &flags) != PITT_OK)
                 return false;
-            hipMemcpy(x, v, (size_t)nv * 4, hipMemcpyDeviceToDevice);
-            hipMemcpy(x + nv, v + n, (size_t)nv * 4, hipMemcpyDeviceToDevice);
-            hipMemcpy(x + 2 * nv, v + 2 * n, (size_t)nv * 4, hipMemcpyDeviceToDevice);
+            if (!copy_ok(hipMemcpy(x, v, (size_t)nv * 4, hipMemcpyDeviceToDevice)) ||
+                !copy_ok(hipMemcpy(x + nv, v + n, (size_t)nv * 4, hipMemcpyDeviceToDevice)) ||
+                !copy_ok(hipMemcpy(x + 2 * nv, v + 2 * n, (size_t)nv * 4, hipMemcpyDeviceToDevice)))
+                return false;
             y = x + nv;
             z = x + 2 * nv;
             n = nv;
@@ -93,8 +102,9 @@ bool deepFiltering(pitt_msgs::DeepFilter::Request& req, pitt_msgs::DeepFilter::R
         ROS_ERROR_STREAM("deep filter (MI355X) failed: " << pitt_last_error(ctx));
         return false;
     }
-    const std::vector<float> closer = download_xyz16(c, c + n, c + 2 * n, nc);
-    const std::vector<float> further = download_xyz16(f, f + n, f + 2 * n, nf);
+    std::vector<float> closer, further;
+    if (!download_xyz16(c, c + n, c + 2 * n, nc, closer) || !download_xyz16(f, f + n, f + 2 * n, nf, further))
+        return false;
     res.cloud_closer = pitt_ros::from_xyz16(closer.data(), nc);
     res.cloud_further = pitt_ros::from_xyz16(further.data(), nf);
     res.used_deep_threshold = used;

@@ -17,6 +17,8 @@
 #include <sensor_msgs/PointCloud2.h>
 #include <sensor_msgs/PointField.h>
 
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -85,8 +87,36 @@ inline void sync_params(ros::NodeHandle& nh, const std::vector<std::string>& nam
     }
 }
 
+// The payload layout check pitt_unpack_pointcloud2 applies on the device (preprocess.hip), done on
+// the host before any byte is read: little-endian only, every located field (offset + 4) inside
+// point_step, row_step >= width * point_step, and the last point's last byte inside data.
+// Returns false, with the reason, for a message whose layout would read past its payload.
+inline bool layout_ok(const sensor_msgs::PointCloud2& msg, const int* off, int nf, std::string* why) {
+    const size_t n = (size_t)msg.width * msg.height;
+    if (msg.is_bigendian) {
+        *why = "big-endian payload";
+        return false;
+    }
+    for (int k = 0; k < nf; ++k)
+        if (off[k] >= 0 && (size_t)off[k] + 4 > msg.point_step) {
+            *why = "field offset + 4 beyond point_step";
+            return false;
+        }
+    if (n == 0) return true;
+    if ((size_t)msg.row_step < (size_t)msg.width * msg.point_step) {
+        *why = "row_step < width * point_step";
+        return false;
+    }
+    if ((size_t)(msg.height - 1) * msg.row_step + (size_t)msg.width * msg.point_step > msg.data.size()) {
+        *why = "payload shorter than its layout";
+        return false;
+    }
+    return true;
+}
+
 // fromROSMsg into PointXYZ (x, y, z, pad): fields located by name, FLOAT32 only, any point_step /
-// row_step; a cloud without x/y/z fields converts to zero points (fromROSMsg warns likewise).
+// row_step; a cloud without x/y/z fields converts to zero points (fromROSMsg warns likewise).  A
+// malformed layout (layout_ok) converts to zero points as well, with an error on the log.
 inline std::vector<float> to_xyz16(const sensor_msgs::PointCloud2& msg) {
     int off[3] = {-1, -1, -1};
     const char* names[3] = {"x", "y", "z"};
@@ -96,6 +126,11 @@ inline std::vector<float> to_xyz16(const sensor_msgs::PointCloud2& msg) {
     const size_t n = (size_t)msg.width * msg.height;
     std::vector<float> out;
     if (off[0] < 0 || off[1] < 0 || off[2] < 0) return out;
+    std::string why;
+    if (!layout_ok(msg, off, 3, &why)) {
+        ROS_ERROR_STREAM("PointCloud2 rejected: " << why);
+        return out;
+    }
     out.resize(4 * n);
     for (uint32_t r = 0; r < msg.height; ++r)
         for (uint32_t c = 0; c < msg.width; ++c) {
@@ -132,7 +167,8 @@ inline sensor_msgs::PointCloud2 from_xyz16(const float* xyz16, int64_t n, bool i
 
 // fromROSMsg into PointCloud<Normal> (PCManager::normForRosMsg, pc_manager.cpp:92-97), keeping the
 // (normal_x, normal_y, normal_z) triples: fields located by name, FLOAT32 only; a missing field leaves
-// pcl::Normal's default 0.
+// pcl::Normal's default 0.  A malformed layout gives no normals (the services then fail their
+// normals-size check and answer empty, as PCL does for a size mismatch).
 inline std::vector<float> to_normals3(const sensor_msgs::PointCloud2& msg) {
     int off[3] = {-1, -1, -1};
     const char* names[3] = {"normal_x", "normal_y", "normal_z"};
@@ -140,6 +176,11 @@ inline std::vector<float> to_normals3(const sensor_msgs::PointCloud2& msg) {
         for (int k = 0; k < 3; ++k)
             if (f.name == names[k] && f.datatype == sensor_msgs::PointField::FLOAT32) off[k] = (int)f.offset;
     const size_t n = (size_t)msg.width * msg.height;
+    std::string why;
+    if (!layout_ok(msg, off, 3, &why)) {
+        ROS_ERROR_STREAM("normals PointCloud2 rejected: " << why);
+        return std::vector<float>();
+    }
     std::vector<float> out(3 * n, 0.0f);
     for (uint32_t r = 0; r < msg.height; ++r)
         for (uint32_t c = 0; c < msg.width; ++c) {

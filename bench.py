@@ -292,6 +292,12 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the clutter / PCIe / config-5 passes")
     ap.add_argument("--no-inliers", action="store_true", help="skip writing the final inlier lists")
     ap.add_argument("--pipeline", type=int, default=3, help="contexts/streams with batches in flight")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for world > 1 (nccl = RCCL over xGMI; gloo: tests)")
+    ap.add_argument("--all-ranks-device", type=int, default=-1,
+                    help="test only: every rank on this device (rehearses world > 1 on a 1-GPU box)")
+    ap.add_argument("--dump-records", default="",
+                    help="rank 0 writes the (gathered) records of batch slot 0's last step to this .npy")
     args = ap.parse_args()
 
     import torch
@@ -302,13 +308,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local if args.all_ranks_device < 0 else args.all_ranks_device
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     backend = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         backend = dist.get_backend()
-        log(f"[rank {rank}] torch.distributed backend {backend} (RCCL), world size {dist.get_world_size()}")
+        log(f"[rank {rank}] torch.distributed backend {backend}"
+            f"{' (RCCL)' if backend == 'nccl' else ''}, world size {dist.get_world_size()}, device {gpu}")
 
     import pitt_object_table_segmentation_amd as pitt
     from pitt_object_table_segmentation_amd import distributed
@@ -332,36 +343,48 @@ def main():
     # Several contexts, each on its own library-created stream (own HW queue): batch i+1 is enqueued
     # before batch i completes, so the latency-bound covariance chain of one batch overlaps the
     # HBM-bound kernels of the next.
-    ctxs = [pitt.Context(local) for _ in range(args.pipeline)]
+    ctxs = [pitt.Context(gpu) for _ in range(args.pipeline)]
     outs = [None if args.no_inliers else torch.empty(b.capacity, dtype=torch.int32, device=dev) for b in batches]
     pending = [None] * len(ctxs)
     torch.cuda.synchronize()
     params = pitt.sac_params()
     counter = [0]
+    # config 4: the records of a finished batch are gathered asynchronously (posted when the batch
+    # completes, collected one step later), so the exchange overlaps the next batch's enqueue
+    gather = (distributed.AsyncRecordGather(total, start, end - start, slots=args.pipeline + 2,
+                                            device=dev if backend == "nccl" else "cpu") if world > 1 else None)
+    posted = []                         # (ctx slot, gather handle), oldest first
+    records = [None] * len(ctxs)        # the last completed (gathered) records of each slot
+
+    def collect(keep):
+        while len(posted) > keep:
+            i, h = posted.pop(0)
+            records[i] = gather.collect(h)
+
+    def finish(i):
+        ctxs[i].wait()
+        if gather is None:
+            records[i] = pending[i]
+        else:
+            posted.append((i, gather.post(pending[i])))
+        pending[i] = None
 
     def step():
         i = counter[0] % len(ctxs)
         counter[0] += 1
-        ctx = ctxs[i]
-        done = None
         if pending[i] is not None:
-            ctx.wait()
-            done = pending[i]
-        pending[i] = ctx.plane_segment_batch_async(batches[i], params, outs[i])
-        if done is not None and world > 1:
-            done = distributed.gather_results(done, start, total, device=dev)
-        return done
+            finish(i)
+        pending[i] = ctxs[i].plane_segment_batch_async(batches[i], params, outs[i])
+        if gather is not None:
+            collect(1)
 
     def drain():
-        last = None
-        for i, c in enumerate(ctxs):
+        for i in range(len(ctxs)):
             if pending[i] is not None:
-                c.wait()
-                last = pending[i]
-                if world > 1:
-                    last = distributed.gather_results(last, start, total, device=dev)
-                pending[i] = None
-        return last
+                finish(i)
+        if gather is not None:
+            collect(0)
+        return records[(counter[0] - 1) % len(ctxs)]
 
     ctx = ctxs[0]
     for _ in range(args.warmup):
@@ -380,6 +403,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if gather is not None:
+        gather.seconds, gather.posted = 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -437,7 +462,10 @@ def main():
                 "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU",
                 "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
                 "world_size_seen": world,
-                "collective": (f"{backend} all_gather_into_tensor of per-frame records" if world > 1 else None),
+                "collective": (f"{backend} all_gather_into_tensor of per-frame records, async (collected one "
+                               "step later)" if world > 1 else None),
+                "gather_us_per_step": (round(gather.seconds / args.steps * 1e6, 1) if gather is not None else None),
+                "gathers": (gather.posted if gather is not None else None),
             },
             "roofline": {
                 "kernel": "k_score",
@@ -474,6 +502,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cl = clutter_frames[0] if clutter_frames else make_frames([0], 1, pitt.SCENE_CLUTTER)[0]
         line["cpu_baseline"] = cpu_baseline(frames0, cl, cpus, args.cpu_budget)
+    if rank == 0 and args.dump_records:
+        np.save(args.dump_records, records[0])
     if rank == 0:
         print(json.dumps(line), flush=True)
     for c in ctxs:

@@ -313,7 +313,9 @@ typedef struct {
     double   radius_min, radius_max;  /* 0.005, 0.5 (:25-26) */
     double   normal_distance_weight;  /* 0.001 (:23) */
     uint32_t seed;                    /* 12345 */
-    int32_t  pad;
+    int32_t  eigen33;                 /* getAngle3D's normalized(): 0 = Eigen 3.2 (a zero normal or a point on
+                                         the axis gives NaN: never an inlier); 1 = Eigen >= 3.3 (the zero
+                                         vector stays zero: the angle is pi/2), as pitt_cone_params */
 } pitt_cylinder_params;
 int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
                           const float* ny, const float* nz, int64_t n, const pitt_cylinder_params* params,

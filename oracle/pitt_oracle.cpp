@@ -22,6 +22,7 @@
 // scalar_product_op with Scalar(1)/other for non-integer scalars); the binary `v / s` divides.
 // Eigen >= 3.3 divides in both.  Selected by div_mode.
 #include "pitt_oracle.h"
+#include "eigen_lm.hpp"
 
 #include <algorithm>
 #include <array>
@@ -40,6 +41,12 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // A3: the 4-lane reduction of Eigen's vectorised redux (predux) in the PCL binary.
 //   SSE2 predux: (a0 + a2) + (a1 + a3); SSE3 hadd: (a0 + a1) + (a2 + a3); scalar: sequential.
+// Refinement of the sphere / cylinder / cone models (optimizeModelCoefficients): ORC_LM_PCL restates
+// PCL's own Eigen::LevenbergMarquardt<NumericalDiff<Functor>, float> (eigen_lm.hpp: float, forward
+// differences, stops at Eigen's sqrt(FLT_EPSILON) tolerances); ORC_LM_OPTIMUM runs a double
+// Levenberg-Marquardt to the least-squares optimum of the same residual (what the device computes).
+static int g_lm_mode = ORC_LM_PCL;
+
 inline float red4(float a0, float a1, float a2, float a3, int order) {
     switch (order) {
     case ORC_REDUCE_HADD: return (a0 + a1) + (a2 + a3);
@@ -1190,7 +1197,14 @@ inline bool sphere_in(const Cloud& c, int64_t i, const float m[4], double th) {
 
 // Levenberg-Marquardt in double over the inliers' residuals ||p - c|| - r (the same iteration the
 // library's host loop runs on device sums, pitt_sphere_segment).
+elm::Result pcl_lm_sphere(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m, float c[4]);
+
 void sphere_refine(const Cloud& c, const std::vector<int>& inl, const float in[4], float out[4]) {
+    if (g_lm_mode == ORC_LM_PCL) {
+        for (int k = 0; k < 4; ++k) out[k] = in[k];
+        pcl_lm_sphere(c.x, c.y, c.z, inl.data(), (int64_t)inl.size(), out);
+        return;
+    }
     double x[4] = {in[0], in[1], in[2], in[3]};
     auto sums = [&](const double* v, double* jtj, double* jtr, double* cost) {
         for (int i = 0; i < 10; ++i) jtj[i] = 0;
@@ -1423,8 +1437,10 @@ bool cyl_valid(const float c[7], double rmin, double rmax) {
     return true;
 }
 
+inline double angle3d_e(V4 a, V4 b, int eigen33);
+
 inline bool cyl_in(const float* x, const float* y, const float* z, const float* nx, const float* ny, const float* nz,
-                   int64_t i, const float c[7], double w, double th) {
+                   int64_t i, const float c[7], double w, double th, int eigen33) {
     const V4 lp = v4(c[0], c[1], c[2]), ld = v4(c[3], c[4], c[5]);
     const float ptdotdir = dot(lp, ld), dirdotdir = 1.0f / dot(ld, ld);
     const V4 pt = v4(x[i], y[i], z[i]), nn = v4(nx[i], ny[i], nz[i]);
@@ -1432,7 +1448,7 @@ inline bool cyl_in(const float* x, const float* y, const float* z, const float* 
     const float k = (dot(pt, ld) - ptdotdir) * dirdotdir;
     const V4 proj = add(lp, mul(k, ld));
     const V4 dir = normalize(sub(pt, proj));
-    double d_normal = std::fabs(angle3d(nn, dir));
+    double d_normal = std::fabs(angle3d_e(nn, dir, eigen33));
     d_normal = std::min(d_normal, M_PI - d_normal);
     return std::fabs(w * d_normal + (1 - w) * d_euclid) < th;
 }
@@ -1519,10 +1535,19 @@ void lm_solve(double* x, Sums sums) {
 
 // Levenberg-Marquardt in double on f_i = |u x (c - p_i)|^2 / |u|^2 - r^2 (OptimizationFunctor's
 // residual), parameters (c, u, r); then u normalised.
+elm::Result pcl_lm_cylinder(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m,
+                            float c[7]);
+
 void cyl_refine(const float* x, const float* y, const float* z, const std::vector<int>& inl, const float in[7],
                 float out[7]) {
     double q[7];
     for (int k = 0; k < 7; ++k) q[k] = in[k];
+    if (g_lm_mode == ORC_LM_PCL) {
+        float c[7];
+        for (int k = 0; k < 7; ++k) c[k] = in[k];
+        if (!inl.empty()) pcl_lm_cylinder(x, y, z, inl.data(), (int64_t)inl.size(), c);
+        for (int k = 0; k < 7; ++k) q[k] = c[k];
+    }
     auto sums = [&](const double* v, double* jtj /*28*/, double* jtr /*7*/, double* cost) {
         for (int k = 0; k < 28; ++k) jtj[k] = 0;
         for (int k = 0; k < 7; ++k) jtr[k] = 0;
@@ -1537,7 +1562,7 @@ void cyl_refine(const float* x, const float* y, const float* z, const std::vecto
             *cost += f * f;
         }
     };
-    if (inl.size() >= 7) lm_solve<7>(q, sums);  // Eigen's LM refuses m < n (ImproperInputParameters)
+    if (g_lm_mode != ORC_LM_PCL && inl.size() >= 7) lm_solve<7>(q, sums);  // Eigen's LM refuses m < n
     const double nu = std::sqrt(q[3] * q[3] + q[4] * q[4] + q[5] * q[5]);
     for (int k = 0; k < 3; ++k) out[k] = (float)q[k];
     // Eigen::Vector3f line_dir(...).normalize() on the float coefficients
@@ -1579,7 +1604,7 @@ extern "C" int orc_cylinder_segment(const float* x, const float* y, const float*
         }
         int n_in = 0;
         if (cyl_valid(m, p->radius_min, p->radius_max))
-            for (int64_t i = 0; i < n; ++i) n_in += cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold);
+            for (int64_t i = 0; i < n; ++i) n_in += cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold, p->eigen33);
         if (n_in > n_best) {
             n_best = n_in;
             have = true;
@@ -1601,7 +1626,7 @@ extern "C" int orc_cylinder_segment(const float* x, const float* y, const float*
         inl.clear();
         if (!cyl_valid(m, p->radius_min, p->radius_max)) return;
         for (int64_t i = 0; i < n; ++i)
-            if (cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold)) inl.push_back((int)i);
+            if (cyl_in(x, y, z, nx, ny, nz, i, m, p->normal_distance_weight, p->threshold, p->eigen33)) inl.push_back((int)i);
     };
     select(best);
     float out[7];
@@ -1713,11 +1738,18 @@ inline void cone_residual(const double* q, float px, float py, float pz, double 
 
 // optimizeModelCoefficients: Eigen's LM refuses fewer residuals than parameters (m < n:
 // ImproperInputParameters, the coefficients unchanged); the direction is normalised either way.
+elm::Result pcl_lm_cone(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m, float c[7]);
+
 void cone_refine(const float* x, const float* y, const float* z, const std::vector<int>& inl, const float in[7],
                  float out[7]) {
     double q[7];
     for (int k = 0; k < 7; ++k) q[k] = in[k];
-    if (inl.size() >= 7) {
+    if (g_lm_mode == ORC_LM_PCL) {
+        float c[7];
+        for (int k = 0; k < 7; ++k) c[k] = in[k];
+        if (!inl.empty()) pcl_lm_cone(x, y, z, inl.data(), (int64_t)inl.size(), c);
+        for (int k = 0; k < 7; ++k) q[k] = c[k];
+    } else if (inl.size() >= 7) {
         auto sums = [&](const double* v, double* jtj, double* jtr, double* cost) {
             for (int k = 0; k < 28; ++k) jtj[k] = 0;
             for (int k = 0; k < 7; ++k) jtr[k] = 0;
@@ -1820,5 +1852,154 @@ extern "C" int orc_cone_segment(const float* x, const float* y, const float* z, 
     std::memcpy(coef, out, sizeof out);
     for (size_t i = 0; i < inl.size(); ++i) inliers[i] = inl[i];
     *n_inliers = (int64_t)inl.size();
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// PCL 1.7's optimizeModelCoefficients through Eigen's float Levenberg-Marquardt (eigen_lm.hpp), with
+// each model's OptimizationFunctor (sac_model_sphere.h, sac_model_cylinder.h, sac_model_cone.h):
+//   sphere    fvec[i] = sqrtf(cen_t.dot(cen_t)) - x[3], cen_t = (p - x[0..2], 0) (Vector4f dot, A3)
+//   cylinder  fvec[i] = (float)(sqrPointToLineDistance(pt, line_pt, line_dir) - x[6] * x[6])
+//   cone      fvec[i] = (float)(sqrPointToLineDistance(pt, apex, dir) - r * r),
+//             r = tanf(x[6]) * |apex - proj(pt)| (A7: tanf as correctly rounded)
+namespace {
+inline float tanf_cr(float a) { return (float)std::tan((double)a); }
+
+elm::Result pcl_lm_sphere(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m, float c[4]) {
+    std::vector<float> v(c, c + 4);
+    auto f = [&](const float* q, float* fv) {
+        for (int64_t i = 0; i < m; ++i) {
+            const int32_t id = inl[i];
+            const float cx = x[id] - q[0], cy = y[id] - q[1], cz = z[id] - q[2];
+            fv[i] = std::sqrt(red4(cx * cx, cy * cy, cz * cz, 0.0f * 0.0f, ORC_REDUCE_SSE2)) - q[3];
+        }
+    };
+    const elm::Result r = elm::minimize(f, m, v);
+    for (int k = 0; k < 4; ++k) c[k] = v[(size_t)k];
+    return r;
+}
+
+elm::Result pcl_lm_cylinder(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m,
+                            float c[7]) {
+    std::vector<float> v(c, c + 7);
+    auto f = [&](const float* q, float* fv) {
+        const V4 lp = v4(q[0], q[1], q[2], 0.0f), ld = v4(q[3], q[4], q[5], 0.0f);
+        for (int64_t i = 0; i < m; ++i) {
+            const int32_t id = inl[i];
+            const V4 pt = v4(x[id], y[id], z[id], 0.0f);
+            fv[i] = (float)(sqr_pt_line(pt, lp, ld) - (double)(q[6] * q[6]));
+        }
+    };
+    const elm::Result r = elm::minimize(f, m, v);
+    for (int k = 0; k < 7; ++k) c[k] = v[(size_t)k];
+    return r;
+}
+
+elm::Result pcl_lm_cone(const float* x, const float* y, const float* z, const int32_t* inl, int64_t m, float c[7]) {
+    std::vector<float> v(c, c + 7);
+    auto f = [&](const float* q, float* fv) {
+        const V4 apex = v4(q[0], q[1], q[2], 0.0f), ad = v4(q[3], q[4], q[5], 0.0f);
+        const float apexdotdir = dot(apex, ad), dirdotdir = 1.0f / dot(ad, ad);
+        const float ta = tanf_cr(q[6]);
+        for (int64_t i = 0; i < m; ++i) {
+            const int32_t id = inl[i];
+            const V4 pt = v4(x[id], y[id], z[id], 0.0f);
+            const float k = (dot(pt, ad) - apexdotdir) * dirdotdir;
+            const V4 proj = add(apex, mul(k, ad));
+            const V4 h = sub(apex, proj);
+            const float rad = ta * std::sqrt(dot(h, h));
+            fv[i] = (float)(sqr_pt_line(pt, apex, ad) - (double)(rad * rad));
+        }
+    };
+    const elm::Result r = elm::minimize(f, m, v);
+    for (int k = 0; k < 7; ++k) c[k] = v[(size_t)k];
+    return r;
+}
+}  // namespace
+
+extern "C" {
+void orc_set_lm_mode(int32_t mode) { g_lm_mode = mode == ORC_LM_OPTIMUM ? ORC_LM_OPTIMUM : ORC_LM_PCL; }
+int32_t orc_get_lm_mode(void) { return g_lm_mode; }
+
+int orc_lm_refine(int32_t model, const float* x, const float* y, const float* z, const int32_t* inl, int64_t m,
+                  const float* in, float* out, int32_t mode, int32_t* status, int32_t* nfev) {
+    const int saved = g_lm_mode;
+    g_lm_mode = mode == ORC_LM_OPTIMUM ? ORC_LM_OPTIMUM : ORC_LM_PCL;
+    std::vector<int> v(inl, inl + m);
+    int st = -3, nf = 0;
+    if (g_lm_mode == ORC_LM_PCL) {
+        const int np = model == ORC_MODEL_SPHERE ? 4 : 7;
+        for (int k = 0; k < np; ++k) out[k] = in[k];
+        elm::Result r;
+        if (model == ORC_MODEL_SPHERE) {
+            if (m > 4) r = pcl_lm_sphere(x, y, z, inl, m, out);
+        } else if (m > 0) {
+            r = model == ORC_MODEL_CYLINDER ? pcl_lm_cylinder(x, y, z, inl, m, out) : pcl_lm_cone(x, y, z, inl, m, out);
+        }
+        if (model == ORC_MODEL_SPHERE ? m > 4 : m > 0) st = r.status, nf = r.nfev;
+        if (model != ORC_MODEL_SPHERE) {  // line_dir.normalize() (Vector3f: a0 + (a1 + a2), times 1 / norm)
+            const float rr = 1.0f / std::sqrt(out[3] * out[3] + (out[4] * out[4] + out[5] * out[5]));
+            out[3] *= rr;
+            out[4] *= rr;
+            out[5] *= rr;
+        }
+    } else {
+        Cloud c{x, y, z, 0};
+        if (model == ORC_MODEL_SPHERE) {
+            for (int k = 0; k < 4; ++k) out[k] = in[k];
+            if (m > 4) sphere_refine(c, v, in, out);
+        } else if (model == ORC_MODEL_CYLINDER) {
+            cyl_refine(x, y, z, v, in, out);
+        } else {
+            cone_refine(x, y, z, v, in, out);
+        }
+    }
+    g_lm_mode = saved;
+    if (status) *status = st;
+    if (nfev) *nfev = nf;
+    return 1;
+}
+}  // extern "C"
+
+// ---- independent pin of the LM restatement: the same driver instantiated in double ---------------
+// (elm::Impl<double>) on double residuals, for comparison with MINPACK's lmdif (scipy's leastsq):
+//   sphere    sqrt((dx dx + dy dy) + dz dz) - r,     d = p - c
+//   cylinder  |u x (c - p)|^2 / |u|^2 - r^2           (x, y, z components in that order)
+//   cone      |u x (a - p)|^2 / |u|^2 - (tan(t) |a - proj(p)|)^2
+extern "C" int orc_elm_fit64(int32_t model, const float* x, const float* y, const float* z, const int32_t* inl,
+                             int64_t m, const double* in, double* out, int32_t* status, int32_t* njac,
+                             int32_t* trials) {
+    const int np = model == ORC_MODEL_SPHERE ? 4 : 7;
+    std::vector<double> v(in, in + np);
+    auto cross_sq = [](double ux, double uy, double uz, double vx, double vy, double vz) {
+        const double wx = uy * vz - uz * vy, wy = uz * vx - ux * vz, wz = ux * vy - uy * vx;
+        return (wx * wx + wy * wy) + wz * wz;
+    };
+    auto f = [&](const double* q, double* fv) {
+        for (int64_t i = 0; i < m; ++i) {
+            const int32_t id = inl[i];
+            const double px = x[id], py = y[id], pz = z[id];
+            if (model == ORC_MODEL_SPHERE) {
+                const double dx = px - q[0], dy = py - q[1], dz = pz - q[2];
+                fv[i] = std::sqrt((dx * dx + dy * dy) + dz * dz) - q[3];
+            } else {
+                const double su = (q[3] * q[3] + q[4] * q[4]) + q[5] * q[5];
+                const double d2 = cross_sq(q[3], q[4], q[5], q[0] - px, q[1] - py, q[2] - pz) / su;
+                if (model == ORC_MODEL_CYLINDER) {
+                    fv[i] = d2 - q[6] * q[6];
+                } else {
+                    const double k = (((px - q[0]) * q[3] + (py - q[1]) * q[4]) + (pz - q[2]) * q[5]) / su;
+                    const double hx = k * q[3], hy = k * q[4], hz = k * q[5];
+                    const double r = std::tan(q[6]) * std::sqrt((hx * hx + hy * hy) + hz * hz);
+                    fv[i] = d2 - r * r;
+                }
+            }
+        }
+    };
+    const elm::Result r = elm::minimize(f, m, v);
+    for (int k = 0; k < np; ++k) out[k] = v[(size_t)k];
+    if (status) *status = r.status;
+    if (njac) *njac = r.njac;
+    if (trials) *trials = r.trials;
     return 1;
 }

@@ -26,6 +26,12 @@ enum { ORC_REDUCE_SSE2 = 0, ORC_REDUCE_HADD = 1, ORC_REDUCE_SEQ = 2 };
 /* A7: trig used inside eigen33: CR = float result of the double-evaluated function;
  *     LIBM = the host's atan2f/cosf/sinf (what PCL called on its platform). */
 enum { ORC_TRIG_CR = 0, ORC_TRIG_LIBM = 1 };
+/* Refinement of the sphere / cylinder / cone models (optimizeModelCoefficients):
+ * ORC_LM_PCL      PCL's Eigen::LevenbergMarquardt<NumericalDiff<Functor>, float> restated (eigen_lm.hpp):
+ *                 float, forward differences, Eigen's sqrt(FLT_EPSILON) stopping tolerances (default);
+ * ORC_LM_OPTIMUM  a double Levenberg-Marquardt to the least-squares optimum of the same residual. */
+enum { ORC_LM_PCL = 0, ORC_LM_OPTIMUM = 1 };
+enum { ORC_MODEL_SPHERE = 0, ORC_MODEL_CYLINDER = 1, ORC_MODEL_CONE = 2 };
 /* A9: Eigen 3.2 compound `v /= s` multiplies by (1/s); Eigen >= 3.3 divides. */
 enum { ORC_DIV_EIGEN32 = 0, ORC_DIV_TRUE = 1 };
 
@@ -161,7 +167,7 @@ typedef struct {
     double  radius_min, radius_max;
     double  normal_distance_weight;
     uint32_t seed;
-    int32_t pad;
+    int32_t eigen33;  // getAngle3D's normalized(): 0 = Eigen 3.2, 1 = Eigen >= 3.3 (as orc_cone_params)
 } orc_cylinder_params;
 int     orc_cylinder_segment(const float* x, const float* y, const float* z, const float* nx, const float* ny,
                              const float* nz, int64_t n, const orc_cylinder_params* p, int32_t* inliers,
@@ -199,6 +205,19 @@ int     orc_cone_from3(const float xyz[9], const float nrm[9], double min_angle,
 void    orc_axis_height(const float* x, const float* y, const float* z, int64_t n, const float coef[6],
                         int32_t mode, float* px, float* py, float* pz, float* height, int32_t* idx1,
                         int32_t* idx2, float centroid[3]);
+
+/* Process-wide refinement mode of orc_{sphere,cylinder,cone}_segment (ORC_LM_*). */
+void    orc_set_lm_mode(int32_t mode);
+int32_t orc_get_lm_mode(void);
+/* optimizeModelCoefficients alone: model ORC_MODEL_*, the inliers' indices inl[m] into x/y/z, the
+ * coefficients in[4 or 7] -> out (cylinder / cone: the direction normalised afterwards, as PCL).
+ * *status: Eigen's LevenbergMarquardtSpace::Status (ORC_LM_PCL; -3 when PCL skips the LM for too few
+ * inliers), *nfev: functor evaluations.  Returns 1. */
+int     orc_lm_refine(int32_t model, const float* x, const float* y, const float* z, const int32_t* inl, int64_t m,
+                      const float* in, float* out, int32_t mode, int32_t* status, int32_t* nfev);
+/* The LM restatement instantiated in double on double residuals (its pin against MINPACK's lmdif). */
+int     orc_elm_fit64(int32_t model, const float* x, const float* y, const float* z, const int32_t* inl, int64_t m,
+                      const double* in, double* out, int32_t* status, int32_t* njac, int32_t* trials);
 
 #ifdef __cplusplus
 }

@@ -81,7 +81,7 @@ class CylinderParams(ctypes.Structure):
     """pitt_cylinder_params (include/pitt_seg.h)."""
     _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
                 ("probability", ctypes.c_double), ("radius_min", ctypes.c_double), ("radius_max", ctypes.c_double),
-                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("eigen33", ctypes.c_int32)]
 
 
 class ConeParams(ctypes.Structure):

@@ -379,13 +379,14 @@ class Context:
 
     def cylinder_segment(self, x, y, z, nx, ny, nz, threshold: float = 0.008, max_iterations: int = 1000,
                          optimize: bool = True, radius_min: float = 0.005, radius_max: float = 0.5,
-                         normal_distance_weight: float = 0.001, probability: float = 0.99, seed: int = 12345):
+                         normal_distance_weight: float = 0.001, probability: float = 0.99, seed: int = 12345,
+                         eigen33: int = 0):
         """The cylinder service's seg.segment (cylinder_segmentation_srv.cpp:110-126; defaults :23-30) on
         device tensors (points and normals): (inliers device int32, coefficients[7] or None, hypotheses)."""
         import torch
         n = x.numel()
         prm = L.CylinderParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max,
-                               normal_distance_weight, seed, 0)
+                               normal_distance_weight, seed, eigen33)
         inl = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
         ni = ctypes.c_int64()
         coef = np.zeros(7, np.float32)

@@ -76,15 +76,22 @@ __global__ void k_cyl_model(const float* __restrict__ X, const float* __restrict
     flag[t] = ok;
 }
 
+// getAngle3D's normalized() under Eigen 3.2 (a zero vector divides: NaN, never an inlier) or
+// Eigen >= 3.3 (a zero vector stays zero: the angle is pi/2), as the cone's
+__device__ __forceinline__ CV4 cyl_normalized_e(CV4 a, int eigen33) {
+    if (eigen33 && !(cdot(a, a) > 0.0f)) return a;
+    return cnormalized(a);
+}
+
 __device__ __forceinline__ bool cyl_in(float x, float y, float z, float nx, float ny, float nz, const CylCoef& m,
-                                       double w, double th) {
+                                       double w, double th, int eigen33) {
     const CV4 lp = cv4(m.c[0], m.c[1], m.c[2]), ld = cv4(m.c[3], m.c[4], m.c[5]);
     const float ptdotdir = cdot(lp, ld), dirdotdir = 1.0f / cdot(ld, ld);
     const CV4 pt = cv4(x, y, z), nn = cv4(nx, ny, nz);
     const double d_euclid = fabs(sqrt(csqr_pt_line(pt, lp, ld)) - (double)m.c[6]);
     const float k = (cdot(pt, ld) - ptdotdir) * dirdotdir;
     const CV4 dir = cnormalize(csub(pt, cadd(lp, cmul(k, ld))));
-    double rad = cdot(cnormalized(nn), cnormalized(dir));
+    double rad = cdot(cyl_normalized_e(nn, eigen33), cyl_normalized_e(dir, eigen33));
     if (rad < -1.0) rad = -1.0;
     else if (rad > 1.0) rad = 1.0;
     double d_normal = fabs(acos(rad));
@@ -102,7 +109,8 @@ __global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, 
                                                    const float* __restrict__ NY, const float* __restrict__ NZ,
                                                    int64_t n, const CylCoef* __restrict__ coef,
                                                    const int32_t* __restrict__ flag, int a0, double w, double th,
-                                                   double rmin, double rmax, int32_t* __restrict__ counts) {
+                                                   int eigen33, double rmin, double rmax,
+                                                   int32_t* __restrict__ counts) {
     const int a = a0 + blockIdx.y;
     if (flag[a] != 1) return;
     const CylCoef m = coef[a];
@@ -113,7 +121,7 @@ __global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
-        const bool in = i < n && cyl_in(X[i], Y[i], Z[i], NX[i], NY[i], NZ[i], m, w, th);
+        const bool in = i < n && cyl_in(X[i], Y[i], Z[i], NX[i], NY[i], NZ[i], m, w, th, eigen33);
         cnt += __popcll(__ballot(in));
     }
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
@@ -125,7 +133,10 @@ struct CylIn {
     const float *x, *y, *z, *nx, *ny, *nz;
     CylCoef m;
     double w, th;
-    __device__ bool operator()(int64_t i) const { return cyl_in(x[i], y[i], z[i], nx[i], ny[i], nz[i], m, w, th); }
+    int eigen33;
+    __device__ bool operator()(int64_t i) const {
+        return cyl_in(x[i], y[i], z[i], nx[i], ny[i], nz[i], m, w, th, eigen33);
+    }
 };
 struct CylWriteIdx {
     int32_t* out;
@@ -211,7 +222,8 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
         PITT_HIP_TRY(hipMemsetAsync(dcnt + a, 0, (size_t)nh * 4, s));
         rec = ctx->prof_begin("k_cyl_count", (double)nh * (double)n * 24.0);
         hipLaunchKernelGGL(k_cyl_count, dim3((unsigned)ntc, (unsigned)nh), dim3(256), 0, s, x, y, z, nx, ny, nz, n, dcoef,
-                           dflag, (int)a, p->normal_distance_weight, p->threshold, p->radius_min, p->radius_max,
+                           dflag, (int)a, p->normal_distance_weight, p->threshold, (int)p->eigen33, p->radius_min,
+                           p->radius_max,
                            dcnt + a);
         ctx->prof_end(rec);
         PITT_HIP_TRY(hipGetLastError());
@@ -261,7 +273,7 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
             *n_inliers = 0;
             return PITT_OK;
         }
-        CylIn pred{x, y, z, nx, ny, nz, m, p->normal_distance_weight, p->threshold};
+        CylIn pred{x, y, z, nx, ny, nz, m, p->normal_distance_weight, p->threshold, (int)p->eigen33};
         hipLaunchKernelGGL(k_pred_count<CylIn>, dim3(g), dim3(kBlock), 0, s, pred, n, tc);
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, nt, to);
         hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, CylWriteIdx{inliers}, n,

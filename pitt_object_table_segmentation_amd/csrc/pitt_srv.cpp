@@ -125,7 +125,7 @@ bool SegmentationServices::ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentat
     p.radius_max = maxRadiusLimit;
     p.normal_distance_weight = normalDistanceWeight;
     p.seed = 12345u;
-    p.pad = 0;
+    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain)
     const size_t n = req.cloud.size();
     std::vector<int32_t> inl(n + 1);
     int64_t n_inl = 0;
@@ -193,7 +193,7 @@ bool SegmentationServices::ransacConeDetaction(pitt_msgs::PrimitiveSegmentation:
     p.axis[0] = p.axis[1] = p.axis[2] = 0.0f;
     p.eigen33 = 0;
     p.seed = 12345u;
-    p.pad = 0;
+    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain)
     const size_t n = req.cloud.size();
     std::vector<int32_t> inl(n + 1);
     int64_t n_inl = 0;

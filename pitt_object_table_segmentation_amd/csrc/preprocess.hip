@@ -383,14 +383,17 @@ int pitt_unpack_pointcloud2(pitt_ctx* ctx, const void* data, int64_t data_bytes,
     if (point_step % 4 != 0 || row_step % 4 != 0 || ((uintptr_t)data & 3u) != 0 ||
         (height > 1 && row_step < (int64_t)width * point_step))
         return ctx->fail(PITT_E_INVALID, "point_step / row_step / alignment");
+    int64_t need = 0;
     if (n > 0) {  // the last point's last field must lie inside the payload
         const int32_t omax = std::max(off_x, std::max(off_y, off_z));
-        const int64_t need = (int64_t)(height - 1) * row_step + (int64_t)(width - 1) * point_step + omax + 4;
+        need = (int64_t)(height - 1) * row_step + (int64_t)(width - 1) * point_step + omax + 4;
         if (data_bytes < need) return ctx->fail(PITT_E_INVALID, "PointCloud2 payload shorter than its layout");
     }
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    // The fast path reads a whole 16-byte point: only when the last point's 16 bytes are inside the
+    // payload too (a payload may end right after the last z: 4 bytes short of a float4).
     const int xyz16 = point_step == 16 && off_x == 0 && off_y == 4 && off_z == 8 && row_step % 16 == 0 &&
-                      ((uintptr_t)data & 15u) == 0;
+                      ((uintptr_t)data & 15u) == 0 && data_bytes >= need + 4;
     hipStream_t s = ctx->stream;
     const int rec = ctx->prof_begin("k_unpack_pc2", (double)n * (12.0 + (xyz16 ? 16.0 : 12.0)));
     if (n > 0)

@@ -38,18 +38,23 @@ def pack_records(results: np.ndarray, frame_ids: np.ndarray, slots: int) -> np.n
 
 
 def unpack_records(buf: np.ndarray, n_frames: int) -> np.ndarray:
-    """Inverse of pack_records over the gathered buffer; returns results ordered by frame id."""
-    buf = np.ascontiguousarray(buf.reshape(-1, 8 + RECORD_BYTES))
-    ids = buf[:, :8].copy().view(np.int64).reshape(-1)
-    recs = buf[:, 8:].copy().view(RESULT_DTYPE).reshape(-1)
-    out = np.zeros(n_frames, RESULT_DTYPE)
-    seen = np.zeros(n_frames, bool)
-    for i, r in zip(ids, recs):
-        if i >= 0:
-            out[i] = r
-            seen[i] = True
-    if not seen.all():
-        raise RuntimeError(f"gather lost frames: {np.nonzero(~seen)[0][:8]}")
+    """Inverse of pack_records over the gathered buffer; returns results ordered by frame id.
+
+    Vectorised: the frame ids index the output directly (fancy indexing, no per-record Python
+    loop), and np.bincount checks that every frame arrived exactly once."""
+    buf = np.ascontiguousarray(buf, np.uint8).reshape(-1, 8 + RECORD_BYTES)
+    ids = np.ascontiguousarray(buf[:, :8]).view(np.int64).reshape(-1)
+    recs = np.ascontiguousarray(buf[:, 8:]).view(RESULT_DTYPE).reshape(-1)
+    live = ids >= 0
+    ids, recs = ids[live], recs[live]
+    if len(ids) and (ids.max() >= n_frames):
+        raise RuntimeError(f"gather carried frame ids beyond the batch: {ids[ids >= n_frames][:8]}")
+    seen = np.bincount(ids, minlength=n_frames)
+    if not (seen == 1).all():
+        lost, dup = np.nonzero(seen == 0)[0], np.nonzero(seen > 1)[0]
+        raise RuntimeError(f"gather lost frames {lost[:8]} / duplicated frames {dup[:8]}")
+    out = np.empty(n_frames, RESULT_DTYPE)
+    out[ids] = recs
     return out
 
 
@@ -105,3 +110,65 @@ def gather_inliers(inliers: np.ndarray, counts: np.ndarray, device=None):
     out_i = np.concatenate([all_i[r, :metas[r, 0]] for r in range(world)]) if world else np.zeros(0, np.int32)
     out_c = np.concatenate([all_c[r, :metas[r, 1]] for r in range(world)]) if world else np.zeros(0, np.int64)
     return out_i, out_c
+
+
+class AsyncRecordGather:
+    """The per-step result gather of config 4, taken off the ranks' critical path.
+
+    post() packs a finished batch's records into a staging slot and enqueues the all_gather
+    without waiting (async_op); collect() completes a posted gather and unpacks it.  The bench
+    posts batch i's records as soon as batch i is done and collects them one step later, so the
+    exchange runs while the next batch is being enqueued.  Staging slots rotate (one per posted,
+    uncollected gather), so a slot is never rewritten while its copy or collective is in flight.
+
+    device: 'cuda:k' for the nccl (= RCCL over xGMI) backend -- the records go through a pinned
+    host slot and a non-blocking H2D copy -- or 'cpu' for gloo.
+    """
+
+    def __init__(self, n_frames: int, frame_start: int, n_local: int, slots: int = 4, device="cpu"):
+        import torch
+        import torch.distributed as dist
+
+        self.world = dist.get_world_size()
+        self.n_frames = n_frames
+        self.per_rank = -(-n_frames // self.world)
+        self.ids = np.arange(frame_start, frame_start + n_local, dtype=np.int64)
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        nb = self.per_rank * (8 + RECORD_BYTES)
+        self.host = [torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda) for _ in range(slots)]
+        self.src = [h.to(self.device) if self.cuda else h for h in self.host]
+        self.dst = [torch.empty(self.world * nb, dtype=torch.uint8, device=self.device) for _ in range(slots)]
+        self.next = 0
+        self.busy = [False] * slots
+        self.seconds = 0.0  # host time spent in post() + collect()
+        self.posted = 0
+
+    def post(self, results: np.ndarray):
+        import time
+        import torch.distributed as dist
+
+        t = time.perf_counter()
+        k = self.next
+        if self.busy[k]:
+            raise RuntimeError("AsyncRecordGather: every staging slot is in flight (collect first)")
+        self.next = (k + 1) % len(self.host)
+        self.busy[k] = True
+        self.host[k].numpy()[:] = pack_records(results, self.ids, self.per_rank).reshape(-1)
+        if self.cuda:
+            self.src[k].copy_(self.host[k], non_blocking=True)
+        work = dist.all_gather_into_tensor(self.dst[k], self.src[k], async_op=True)
+        self.posted += 1
+        self.seconds += time.perf_counter() - t
+        return (k, work)
+
+    def collect(self, handle) -> np.ndarray:
+        import time
+
+        t = time.perf_counter()
+        k, work = handle
+        work.wait()
+        out = unpack_records(self.dst[k].cpu().numpy(), self.n_frames)
+        self.busy[k] = False
+        self.seconds += time.perf_counter() - t
+        return out

@@ -340,14 +340,14 @@ def sphere_segment(x, y, z, params=None, counts_cap=20000):
 class CylinderParams(ctypes.Structure):
     _fields_ = [("threshold", ctypes.c_double), ("max_iterations", ctypes.c_int32), ("optimize", ctypes.c_int32),
                 ("probability", ctypes.c_double), ("radius_min", ctypes.c_double), ("radius_max", ctypes.c_double),
-                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("pad", ctypes.c_int32)]
+                ("normal_distance_weight", ctypes.c_double), ("seed", ctypes.c_uint32), ("eigen33", ctypes.c_int32)]
 
 
 def cylinder_params(threshold=0.008, max_iterations=1000, optimize=True, radius_min=0.005, radius_max=0.5,
-                    normal_distance_weight=0.001, probability=0.99, seed=12345):
+                    normal_distance_weight=0.001, probability=0.99, seed=12345, eigen33=0):
     """cylinder_segmentation_srv.cpp:23-30 defaults."""
     return CylinderParams(threshold, max_iterations, int(optimize), probability, radius_min, radius_max,
-                          normal_distance_weight, seed, 0)
+                          normal_distance_weight, seed, eigen33)
 
 
 O.orc_cylinder_segment.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.POINTER(CylinderParams)] + \
@@ -413,3 +413,67 @@ def cone_segment(xyz, nrm, params=None):
     ok = O.orc_cone_segment(*(_fp(c) for c in cols), n, ctypes.byref(p), _ip(inl), ctypes.byref(ni), _fp(coef),
                             _fp(best), ctypes.byref(hyp))
     return {"ok": bool(ok), "inliers": inl[:ni.value].copy(), "coef": coef, "best": best, "hypotheses": hyp.value}
+
+
+# ---- primitive refinement: PCL's float Eigen LM (default) vs the least-squares optimum -------------
+LM_PCL, LM_OPTIMUM = 0, 1
+MODEL_SPHERE, MODEL_CYLINDER, MODEL_CONE = 0, 1, 2
+O.orc_set_lm_mode.argtypes = [ctypes.c_int32]
+O.orc_get_lm_mode.restype = ctypes.c_int32
+O.orc_lm_refine.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+
+
+def set_lm_mode(mode):
+    O.orc_set_lm_mode(mode)
+
+
+def get_lm_mode():
+    return O.orc_get_lm_mode()
+
+
+def lm_refine(model, xyz, inliers, coef, mode=LM_PCL):
+    """optimizeModelCoefficients alone (orc_lm_refine): returns (coefficients, Eigen status, nfev)."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    cols = [np.ascontiguousarray(xyz[:, k]) for k in range(3)]
+    inl = np.ascontiguousarray(inliers, np.int32)
+    cin = np.ascontiguousarray(coef, np.float32)
+    out = np.zeros(len(cin), np.float32)
+    st, nf = ctypes.c_int32(), ctypes.c_int32()
+    O.orc_lm_refine(model, *(_fp(c) for c in cols), _ip(inl), len(inl), _fp(cin), _fp(out), mode, ctypes.byref(st),
+                    ctypes.byref(nf))
+    return out, st.value, nf.value
+
+
+O.orc_elm_fit64.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+
+
+def elm_fit64(model, xyz, inliers, coef):
+    """The Eigen LM restatement instantiated in double (orc_elm_fit64): (x, status, njac, trials)."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    cols = [np.ascontiguousarray(xyz[:, k]) for k in range(3)]
+    inl = np.ascontiguousarray(inliers, np.int32)
+    cin = np.ascontiguousarray(coef, np.float64)
+    out = np.zeros(len(cin), np.float64)
+    st, nj, tr = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    O.orc_elm_fit64(model, *(c.ctypes.data for c in cols), inl.ctypes.data, len(inl), cin.ctypes.data,
+                    out.ctypes.data, ctypes.byref(st), ctypes.byref(nj), ctypes.byref(tr))
+    return out, st.value, nj.value, tr.value
+
+
+class lm_mode:
+    """with orc.lm_mode(orc.LM_OPTIMUM): ... -- the oracle's refinement mode inside the block."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.saved = get_lm_mode()
+        set_lm_mode(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_lm_mode(self.saved)

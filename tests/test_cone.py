@@ -78,7 +78,8 @@ def test_oracle_cone_from3_analytic():
 def test_oracle_cone_recovers_and_refines(seed):
     from scipy.optimize import least_squares
     P, N, a = cone_scene(3000, 1000, seed)
-    res = orc.cone_segment(P, N)
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        res = orc.cone_segment(P, N)
     assert res["ok"] and len(res["inliers"]) > 2500
     c = res["coef"].astype(np.float64)
     assert same_cone(c, np.r_[0.3, -0.1, 1.1, a, np.deg2rad(25.0)], pos=3e-3, ang=1e-3, opening=5e-3)
@@ -109,6 +110,17 @@ def test_oracle_cone_edges():
     assert res["ok"] and len(res["inliers"]) > 1200
 
 
+# the least-squares optimum (the device) against PCL's float LM stopping point: apex (m), axis
+# 1 - |cos|, tan^2 of the opening angle (measured envelope in tests/test_pcl_lm.py, with margin)
+CONE_PCL_TOL = dict(pos=1e-4, ang=1e-7, opening=1e-4)
+
+
+def _optimum(fn, *a):
+    """The oracle in its least-squares-optimum refinement mode (what the device computes)."""
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        return fn(*a)
+
+
 def _gpu(ctx, P, N, **kw):
     import torch
     t = [torch.from_numpy(np.ascontiguousarray(a[:, k])).cuda() for a in (P, N) for k in range(3)]
@@ -130,11 +142,16 @@ def test_hip_cone_matches_oracle(ctx, n, n_out, seed, half):
     assert hyp == raw["hypotheses"]
     assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
     assert np.array_equal(inl, raw["inliers"])
-    want = orc.cone_segment(P, N)
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        want = _optimum(orc.cone_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert hyp == want["hypotheses"]
     assert same_cone(coef.astype(np.float64), want["coef"].astype(np.float64), pos=1e-5, ang=1e-9, opening=1e-6)
     assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)
+    # against PCL's float Eigen LM: within its stopping envelope (tests/test_pcl_lm.py)
+    pcl = orc.cone_segment(P, N)
+    assert same_cone(coef.astype(np.float64), pcl["coef"].astype(np.float64), **CONE_PCL_TOL)
+    assert len(np.setxor1d(inl, pcl["inliers"])) <= max(2, len(pcl["inliers"]) // 2000)
 
 
 @pytest.mark.gpu
@@ -160,7 +177,7 @@ def test_hip_cone_edges(ctx):
     assert (coef is not None) == want["ok"] and hyp == want["hypotheses"] and len(inl) == len(want["inliers"]) == 0
     # fewer than 7 inliers: the model is kept, only the direction normalised
     P, N, _ = cone_scene(5, 0, 5)
-    want = orc.cone_segment(P, N)
+    want = _optimum(orc.cone_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert (coef is not None) == want["ok"] and hyp == want["hypotheses"]
     if coef is not None:
@@ -182,7 +199,7 @@ def test_hip_cone_nan_inputs(ctx, what):
     assert hyp == raw["hypotheses"] and (coef is not None) == raw["ok"]
     assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
     assert np.array_equal(inl, raw["inliers"]) and not bad[inl].any()
-    want = orc.cone_segment(P, N)
+    want = _optimum(orc.cone_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert same_cone(coef.astype(np.float64), want["coef"].astype(np.float64), pos=1e-5, ang=1e-9, opening=1e-6)
     assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)

@@ -50,7 +50,7 @@ def same_line(c1, c2, ang=1e-4, dist=1e-5, rad=1e-5):
 def test_oracle_cylinder_recovers_and_refines(seed):
     from scipy.optimize import least_squares
     P, N, a = cylinder_scene(3000, 1000, seed)
-    res = orc.cylinder_segment(P, N)
+    res = _optimum(orc.cylinder_segment, P, N)
     assert res["ok"] and len(res["inliers"]) > 2500
     c = res["coef"]
     assert abs(abs(np.dot(c[3:6], a)) - 1) < 1e-3 and abs(c[6] - 0.04) < 1e-3
@@ -74,6 +74,17 @@ def test_oracle_cylinder_edges():
     assert not res["ok"] or len(res["inliers"]) == 0
 
 
+# the least-squares optimum (the device) against PCL's float LM stopping point: axis 1 - |cos|,
+# distance between the axis lines (m), radius (m) (measured envelope in tests/test_pcl_lm.py)
+CYL_PCL_TOL = dict(ang=1e-7, dist=5e-5, rad=5e-5)
+
+
+def _optimum(fn, *a):
+    """The oracle in its least-squares-optimum refinement mode (what the device computes)."""
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        return fn(*a)
+
+
 def _gpu(ctx, P, N, **kw):
     import torch
     t = [torch.from_numpy(np.ascontiguousarray(a[:, k])).cuda() for a in (P, N) for k in range(3)]
@@ -90,11 +101,15 @@ def test_hip_cylinder_matches_oracle(ctx, n, n_out, seed):
     assert hyp == raw["hypotheses"]
     assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
     assert np.array_equal(inl, raw["inliers"])
-    want = orc.cylinder_segment(P, N)
+    want = _optimum(orc.cylinder_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert hyp == want["hypotheses"]
     assert same_line(coef.astype(np.float64), want["coef"].astype(np.float64), ang=1e-9, dist=1e-6, rad=1e-6)
     assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)
+    # against PCL's float Eigen LM: the same line and radius within its stopping envelope
+    pcl = orc.cylinder_segment(P, N)
+    assert same_line(coef.astype(np.float64), pcl["coef"].astype(np.float64), **CYL_PCL_TOL)
+    assert len(np.setxor1d(inl, pcl["inliers"])) <= max(2, len(pcl["inliers"]) // 2000)
 
 
 @pytest.mark.gpu
@@ -118,7 +133,7 @@ def test_hip_cylinder_edges(ctx):
 def test_hip_cylinder_few_inliers(ctx):
     """Fewer than 7 inliers: Eigen's LM refuses m < n, the model stays and only the direction is normalised."""
     P, N, _ = cylinder_scene(5, 0, 5)
-    want = orc.cylinder_segment(P, N)
+    want = _optimum(orc.cylinder_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert (coef is not None) == want["ok"] and hyp == want["hypotheses"]
     if coef is not None:
@@ -140,7 +155,38 @@ def test_hip_cylinder_nan_inputs(ctx, what):
     assert hyp == raw["hypotheses"] and (coef is not None) == raw["ok"]
     assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
     assert np.array_equal(inl, raw["inliers"]) and not bad[inl].any()
-    want = orc.cylinder_segment(P, N)
+    want = _optimum(orc.cylinder_segment, P, N)
     inl, coef, hyp = _gpu(ctx, P, N)
     assert same_line(coef.astype(np.float64), want["coef"].astype(np.float64), ang=1e-9, dist=1e-6, rad=1e-6)
     assert len(np.setxor1d(inl, want["inliers"])) <= max(2, len(want["inliers"]) // 2000)
+
+
+def _zero_normals(seed):
+    P, N, _ = cylinder_scene(3000, 600, seed)
+    rng = np.random.default_rng(seed)
+    zero = rng.random(len(P)) < 0.2
+    N[zero] = 0.0
+    return P, N, zero
+
+
+def test_oracle_cylinder_zero_normals_eigen_conventions():
+    """A zero normal (the ROS adapter's fill for a cloud without normal fields): Eigen 3.2's
+    normalized() gives NaN, so the point never counts; Eigen >= 3.3 keeps it zero (angle pi/2), and
+    with the 0.001 normal weight such points can count (the cylinder follows the cone)."""
+    P, N, zero = _zero_normals(21)
+    e32 = orc.cylinder_segment(P, N, orc.cylinder_params(optimize=False, eigen33=0))
+    e33 = orc.cylinder_segment(P, N, orc.cylinder_params(optimize=False, eigen33=1))
+    assert e32["ok"] and e33["ok"]
+    assert not zero[e32["inliers"]].any()
+    assert zero[e33["inliers"]].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("eigen33", [0, 1])
+def test_hip_cylinder_zero_normals(ctx, eigen33):
+    P, N, _ = _zero_normals(21)
+    raw = orc.cylinder_segment(P, N, orc.cylinder_params(optimize=False, eigen33=eigen33))
+    inl, coef, hyp = _gpu(ctx, P, N, optimize=False, eigen33=eigen33)
+    assert hyp == raw["hypotheses"] and (coef is not None) == raw["ok"]
+    assert np.array_equal(coef.view(np.int32), raw["coef"].view(np.int32))
+    assert np.array_equal(inl, raw["inliers"])

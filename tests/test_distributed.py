@@ -1,8 +1,11 @@
 """World-size-2 `gloo` tests of the frame-sharded path (config 4).  CPU: the gather of fixed-size
 records and of variable-length inlier lists (the multi-GPU path's only collectives).  GPU: the
 whole shard -> segment -> gather path on the HIP kernels, byte-equal to one single-batch run."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -47,6 +50,65 @@ def _worker(rank, world, port, n_frames, out_q):
         out_q.put((rank, got.tobytes() == allrec.tobytes() and ok_inl))
     finally:
         dist.destroy_process_group()
+
+
+def _async_worker(rank, world, port, n_frames, out_q):
+    """AsyncRecordGather as bench.py drives it: several gathers posted before the oldest is collected."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, e = distributed.shard_range(n_frames, world, rank)
+        g = distributed.AsyncRecordGather(n_frames, s, e - s, slots=3, device="cpu")
+        recs = [_records(n_frames) for _ in range(4)]
+        for k in range(4):
+            recs[k]["hypotheses"] += k  # distinct per step
+        handles, got = [], []
+        for k in range(4):
+            handles.append(g.post(recs[k][s:e]))
+            if len(handles) > 2:
+                got.append(g.collect(handles.pop(0)))
+        got += [g.collect(h) for h in handles]
+        out_q.put((rank, all(a.tobytes() == b.tobytes() for a, b in zip(got, recs)) and g.posted == 4))
+    except Exception as ex:
+        out_q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("n_frames", [16, 13])
+def test_gloo_world2_async_gather(n_frames):
+    """bench.py's config-4 exchange: gathers posted asynchronously and collected later, in order."""
+    assert _spawn(_async_worker, 2, n_frames) == {0: True, 1: True}
+
+
+def test_unpack_records_vectorised_checks():
+    rec = _records(6)
+    buf = np.concatenate([distributed.pack_records(rec[:3], np.arange(3), 4),
+                          distributed.pack_records(rec[3:], np.arange(3, 6), 4)])
+    assert distributed.unpack_records(buf, 6).tobytes() == rec.tobytes()
+    # a permuted buffer unpacks to the same frame order
+    assert distributed.unpack_records(buf[::-1].copy(), 6).tobytes() == rec.tobytes()
+    with pytest.raises(RuntimeError, match="lost"):
+        distributed.unpack_records(buf[:4], 6)
+    dup = buf.copy()
+    dup[1] = dup[0]
+    with pytest.raises(RuntimeError, match="duplicated"):
+        distributed.unpack_records(dup, 6)
 
 
 @pytest.mark.parametrize("n_frames", [16, 13])
@@ -127,3 +189,38 @@ def test_config4_sharded_hip_path_equals_single_batch(ctx):
         assert ginl == ref_inl.tobytes(), f"rank {rank}: gathered inlier lists differ"
         assert gcnt == ref["n_inliers"].astype(np.int64).tobytes()
     assert sorted(r for r, *_ in got) == [0, 1]
+
+
+# ---- bench.py's own world > 1 branch, rehearsed on the 1-GPU box -------------------------------
+def _run_bench(world, frames_per_gpu, dump, port):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--steps", "4", "--warmup", "1", "--pipeline", "2", "--frames-per-gpu", str(frames_per_gpu),
+              "--no-extras", "--no-cpu-baseline", "--dump-records", dump]
+    if world == 1:
+        cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "1"] + common
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+               "--gpus", str(world), "--dist-backend", "gloo", "--all-ranks-device", "0"] + common
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_world2_gloo_equals_world1(tmp_path):
+    """bench.py's world > 1 branch (shards, async record gather, barriers, max
+    over ranks) runs at world 2 -- gloo, both ranks on device 0 -- and the gathered records of 2 x B
+    frames are byte-equal to a world-1 run over the same 2 B frames."""
+    B = 4
+    one = _run_bench(1, 2 * B, str(tmp_path / "w1.npy"), _free_port())
+    two = _run_bench(2, B, str(tmp_path / "w2.npy"), _free_port())
+    assert one["config"]["world_size_seen"] == 1 and two["config"]["world_size_seen"] == 2
+    assert two["n_gpus"] == 2 and two["config"]["gather_us_per_step"] is not None
+    assert two["config"]["gathers"] == 4 and "gloo" in two["config"]["collective"]
+    r1, r2 = np.load(tmp_path / "w1.npy"), np.load(tmp_path / "w2.npy")
+    assert r1.dtype == pitt.RESULT_DTYPE and len(r1) == 2 * B
+    assert r1.tobytes() == r2.tobytes()

@@ -173,6 +173,19 @@ def test_unpack_pointcloud2_rejects_bad_layout(ctx):
     assert x.numel() == 4
 
 
+def test_unpack_pointcloud2_payload_ends_after_last_z(ctx):
+    """a PointXYZ payload that ends right after the last point's z (width * 16 - 4 bytes)
+    is valid; the 16-byte load path would read 4 bytes past it, so the scalar path must take it."""
+    rng = np.random.default_rng(6)
+    n = 4099
+    xyz = rng.normal(size=(n, 3)).astype(np.float32)
+    buf = np.zeros((n, 4), np.float32)
+    buf[:, :3] = xyz
+    raw = buf.view(np.uint8).reshape(-1)[:n * 16 - 4].copy()
+    dx, dy, dz = ctx.unpack_pointcloud2(torch.from_numpy(raw).cuda(), n, 1, 16, n * 16)
+    assert _same(_host((dx, dy, dz)), xyz)
+
+
 def test_preprocessed_frames_through_plane_batch(ctx):
     """PointCloud2 payloads -> unpack -> deep filter -> world transform on the device, then the frames
     (now of different sizes) through the batched plane RANSAC; every stage and the RANSAC results

@@ -147,12 +147,12 @@ def test_call_ransac_plane_client(srv):
 
 def test_sphere_handler(srv):
     """ransacSphereDetection (sphere_segmentation_srv.cpp:29-96): params, Q1, centroid = centre."""
-    from test_sphere import sphere_scene
+    from test_sphere import SPHERE_PCL_ATOL, sphere_scene
     xyz = sphere_scene(1500, 800, 9)
     ok, inl, coef, centroid = srv.ransac_sphere(xyz)
-    want = orc.sphere_segment(*xyz.T)
+    want = orc.sphere_segment(*xyz.T)  # PCL's float Eigen LM refinement
     assert ok and want["ok"] and len(coef) == 4
-    assert np.allclose(coef, want["coef"], rtol=2e-6, atol=1e-7)
+    assert np.allclose(coef, want["coef"], rtol=0, atol=SPHERE_PCL_ATOL)
     assert np.array_equal(centroid, coef[:3])
     ref = want["inliers"][want["inliers"] != 0]
     assert len(np.setxor1d(inl, ref)) <= max(3, len(ref) // 1000) and 0 not in inl
@@ -172,12 +172,12 @@ def test_sphere_handler(srv):
 def test_cylinder_handler(srv):
     """ransacCylinderDetaction (cylinder_segmentation_srv.cpp:82-216): the model, then the axis height
     pushed after the 7 coefficients and the centroid of the farthest projected pair (:129-200)."""
-    from test_cylinder import cylinder_scene, same_line
+    from test_cylinder import CYL_PCL_TOL, cylinder_scene, same_line
     P, N, _ = cylinder_scene(1500, 500, 11)
     ok, inl, coef, centroid = srv.ransac_cylinder(P, N)
     want = orc.cylinder_segment(P, N)
     assert ok and want["ok"] and len(coef) == 8
-    assert same_line(coef[:7].astype(np.float64), want["coef"].astype(np.float64), ang=1e-9, dist=1e-6, rad=1e-6)
+    assert same_line(coef[:7].astype(np.float64), want["coef"].astype(np.float64), **CYL_PCL_TOL)
     # the post-processing on the handler's own coefficients: bit-exact against the restatement
     h, i1, i2, cen, _ = orc.axis_height(*P.T, coef[:6], 0)
     assert np.float32(coef[7]).view(np.int32) == np.float32(h).view(np.int32)
@@ -193,12 +193,12 @@ def test_cone_handler(srv):
     """ransacConeDetaction (cone_segmentation_srv.cpp:83-216): the parameter-server defaults (:24-31, the
     opening angles converted at :124), the model, then the axis height pushed after the 7 coefficients and
     the centroid apex + 3/4 height along the axis (:129-200)."""
-    from test_cone import cone_scene, same_cone
+    from test_cone import CONE_PCL_TOL, cone_scene, same_cone
     P, N, _ = cone_scene(1500, 500, 11)
     ok, inl, coef, centroid = srv.ransac_cone(P, N)
     want = orc.cone_segment(P, N)
     assert ok and want["ok"] and len(coef) == 8
-    assert same_cone(coef[:7].astype(np.float64), want["coef"].astype(np.float64), pos=1e-5, ang=1e-9, opening=1e-6)
+    assert same_cone(coef[:7].astype(np.float64), want["coef"].astype(np.float64), **CONE_PCL_TOL)
     # the post-processing on the handler's own coefficients: bit-exact against the restatement
     h, i1, i2, cen, _ = orc.axis_height(*P.T, coef[:6], 1)
     assert np.float32(coef[7]).view(np.int32) == np.float32(h).view(np.int32)

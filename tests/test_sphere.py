@@ -50,11 +50,12 @@ def test_oracle_sphere_from4_recovers_the_sphere():
 def test_oracle_sphere_ransac_and_refinement(seed):
     from scipy.optimize import least_squares
     p = sphere_scene(3000, 1500, seed)
-    res = orc.sphere_segment(*p.T)
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        res = orc.sphere_segment(*p.T)
     assert res["ok"] and len(res["inliers"]) > 2500
     c = res["coef"]
     assert np.allclose(c[:3], (0.3, -0.2, 1.1), atol=1e-3) and abs(c[3] - 0.05) < 1e-3
-    # the refinement is the float64 least-squares optimum over the pre-refinement inliers
+    # the optimum mode's refinement is the float64 least-squares optimum over the pre-refinement inliers
     b = res["best"]
     q = p.astype(np.float64)
     d = q - b[:3].astype(np.float64)
@@ -77,6 +78,11 @@ def test_oracle_sphere_edges():
     assert res["ok"] and len(res["inliers"]) > 1500
 
 
+# |device (least-squares optimum) - PCL's float LM| on sphere coefficients (metres): the float LM
+# stops at Eigen's sqrt(FLT_EPSILON) tolerances; measured <= 1.7e-6 (tests/test_pcl_lm.py)
+SPHERE_PCL_ATOL = 5e-6
+
+
 def _gpu(ctx, p, **kw):
     import torch
     t = [torch.from_numpy(np.ascontiguousarray(p[:, k])).cuda() for k in range(3)]
@@ -93,7 +99,9 @@ def _shell_distance(p, c):
 @pytest.mark.parametrize("n_s,n_o,seed", [(3000, 1500, 1), (800, 4000, 2), (20000, 5000, 3), (200, 50, 4)])
 def test_hip_sphere_matches_oracle(ctx, n_s, n_o, seed):
     p = sphere_scene(n_s, n_o, seed)
-    want = orc.sphere_segment(*p.T)
+    with orc.lm_mode(orc.LM_OPTIMUM):
+        want = orc.sphere_segment(*p.T)
+    pcl = orc.sphere_segment(*p.T)  # PCL's float Eigen LM (the reference's refinement)
     # RANSAC stage (optimize off): bit-exact
     raw = orc.sphere_segment(*p.T, orc.sphere_params(optimize=False))
     inl, coef, hyp = _gpu(ctx, p, optimize=False)
@@ -106,6 +114,11 @@ def test_hip_sphere_matches_oracle(ctx, n_s, n_o, seed):
     assert np.allclose(coef, want["coef"], rtol=2e-6, atol=1e-7)
     diff = np.setxor1d(inl, want["inliers"])
     assert np.all(_shell_distance(p[diff], want["coef"]) < 1e-5), diff
+    # against PCL's float LM: within its stopping envelope (tests/test_pcl_lm.py), final inliers
+    # equal but for points at the threshold shell
+    assert np.allclose(coef, pcl["coef"], rtol=0, atol=SPHERE_PCL_ATOL)
+    diff = np.setxor1d(inl, pcl["inliers"])
+    assert np.all(_shell_distance(p[diff], pcl["coef"]) < 2e-5), diff
 
 
 @pytest.mark.gpu
