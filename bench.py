@@ -179,6 +179,37 @@ def clutter_pass(pitt, ctx, dev, threads, frames_n=64, steps=3):
                                           "(group, hypothesis) pairs by certified box tests, so it executes fewer"}}
 
 
+def cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, steps, frames_per_batch):
+    """SURVEY A6's fast covariance mode (PITT_COV_FAST: tree-reduced double sums instead of PCL's
+    nine sequential float chains), reported beside the exact-order headline: frames/s over the same
+    pipelined steps, and on batch 0 the max |coefficient difference| and the final-inlier differences
+    against the exact mode.  Exact order stays the default and the parity path."""
+    import torch
+    fast = pitt.sac_params(cov_mode=pitt.COV_FAST)
+    for _ in range(3):
+        step(fast)
+    drain()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(fast)
+    drain()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    b = batches[0]
+    out_e = torch.empty(b.capacity, dtype=torch.int32, device=b.x.device)
+    out_f = torch.empty(b.capacity, dtype=torch.int32, device=b.x.device)
+    re = ctx.plane_segment_batch(b, params, out_e)
+    rf = ctx.plane_segment_batch(b, fast, out_f)
+    he, hf = out_e.cpu().numpy(), out_f.cpu().numpy()
+    xor = [len(np.setxor1d(he[o:o + a], hf[o:o + c])) for o, a, c in zip(b.offsets, re["n_inliers"], rf["n_inliers"])]
+    return {"frames_per_s": round(frames_per_batch * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
+            "max_abs_dcoef_vs_exact": float(np.max(np.abs(re["coefficients"] - rf["coefficients"]))),
+            "frames_coef_bit_equal": int(np.sum(np.all(re["coefficients"] == rf["coefficients"], axis=1))),
+            "frames_inliers_differ": int(np.count_nonzero(xor)), "max_inlier_xor": int(max(xor)),
+            "frames": int(len(re)), "note": "not the parity path: the headline value is exact order"}
+
+
 def pcie_pass(pitt, ctxs, host_batches, dev, params, steps):
     """Every step's batch starts in pinned host memory: H2D copy on the context's stream, then the
     batch; the copy of one batch overlaps the kernels of the others."""
@@ -247,12 +278,19 @@ def config2_pass(pitt, ctx, frame, reps=10):
 
 def config5_pass(pitt, ctx, threads, reps=5):
     """BASELINE config 5: find_supports (th 0.02f, 10 iterations) on the 1.2M-point fused scene, then
-    euclidean_clusters (0.03 m, 1 % / 99 %) on every support's on-support cloud; host arrays in and
-    out (the service boundary), GPU median of `reps` vs the oracle once, results compared."""
+    euclidean_clusters (0.03 m, 1 % / 99 %) on every support's on-support cloud
+    (obj_segmentation.cpp:261-312).  Timed through pitt_segment_objects_dev with the scene resident
+    in HBM (nothing read back but sizes, coefficients and sums), median of `reps` after 1 warm-up;
+    the host-array service path (H2D / D2H per call) is timed beside it.  Results vs the oracle once."""
+    import torch
     orc = oracle()
     x, y, z = pitt.synth_fused(1000, 4)
+    dx, dy, dz = (torch.from_numpy(a).cuda() for a in (x, y, z))
 
-    def gpu_once():
+    def dev_once():
+        return ctx.segment_objects_dev(dx, dy, dz, copy=False)
+
+    def host_once():
         sups = ctx.find_supports(x, y, z)
         cl = []
         for s in sups:
@@ -262,21 +300,32 @@ def config5_pass(pitt, ctx, threads, reps=5):
                                              max_size=int(np.floor(n * 0.99 + 0.5))) if n >= 30 else [])
         return sups, cl
 
-    gpu_once()
-    ts = []
-    for _ in range(reps):
-        t = time.perf_counter()
-        sups, cl = gpu_once()
-        ts.append((time.perf_counter() - t) * 1e3)
+    def median_ms(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            ts.append((time.perf_counter() - t) * 1e3)
+        return round(float(np.median(ts)), 2)
+
+    dev_ms = median_ms(dev_once)
+    host_ms = median_ms(host_once)
+    sups, objs = ctx.segment_objects_dev(dx, dy, dz)
     t = time.perf_counter()
     rs = orc.find_supports(x, y, z)
-    rcl = [orc.euclidean_clusters(*s["on_support_cloud"].T) for s in rs]
+    rcl = [(k, c) for k, s in enumerate(rs) if len(s["on_support_cloud"]) >= 30
+           for c in orc.euclidean_clusters(*s["on_support_cloud"].T)]
     cpu_ms = (time.perf_counter() - t) * 1e3
-    same = (len(rs) == len(sups) and all(np.array_equal(a.idx_map, b["idx_map"]) for a, b in zip(sups, rs)) and
-            all(len(a) == len(b) and all(np.array_equal(p.indices, q["inliers"]) for p, q in zip(a, b))
-                for a, b in zip(cl, rcl)))
-    return {"points": int(len(x)), "supports": len(sups), "clusters": int(sum(len(c) for c in cl)),
-            "gpu_ms_per_scene": round(float(np.median(ts)), 2), "gpu_statistic": f"median of {reps} after 1 warm-up",
+    same = (len(rs) == len(sups) and
+            all(np.array_equal(a["idx_map"].cpu().numpy(), b["idx_map"]) for a, b in zip(sups, rs)) and
+            len(objs) == len(rcl) and
+            all(k == kr and np.array_equal(i.cpu().numpy(), c["inliers"]) for (k, i, _), (kr, c) in zip(objs, rcl)))
+    return {"points": int(len(x)), "supports": len(sups), "clusters": len(objs),
+            "gpu_ms_per_scene": dev_ms, "gpu_statistic": f"median of {reps} after 1 warm-up",
+            "gpu_path": "pitt_segment_objects_dev (device-resident: scene in HBM, sizes/coefficients/sums back)",
+            "host_api_ms_per_scene": host_ms,
             "cpu_ms_per_scene": round(cpu_ms, 1), "cpu": "oracle, one thread, O(N) restatement of the loop",
             "matches_oracle": bool(same)}
 
@@ -369,12 +418,12 @@ def main():
             posted.append((i, gather.post(pending[i])))
         pending[i] = None
 
-    def step():
+    def step(prm=params):
         i = counter[0] % len(ctxs)
         counter[0] += 1
         if pending[i] is not None:
             finish(i)
-        pending[i] = ctxs[i].plane_segment_batch_async(batches[i], params, outs[i])
+        pending[i] = ctxs[i].plane_segment_batch_async(batches[i], prm, outs[i])
         if gather is not None:
             collect(1)
 
@@ -487,6 +536,8 @@ def main():
             "kernels": kernels,
         }
     if rank == 0 and world == 1 and not args.no_extras:
+        line["cov_fast"] = cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, args.steps, B)
+        log(f"[rank 0] cov_fast: {line['cov_fast']}")
         clutter_frames, line["clutter"] = clutter_pass(pitt, ctx, dev, threads)
         log(f"[rank 0] clutter: {line['clutter']}")
         host = [pitt.FrameBatch(b.x.cpu().pin_memory(), b.y.cpu().pin_memory(), b.z.cpu().pin_memory(), b.offsets,

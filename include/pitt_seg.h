@@ -65,6 +65,11 @@ enum {
 enum { PITT_REDUCE_SSE2 = 0, PITT_REDUCE_HADD = 1, PITT_REDUCE_SEQ = 2 };
 /* A9: Eigen 3.2 `v /= s` multiplies by 1/s (default); Eigen >= 3.3 divides. */
 enum { PITT_DIV_EIGEN32 = 0, PITT_DIV_TRUE = 1 };
+/* A6: optimizeModelCoefficients' covariance.  EXACT (default, the parity path): PCL's nine float
+ * accumulators summed sequentially in inlier order.  FAST: the nine sums in double, each (frame,
+ * 2048-point tile) summed by one wave and the tiles reduced in a fixed tree -- the whole chip on the
+ * batch instead of one serial chain per frame; coefficients within ~1e-6 of EXACT, not bit-equal. */
+enum { PITT_COV_EXACT = 0, PITT_COV_FAST = 1 };
 
 typedef struct pitt_ctx pitt_ctx;
 
@@ -79,6 +84,8 @@ typedef struct {
     int32_t  div_mode;        /* PITT_DIV_*                                                  */
     int32_t  sampler_slack;   /* sampler attempts beyond max_it+1 for rejected samples; at least  *
                                * 1000 are always provided (getSamples' consecutive-draw limit)  */
+    int32_t  cov_mode;        /* PITT_COV_* (A6); EXACT unless asked                          */
+    int32_t  pad;
 } pitt_sac_params;
 
 /* plane_segmentation_srv.cpp:19-21 defaults: th 0.007, 1000 iterations, seed 12345. */
@@ -120,6 +127,9 @@ int  pitt_create(pitt_ctx** out, int hip_device);
 void pitt_destroy(pitt_ctx* ctx);
 /* Run on a caller-owned hipStream_t (NULL = the context's own stream). */
 int  pitt_set_stream(pitt_ctx* ctx, void* hip_stream);
+/* Copy bytes between any host / device addresses on the context's stream (synchronous): for FFI
+ * callers without HIP bindings reading the device-resident outputs (pitt_*_dev). */
+int  pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes);
 void* pitt_get_stream(pitt_ctx* ctx);
 const char* pitt_last_error(pitt_ctx* ctx);
 int  pitt_abi_version(void);
@@ -189,6 +199,29 @@ typedef struct {
 int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                        const pitt_support_params* p, pitt_support_list* out);
 
+/* Device-resident form (the cloud a device preprocessing chain left in HBM: pitt_voxel_grid ->
+ * pitt_deep_filter -> pitt_transform_cloud, obj_segmentation.cpp:238-248): x/y/z device SoA; every
+ * output stays in the context's device arena (valid until the next call on the context). */
+typedef struct {
+    int32_t      n_points;          /* original cloud size                                       */
+    const int32_t* idx_map;         /* device, n_points ints (Support::inliers)                   */
+    float        coefficients[4];   /* host: support_coefficient_a..d (refined)                   */
+    int64_t      n_support;
+    const float* support_xyz;       /* device SoA planes: x at [0], y at [stride], z at [2 stride] */
+    int64_t      n_on_support;
+    const float* on_support_xyz;    /* device SoA planes, same stride                              */
+    int64_t      stride;            /* plane stride (floats) of support_xyz / on_support_xyz       */
+} pitt_support_dev;
+
+typedef struct {
+    int32_t                 n_supports;
+    const pitt_support_dev* supports;
+    int32_t                 iterations;
+} pitt_support_list_dev;
+
+int pitt_find_supports_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                           const pitt_support_params* p, pitt_support_list_dev* out);
+
 /* --- Euclidean clusters -------------------------------------------------------------------- */
 typedef struct {
     int64_t        size;
@@ -206,6 +239,58 @@ typedef struct {
 int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const float* y, const float* z,
                             int64_t n, double tolerance, int32_t min_size, int32_t max_size,
                             pitt_cluster_list* out);
+
+/* Device-resident form: x/y/z device SoA; each cluster's members (ascending) stay on the device at
+ * indices[offset, offset + size); the sums come back to the host. */
+typedef struct {
+    int64_t size;
+    int64_t offset;
+    float   sum_xyz[3];
+    float   pad;
+} pitt_cluster_dev;
+
+typedef struct {
+    int32_t                 n_clusters;
+    const pitt_cluster_dev* clusters;   /* size-descending (PCL order); valid until the next call */
+    const int32_t*          indices;    /* device */
+} pitt_cluster_list_dev;
+
+int pitt_euclidean_clusters_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list_dev* out);
+
+/* --- the support -> cluster glue on the device (obj_segmentation.cpp:261-312) ------------------ */
+/* clusterize's parameters (cluster_segmentation_srv.cpp:32-35, 45-54): tolerance 0.03, min rate 0.01,
+ * max rate 0.99, min input size 30 (Q6: read from the tolerance's parameter name -- its default). */
+typedef struct {
+    double  tolerance;
+    double  min_rate;
+    double  max_rate;
+    int32_t min_input_size;
+    int32_t pad;
+} pitt_cluster_params;
+void pitt_cluster_params_default(pitt_cluster_params* p);
+
+typedef struct {
+    int32_t support;      /* the support whose on-support cloud the cluster belongs to */
+    int32_t pad;
+    int64_t size;
+    int64_t offset;       /* members at pitt_scene.indices[offset, offset + size): on-support indices */
+    float   sum_xyz[3];   /* float sums in index order (the service's centroid = sum / (size + 1), Q7) */
+    float   pad2;
+} pitt_object;
+
+typedef struct {
+    pitt_support_list_dev supports;
+    int32_t               n_objects;   /* clusters of every support, support by support, PCL order */
+    const pitt_object*    objects;
+    const int32_t*        indices;     /* device */
+} pitt_scene;
+
+/* findSupports on the device cloud, then clusterize on every support's on-support cloud (supports with
+ * fewer than min_input_size points give no clusters; min / max cluster sizes round(n * rate)), with
+ * nothing leaving HBM but sizes, coefficients and sums.  Valid until the next call on the context. */
+int pitt_segment_objects_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                             const pitt_support_params* sp, const pitt_cluster_params* cp, pitt_scene* out);
 
 /* --- preprocessing in front of findSupports ------------------------------ */
 /* deepFiltering, src/segmentation_services/deep_filter_srv.cpp:27-44: points whose z is NaN are

@@ -5,7 +5,7 @@ Importing this package loads libpitt_seg.so (hand-written HIP kernels for gfx950
 loudly when the library is missing -- there is no CPU fallback.
 """
 from . import _lib
-from ._lib import (DIV_EIGEN32, DIV_TRUE, PITT_E_SAMPLER, PITT_NO_MODEL, PITT_OK, PITT_TILE_POINTS,
+from ._lib import (COV_EXACT, COV_FAST, DIV_EIGEN32, DIV_TRUE, PITT_E_SAMPLER, PITT_NO_MODEL, PITT_OK, PITT_TILE_POINTS,
                    REDUCE_HADD, REDUCE_SEQ, REDUCE_SSE2, SCENE_CLUTTER, SCENE_TABLE, SCENE_TABLE_NAN)
 from .api import (RESULT_DTYPE, ClusterResult, Context, FrameBatch, PittError, PlaneModel, Services,
                   SupportResult, float_threshold, padded_offsets, sac_params, sampler_table, support_params,
@@ -16,5 +16,5 @@ __all__ = [
     "RESULT_DTYPE", "sac_params", "support_params", "synth_frame", "synth_fused", "sampler_table",
     "float_threshold", "padded_offsets", "REDUCE_SSE2", "REDUCE_HADD", "REDUCE_SEQ", "DIV_EIGEN32",
     "DIV_TRUE", "SCENE_TABLE", "SCENE_CLUTTER", "SCENE_TABLE_NAN", "PITT_OK", "PITT_NO_MODEL",
-    "PITT_E_SAMPLER", "PITT_TILE_POINTS",
+    "PITT_E_SAMPLER", "PITT_TILE_POINTS", "COV_EXACT", "COV_FAST",
 ]

@@ -28,6 +28,7 @@ PITT_AXIS_CYLINDER, PITT_AXIS_CONE = 0, 1
 
 REDUCE_SSE2, REDUCE_HADD, REDUCE_SEQ = 0, 1, 2
 DIV_EIGEN32, DIV_TRUE = 0, 1
+COV_EXACT, COV_FAST = 0, 1
 SCENE_TABLE, SCENE_CLUTTER, SCENE_TABLE_NAN = 0, 1, 2
 
 
@@ -41,6 +42,8 @@ class SacParams(ctypes.Structure):
         ("reduce_order", ctypes.c_int32),
         ("div_mode", ctypes.c_int32),
         ("sampler_slack", ctypes.c_int32),
+        ("cov_mode", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
     ]
 
 
@@ -142,6 +145,48 @@ class ClusterList(ctypes.Structure):
     ]
 
 
+class SupportDev(ctypes.Structure):
+    """pitt_support_dev: device pointers (ints), host coefficients."""
+    _fields_ = [
+        ("n_points", ctypes.c_int32),
+        ("idx_map", ctypes.c_void_p),
+        ("coefficients", ctypes.c_float * 4),
+        ("n_support", ctypes.c_int64),
+        ("support_xyz", ctypes.c_void_p),
+        ("n_on_support", ctypes.c_int64),
+        ("on_support_xyz", ctypes.c_void_p),
+        ("stride", ctypes.c_int64),
+    ]
+
+
+class SupportListDev(ctypes.Structure):
+    _fields_ = [("n_supports", ctypes.c_int32), ("supports", ctypes.POINTER(SupportDev)), ("iterations", ctypes.c_int32)]
+
+
+class ClusterDev(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_int64), ("offset", ctypes.c_int64), ("sum_xyz", ctypes.c_float * 3),
+                ("pad", ctypes.c_float)]
+
+
+class ClusterListDev(ctypes.Structure):
+    _fields_ = [("n_clusters", ctypes.c_int32), ("clusters", ctypes.POINTER(ClusterDev)), ("indices", ctypes.c_void_p)]
+
+
+class ClusterParams(ctypes.Structure):
+    _fields_ = [("tolerance", ctypes.c_double), ("min_rate", ctypes.c_double), ("max_rate", ctypes.c_double),
+                ("min_input_size", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class SceneObject(ctypes.Structure):
+    _fields_ = [("support", ctypes.c_int32), ("pad", ctypes.c_int32), ("size", ctypes.c_int64),
+                ("offset", ctypes.c_int64), ("sum_xyz", ctypes.c_float * 3), ("pad2", ctypes.c_float)]
+
+
+class Scene(ctypes.Structure):
+    _fields_ = [("supports", SupportListDev), ("n_objects", ctypes.c_int32), ("objects", ctypes.POINTER(SceneObject)),
+                ("indices", ctypes.c_void_p)]
+
+
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
@@ -184,6 +229,14 @@ SIGNATURES = {
                                   ctypes.POINTER(SupportList)]),
     "pitt_euclidean_clusters": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.c_double, _i32, _i32,
                                        ctypes.POINTER(ClusterList)]),
+    "pitt_find_supports_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SupportParams),
+                                      ctypes.POINTER(SupportListDev)]),
+    "pitt_euclidean_clusters_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_double, _i32, _i32,
+                                           ctypes.POINTER(ClusterListDev)]),
+    "pitt_cluster_params_default": (None, [ctypes.POINTER(ClusterParams)]),
+    "pitt_memcpy": (_i32, [_vp, _vp, _vp, _i64]),
+    "pitt_segment_objects_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SupportParams),
+                                        ctypes.POINTER(ClusterParams), ctypes.POINTER(Scene)]),
     "pitt_synth_frame": (_i32, [_i32, ctypes.c_uint64, _i32, _i32, _f32p, _f32p, _f32p]),
     "pitt_synth_fused": (_i32, [ctypes.c_uint64, _i32, _i32, _i32, _f32p, _f32p, _f32p]),
     "pitt_sampler_table": (_i32, [_i64, ctypes.c_uint32, _i64, _i32p]),

@@ -35,7 +35,8 @@ class PittError(RuntimeError):
 
 def sac_params(threshold: float = 0.007, max_iterations: int = 1000, probability: float = 0.99,
                seed: int = 12345, optimize: bool = True, reduce_order: int = L.REDUCE_SSE2,
-               div_mode: int = L.DIV_EIGEN32, sampler_slack: int = 1000) -> L.SacParams:
+               div_mode: int = L.DIV_EIGEN32, sampler_slack: int = 1000,
+               cov_mode: int = 0) -> L.SacParams:
     """SACSegmentation parameters (defaults: plane_segmentation_srv.cpp:19-21)."""
     p = L.SacParams()
     lib.pitt_sac_params_default(ctypes.byref(p))
@@ -47,6 +48,7 @@ def sac_params(threshold: float = 0.007, max_iterations: int = 1000, probability
     p.reduce_order = reduce_order
     p.div_mode = div_mode
     p.sampler_slack = sampler_slack
+    p.cov_mode = cov_mode
     return p
 
 
@@ -471,6 +473,73 @@ class Context:
             idx = np.ctypeslib.as_array(c.indices, (c.size,)).copy() if c.size else np.zeros(0, np.int32)
             res.append(ClusterResult(idx, np.array(list(c.sum_xyz), np.float32)))
         return res
+
+    # ---- device-resident support / cluster path (pitt_*_dev) ---------------------------------
+    def _dev_copy(self, ptr, n: int, dtype, device):
+        """A fresh device tensor holding n elements copied from a device address of the arena."""
+        import torch
+        t = torch.empty(max(n, 1), dtype=dtype, device=device)
+        if n:
+            self._check(lib.pitt_memcpy(self.h, ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
+                                        n * t.element_size()), "pitt_memcpy")
+        return t[:n]
+
+    def _planes_copy(self, ptr, n: int, stride: int, device):
+        import torch
+        if n == 0:
+            return torch.zeros((0, 3), dtype=torch.float32, device=device)
+        return torch.stack([self._dev_copy(ptr + 4 * k * stride, n, torch.float32, device) for k in range(3)], 1)
+
+    def find_supports_dev(self, x, y, z, params: Optional[L.SupportParams] = None):
+        """pitt_find_supports_dev on device tensors: a list of dicts of device tensors (idx_map,
+        support_cloud, on_support_cloud as (m, 3)) and host coefficients."""
+        p = params or support_params()
+        out = L.SupportListDev()
+        self._check(lib.pitt_find_supports_dev(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), x.numel(),
+                                               ctypes.byref(p), ctypes.byref(out)), "pitt_find_supports_dev")
+        return [self._support_dev(out.supports[i], x.device) for i in range(out.n_supports)]
+
+    def _support_dev(self, s, device):
+        import torch
+        return {"idx_map": self._dev_copy(s.idx_map, s.n_points, torch.int32, device),
+                "coefficients": np.array(list(s.coefficients), np.float32),
+                "support_cloud": self._planes_copy(s.support_xyz, s.n_support, s.stride, device),
+                "on_support_cloud": self._planes_copy(s.on_support_xyz, s.n_on_support, s.stride, device)}
+
+    def euclidean_clusters_dev(self, x, y, z, tolerance: float = 0.03, min_size: int = 1, max_size: int = 2 ** 31 - 1):
+        """pitt_euclidean_clusters_dev on device tensors: [(device int32 members, host sums)]."""
+        import torch
+        out = L.ClusterListDev()
+        self._check(lib.pitt_euclidean_clusters_dev(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), x.numel(),
+                                                    tolerance, min_size, max_size, ctypes.byref(out)),
+                    "pitt_euclidean_clusters_dev")
+        total = sum(out.clusters[i].size for i in range(out.n_clusters))
+        idx = self._dev_copy(out.indices or 0, total, torch.int32, x.device)
+        return [(idx[out.clusters[i].offset:out.clusters[i].offset + out.clusters[i].size],
+                 np.array(list(out.clusters[i].sum_xyz), np.float32)) for i in range(out.n_clusters)]
+
+    def segment_objects_dev(self, x, y, z, support: Optional[L.SupportParams] = None,
+                            tolerance: float = 0.03, min_rate: float = 0.01, max_rate: float = 0.99,
+                            min_input_size: int = 30, copy: bool = True):
+        """pitt_segment_objects_dev (obj_segmentation.cpp:261-312 on the device): (supports, objects)
+        with objects = [(support index, device members, host sums)]; copy=False returns only the
+        sizes (what crosses the boundary when nothing is read back)."""
+        import torch
+        sp = support or support_params()
+        cp = L.ClusterParams(tolerance, min_rate, max_rate, min_input_size, 0)
+        out = L.Scene()
+        self._check(lib.pitt_segment_objects_dev(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), x.numel(),
+                                                 ctypes.byref(sp), ctypes.byref(cp), ctypes.byref(out)),
+                    "pitt_segment_objects_dev")
+        if not copy:
+            return ([out.supports.supports[i].n_on_support for i in range(out.supports.n_supports)],
+                    [out.objects[i].size for i in range(out.n_objects)])
+        sups = [self._support_dev(out.supports.supports[i], x.device) for i in range(out.supports.n_supports)]
+        total = sum(out.objects[i].size for i in range(out.n_objects))
+        idx = self._dev_copy(out.indices or 0, total, torch.int32, x.device)
+        objs = [(out.objects[i].support, idx[out.objects[i].offset:out.objects[i].offset + out.objects[i].size],
+                 np.array(list(out.objects[i].sum_xyz), np.float32)) for i in range(out.n_objects)]
+        return sups, objs
 
     # ---- profiling --------------------------------------------------------------------------
     def profile(self, on: bool = True) -> None:

@@ -53,46 +53,44 @@ __device__ __forceinline__ bool finite3(float x, float y, float z) {
 // one block combines them (k_minxyz_final).
 constexpr int kMinBlocks = 512;
 
+// The finite points' bounds: part[6 b + k] = min (k < 3) / max (k >= 3) of coordinate k % 3.
 __global__ __launch_bounds__(kBlock) void k_minxyz(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ z, int64_t n, float* __restrict__ part) {
-    __shared__ float s[3][kBlock / 64];
-    float a = INFINITY, b = INFINITY, c = INFINITY;
+    __shared__ float s[6][kBlock / 64];
+    float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
     for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         const float px = x[i], py = y[i], pz = z[i];
         if (finite3(px, py, pz)) {
-            a = fminf(a, px);
-            b = fminf(b, py);
-            c = fminf(c, pz);
+            v[0] = fminf(v[0], px);
+            v[1] = fminf(v[1], py);
+            v[2] = fminf(v[2], pz);
+            v[3] = fmaxf(v[3], px);
+            v[4] = fmaxf(v[4], py);
+            v[5] = fmaxf(v[5], pz);
         }
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        a = fminf(a, __shfl_xor(a, d, 64));
-        b = fminf(b, __shfl_xor(b, d, 64));
-        c = fminf(c, __shfl_xor(c, d, 64));
-    }
+    for (int d = 32; d >= 1; d >>= 1)
+        for (int k = 0; k < 6; ++k) v[k] = k < 3 ? fminf(v[k], __shfl_xor(v[k], d, 64)) : fmaxf(v[k], __shfl_xor(v[k], d, 64));
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { s[0][w] = a; s[1][w] = b; s[2][w] = c; }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 6; ++k) s[k][w] = v[k];
     __syncthreads();
-    if (threadIdx.x < 3) {
-        float m = s[threadIdx.x][0];
-        for (int i = 1; i < kBlock / 64; ++i) m = fminf(m, s[threadIdx.x][i]);
-        part[3 * blockIdx.x + threadIdx.x] = m;
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        float m = s[k][0];
+        for (int i = 1; i < kBlock / 64; ++i) m = k < 3 ? fminf(m, s[k][i]) : fmaxf(m, s[k][i]);
+        part[6 * blockIdx.x + k] = m;
     }
 }
 
 __global__ __launch_bounds__(64) void k_minxyz_final(const float* __restrict__ part, int nb, float* __restrict__ mn) {
-    float a = INFINITY, b = INFINITY, c = INFINITY;
-    for (int i = threadIdx.x; i < nb; i += 64) {
-        a = fminf(a, part[3 * i]);
-        b = fminf(b, part[3 * i + 1]);
-        c = fminf(c, part[3 * i + 2]);
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-        a = fminf(a, __shfl_xor(a, d, 64));
-        b = fminf(b, __shfl_xor(b, d, 64));
-        c = fminf(c, __shfl_xor(c, d, 64));
-    }
-    if (threadIdx.x == 0) { mn[0] = a; mn[1] = b; mn[2] = c; }
+    float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int i = threadIdx.x; i < nb; i += 64)
+        for (int k = 0; k < 6; ++k) v[k] = k < 3 ? fminf(v[k], part[6 * i + k]) : fmaxf(v[k], part[6 * i + k]);
+    for (int d = 32; d >= 1; d >>= 1)
+        for (int k = 0; k < 6; ++k) v[k] = k < 3 ? fminf(v[k], __shfl_xor(v[k], d, 64)) : fmaxf(v[k], __shfl_xor(v[k], d, 64));
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 6; ++k) mn[k] = v[k];
 }
 
 // ---- cell grid ---------------------------------------------------------------------------------
@@ -477,13 +475,26 @@ static int compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total)
     return PITT_OK;
 }
 
+// EuclideanClusterExtraction::extract (cluster_segmentation_srv.cpp:57-69).  x/y/z: host SoA, or
+// device SoA when dev_in.  Results: host member lists into `out`, or the context's device buffer
+// into `dout` (members at dout->indices[offset, offset + size)); the float sums come back to the host
+// either way.
 int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t n,
-                            double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list* out) {
+                            double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list* out,
+                            pitt_cluster_list_dev* dout, bool dev_in) {
     hipStream_t s = ctx->stream;
     ctx->keep_clusters.clear();
+    ctx->keep_clusters_dev.clear();
     ctx->keep_i32.clear();
-    out->n_clusters = 0;
-    out->clusters = nullptr;
+    if (out) {
+        out->n_clusters = 0;
+        out->clusters = nullptr;
+    }
+    if (dout) {
+        dout->n_clusters = 0;
+        dout->clusters = nullptr;
+        dout->indices = nullptr;
+    }
     if (n == 0) return PITT_OK;  // extract(): empty input => no clusters
     // KdTreeFLANN::radiusSearch: r^2 = (float)(radius * radius) with radius = (double)(float)tol
     const float tol_f = (float)tolerance;
@@ -521,33 +532,29 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     int32_t* CSTART = (int32_t*)ctx->buf("cl_cstart", (N + 1) * 4);
     if (!CSTART) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
     float *Y = X + N, *Z = X + 2 * N;
-    PITT_HIP_TRY(hipMemcpyAsync(X, hx, N * 4, hipMemcpyHostToDevice, s));
-    PITT_HIP_TRY(hipMemcpyAsync(Y, hy, N * 4, hipMemcpyHostToDevice, s));
-    PITT_HIP_TRY(hipMemcpyAsync(Z, hz, N * 4, hipMemcpyHostToDevice, s));
+    const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    PITT_HIP_TRY(hipMemcpyAsync(X, hx, N * 4, kin, s));
+    PITT_HIP_TRY(hipMemcpyAsync(Y, hy, N * 4, kin, s));
+    PITT_HIP_TRY(hipMemcpyAsync(Z, hz, N * 4, kin, s));
     PITT_HIP_TRY(hipMemsetAsync(KEYS, 0xFF, (size_t)hsize * 8, s));
     PITT_HIP_TRY(hipMemsetAsync(CELLS, 0, (N * 7 + 16) * 4, s));
     PITT_HIP_TRY(hipMemsetAsync(CMIN, 0x7F, N * 4, s));   // INT_MAX-ish: atomicMin seeds
     PITT_HIP_TRY(hipMemsetAsync(CSEED, 0x7F, N * 4, s));
     {
         const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMinBlocks));
-        float* PART = (float*)ctx->buf("cl_minpart", (size_t)kMinBlocks * 3 * sizeof(float));
+        float* PART = (float*)ctx->buf("cl_minpart", (size_t)kMinBlocks * 6 * sizeof(float));
         if (!PART) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
         hipLaunchKernelGGL(k_minxyz, dim3(nb), dim3(kBlock), 0, s, X, Y, Z, n, PART);
         hipLaunchKernelGGL(k_minxyz_final, dim3(1), dim3(64), 0, s, PART, nb, MN);
     }
-    // the grid's extent must fit the 21-bit cell coordinates (else distinct cells would alias)
+    // the grid's extent must fit the 21-bit cell coordinates (else distinct cells would alias); the
+    // bounds come from the device (k_minxyz), read back once
     {
-        float mxh[3] = {-INFINITY, -INFINITY, -INFINITY}, mnh[3];
-        for (int64_t i = 0; i < n; ++i) {
-            if (!(std::isfinite(hx[i]) && std::isfinite(hy[i]) && std::isfinite(hz[i]))) continue;
-            mxh[0] = std::max(mxh[0], hx[i]);
-            mxh[1] = std::max(mxh[1], hy[i]);
-            mxh[2] = std::max(mxh[2], hz[i]);
-        }
-        PITT_HIP_TRY(hipMemcpyAsync(mnh, MN, 12, hipMemcpyDeviceToHost, s));
+        float* mm = (float*)ctx->pinned("cl_minmax_h", 64);
+        PITT_HIP_TRY(hipMemcpyAsync(mm, MN, 24, hipMemcpyDeviceToHost, s));
         PITT_HIP_TRY(hipStreamSynchronize(s));
         for (int k = 0; k < 3; ++k)
-            if (std::isfinite(mnh[k]) && ((double)mxh[k] - (double)mnh[k]) / cell >= (double)kCellSpan)
+            if (std::isfinite(mm[k]) && ((double)mm[3 + k] - (double)mm[k]) / cell >= (double)kCellSpan)
                 return ctx->fail(PITT_E_INVALID, "cloud extent exceeds 2^21 cells of tolerance / sqrt(3)");
     }
     Grid g{X, Y, Z, MN, 1.0 / cell, KEYS, HCID, hsize - 1};
@@ -566,8 +573,14 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     if (K == 0) return PITT_OK;
     // PCL order: clusters discovered by ascending seed, then std::sort(rbegin, rend, size <).
     std::vector<int32_t> roots((size_t)K), sizes((size_t)K);
-    PITT_HIP_TRY(hipMemcpy(roots.data(), ROOTS, (size_t)K * 4, hipMemcpyDeviceToHost));
-    PITT_HIP_TRY(hipMemcpy(sizes.data(), RSIZES, (size_t)K * 4, hipMemcpyDeviceToHost));
+    {
+        int32_t* h = (int32_t*)ctx->pinned("cl_roots_h", (size_t)K * 8);
+        PITT_HIP_TRY(hipMemcpyAsync(h, ROOTS, (size_t)K * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipMemcpyAsync(h + K, RSIZES, (size_t)K * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        std::memcpy(roots.data(), h, (size_t)K * 4);
+        std::memcpy(sizes.data(), h + K, (size_t)K * 4);
+    }
     struct RS {
         int32_t root, size;
     };
@@ -611,10 +624,27 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     hipLaunchKernelGGL(k_members, dim3(ew(M)), dim3(256), 0, s, SK, M, X, Y, Z, MIDX, MXYZ, MXYZ + M, MXYZ + 2 * M);
     hipLaunchKernelGGL(k_sums, dim3((unsigned)K), dim3(256), 0, s, COFF, (int32_t)K, MXYZ, MXYZ + M, MXYZ + 2 * M, SUMS);
     PITT_HIP_TRY(hipGetLastError());
+    float* sums = (float*)ctx->pinned("cl_sums_h", (size_t)K * 12);
+    PITT_HIP_TRY(hipMemcpyAsync(sums, SUMS, (size_t)K * 12, hipMemcpyDeviceToHost, s));
+    if (dout) {  // members stay on the device
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        for (int64_t t = 0; t < K; ++t) {
+            pitt_cluster_dev c;
+            c.size = coff[(size_t)t + 1] - coff[(size_t)t];
+            c.offset = coff[(size_t)t];
+            c.sum_xyz[0] = sums[(size_t)t * 3];
+            c.sum_xyz[1] = sums[(size_t)t * 3 + 1];
+            c.sum_xyz[2] = sums[(size_t)t * 3 + 2];
+            c.pad = 0.0f;
+            ctx->keep_clusters_dev.push_back(c);
+        }
+        dout->n_clusters = (int32_t)K;
+        dout->clusters = ctx->keep_clusters_dev.data();
+        dout->indices = MIDX;
+        return PITT_OK;
+    }
     ctx->keep_i32.emplace_back((size_t)M);
-    std::vector<float> sums((size_t)K * 3);
     PITT_HIP_TRY(hipMemcpyAsync(ctx->keep_i32.back().data(), MIDX, (size_t)M * 4, hipMemcpyDeviceToHost, s));
-    PITT_HIP_TRY(hipMemcpyAsync(sums.data(), SUMS, (size_t)K * 12, hipMemcpyDeviceToHost, s));
     PITT_HIP_TRY(hipStreamSynchronize(s));
     const int32_t* base = ctx->keep_i32.back().data();
     for (int64_t t = 0; t < K; ++t) {
@@ -639,5 +669,96 @@ extern "C" int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const floa
     if (!out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, out);
+    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, out, nullptr, false);
+}
+
+extern "C" int pitt_euclidean_clusters_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                           double tolerance, int32_t min_size, int32_t max_size,
+                                           pitt_cluster_list_dev* out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, nullptr, out, true);
+}
+
+namespace pitt {
+int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t N,
+                       const pitt_support_params* sp, pitt_support_list* out, pitt_support_list_dev* dout,
+                       bool dev_in);
+
+__global__ void k_offset_indices(const int32_t* __restrict__ src, int64_t m, int32_t* __restrict__ dst) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        dst[k] = src[k];
+}
+}  // namespace pitt
+
+extern "C" void pitt_cluster_params_default(pitt_cluster_params* p) {
+    if (!p) return;
+    p->tolerance = 0.03;     // cluster_segmentation_srv.cpp:32
+    p->min_rate = 0.01;      // :33
+    p->max_rate = 0.99;      // :34
+    p->min_input_size = 30;  // :35 (Q6)
+    p->pad = 0;
+}
+
+// obj_segmentation.cpp:261-312: for each support (discovery order) clusterize its on-support cloud
+// (cluster_segmentation_srv.cpp:54: skipped below min_input_size; :60-61 the size limits rounded from
+// the rates), everything device-resident.  The supports' outputs live in the context arena under
+// their own names, so the cluster calls do not disturb them; each support's members are copied into
+// one scene buffer.
+extern "C" int pitt_segment_objects_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                        const pitt_support_params* sp, const pitt_cluster_params* cp,
+                                        pitt_scene* out) {
+    using namespace pitt;
+    if (!ctx) return PITT_E_INVALID;
+    if (!sp || !cp || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    out->n_objects = 0;
+    out->objects = nullptr;
+    out->indices = nullptr;
+    int rc = find_supports_impl(ctx, x, y, z, n, sp, nullptr, &out->supports, true);
+    if (rc) return rc;
+    const std::vector<pitt_support_dev> sups = ctx->keep_supports_dev;  // cluster calls clear the keep lists
+    std::vector<pitt_object> objs;
+    int64_t total = 0;
+    for (const pitt_support_dev& su : sups) total += su.n_on_support;
+    int32_t* IDX = (int32_t*)ctx->buf("scene_idx", (size_t)std::max<int64_t>(total, 1) * 4);
+    if (!IDX) return ctx->fail(PITT_E_NOMEM, "scene indices");
+    int64_t used = 0;
+    for (size_t k = 0; k < sups.size(); ++k) {
+        const pitt_support_dev& su = sups[k];
+        const int64_t m = su.n_on_support;
+        if (m < (int64_t)cp->min_input_size) continue;  // cluster_segmentation_srv.cpp:54
+        const int32_t mn = (int32_t)std::round((double)m * cp->min_rate);
+        const int32_t mx = (int32_t)std::round((double)m * cp->max_rate);
+        pitt_cluster_list_dev L;
+        rc = euclidean_clusters_impl(ctx, su.on_support_xyz, su.on_support_xyz + su.stride,
+                                     su.on_support_xyz + 2 * su.stride, m, cp->tolerance, mn, mx, nullptr, &L, true);
+        if (rc) return rc;
+        int64_t members = 0;
+        for (int c = 0; c < L.n_clusters; ++c) {
+            pitt_object o;
+            o.support = (int32_t)k;
+            o.pad = 0;
+            o.size = L.clusters[c].size;
+            o.offset = used + L.clusters[c].offset;
+            for (int j = 0; j < 3; ++j) o.sum_xyz[j] = L.clusters[c].sum_xyz[j];
+            o.pad2 = 0.0f;
+            objs.push_back(o);
+            members += o.size;
+        }
+        if (members > 0)
+            PITT_HIP_TRY(hipMemcpyAsync(IDX + used, L.indices, (size_t)members * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        used += members;
+    }
+    PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->keep_supports_dev = sups;
+    ctx->keep_objects = objs;
+    out->supports.supports = ctx->keep_supports_dev.data();
+    out->n_objects = (int32_t)ctx->keep_objects.size();
+    out->objects = ctx->keep_objects.data();
+    out->indices = IDX;
+    return PITT_OK;
 }

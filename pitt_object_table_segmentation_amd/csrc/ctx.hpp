@@ -1,5 +1,6 @@
 // ctx.hpp -- pitt_ctx: device, stream, scratch arena, sampler-table cache, kernel profiler.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -42,6 +43,12 @@ struct ProfTotal {
 
 }  // namespace pitt
 
+// A boolean knob from the environment ("0" / "1"), read when a context is created.
+inline bool pitt_env_flag(const char* name, bool dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? (v[0] != '0') : dflt;
+}
+
 struct pitt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -56,6 +63,9 @@ struct pitt_ctx {
     std::map<std::tuple<int64_t, uint32_t, int64_t, int>, std::vector<int32_t>> tables;
     // device pool of the last batch's tables
     std::vector<std::tuple<int64_t, uint32_t, int64_t>> pool_keys;
+
+    // first scoring chunk with lane-private counters (k_score LANE); $PITT_LANE_SCORE overrides
+    bool lane_score = pitt_env_flag("PITT_LANE_SCORE", false);
 
     // profiling
     bool prof = false;
@@ -87,7 +97,10 @@ struct pitt_ctx {
     std::vector<std::vector<int32_t>> keep_i32;
     std::vector<std::vector<float>> keep_f32;
     std::vector<pitt_support> keep_supports;
+    std::vector<pitt_support_dev> keep_supports_dev;
     std::vector<pitt_cluster> keep_clusters;
+    std::vector<pitt_cluster_dev> keep_clusters_dev;
+    std::vector<pitt_object> keep_objects;
 
     int fail(int code, const std::string& msg) {
         err = msg;

@@ -510,6 +510,112 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
     }
 }
 
+// First-chunk scoring with per-lane counters (H <= 32): the same box and certified cull as score_sub,
+// then every surviving (group, hypothesis) pair is scored with full-rate VALU only -- PCL's six
+// float ops, |d| - t (VOP3 abs modifier) and the sign bit added into lane-private counter cnt[h].
+// Exact: with denormals kept, fl(|d| - t) < 0 iff |d| < t (a nonzero difference never rounds to
+// zero; equality gives +0), and a NaN |d| (or t) gives a NaN with a clear sign bit.  The pairs are
+// dispatched by scalar bit tests on the cull mask (hypotheses with no surviving group in the
+// sub-step are skipped with one test), so no compaction, no SGPR count, no v_writelane; the
+// counters are reduced across the wave once per item.
+template <int ORDER>
+__device__ __forceinline__ void score_sub_lane(const float4* cl, int Hf, SubPts& P, int rem, float tv, int lane,
+                                               uint32_t (&cnt)[8], float& tb, float* __restrict__ gbox) {
+    if (__builtin_expect(rem < kSub, 0)) {
+#pragma unroll
+        for (int g = 0; g < kGPS; ++g)
+            if (g * kGrp + lane >= rem) P.x[g] = P.y[g] = P.z[g] = __builtin_nanf("");
+    }
+    RowBox B;
+    coord_box(P.x[0], P.x[1], P.x[2], P.x[3], B.lo[0], B.hi[0]);
+    coord_box(P.y[0], P.y[1], P.y[2], P.y[3], B.lo[1], B.hi[1]);
+    coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
+    row_reduce(B);
+    {
+        const int i = lane & 15;
+        float v = B.lo[0];
+        v = i == 1 ? B.lo[1] : v;
+        v = i == 2 ? B.lo[2] : v;
+        v = i == 3 ? B.hi[0] : v;
+        v = i == 4 ? B.hi[1] : v;
+        v = i == 5 ? B.hi[2] : v;
+        if (i < 6) gbox[(lane >> 4) * 8 + i] = v;
+        tb = i < 3 ? vmin(tb, v) : vmax(tb, v);
+    }
+    const RowGeo G = row_geo(B);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        if (kRnd * r >= Hf) break;
+        const int hl = kRnd * r + (lane & (kRnd - 1));
+        const float4 cr = cl[min(hl, Hf - 1)];
+        const int nb = min(kRnd, Hf - kRnd * r);
+        const uint64_t valid = (((uint64_t)1 << nb) - 1) * 0x0001000100010001ull;
+        const uint64_t need = __builtin_amdgcn_ballot_w64(!box_clear(G, cr, tv)) & valid;
+        // bit 16 g + h' of need: group g survives hypothesis 16 r + h'.  Word w holds groups 2 w, 2 w + 1.
+        const uint32_t w0 = (uint32_t)need, w1 = (uint32_t)(need >> 32);
+        const uint32_t hany = (w0 | (w0 >> 16) | w1 | (w1 >> 16)) & 0xFFFFu;
+        if (hany == 0) continue;
+        // coefficient rows read two hypotheses ahead (LDS broadcast), whether or not they are needed
+        float4 c0 = lds_row_v((uint32_t)(uintptr_t)(cl + kRnd * r));
+        float4 c1 = lds_row_v((uint32_t)(uintptr_t)(cl + kRnd * r + 1));
+#pragma unroll
+        for (int hh = 0; hh < kRnd; ++hh) {
+            const float4 c = c0;
+            c0 = c1;
+            if (hh + 2 < kRnd) c1 = lds_row_v((uint32_t)(uintptr_t)(cl + kRnd * r + hh + 2));
+            if (!((hany >> hh) & 1u)) continue;
+            const int h = kRnd * r + hh;
+#pragma unroll
+            for (int g = 0; g < kGPS; ++g) {
+                const uint32_t w = g < 2 ? w0 : w1;
+                if ((w >> (16 * (g & 1) + hh)) & 1u) {
+                    const float d = plane_dot<ORDER>(c, P.x[g], P.y[g], P.z[g]);
+                    float sd;
+                    asm("v_sub_f32_e64 %0, |%1|, %2" : "=v"(sd) : "v"(d), "v"(tv));
+                    // the sign bit into byte h % 4 of counter word h / 4 (<= 32 per lane and item)
+                    cnt[h >> 2] += (__float_as_uint(sd) >> 31) << (8 * (h & 3));
+                }
+            }
+        }
+    }
+}
+
+// The 32 lane-private counters reduced across the wave and stored: out[h] for h < Hf.  Folds with
+// permlane32 / permlane16 swaps (32 -> 16 -> 8 registers, each row of 16 lanes one hypothesis), a
+// row_ror all-reduce inside the rows, then lane 16 q + i (i < 8) stores hypothesis i + 8 q.
+__device__ __forceinline__ uint32_t u32_swap_add32(uint32_t a, uint32_t b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    return r[0] + r[1];
+}
+__device__ __forceinline__ uint32_t u32_swap_add16(uint32_t a, uint32_t b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    return r[0] + r[1];
+}
+__device__ __forceinline__ uint32_t row_allsum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);  // row_ror:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);  // row_ror:1
+    return v;
+}
+__device__ __forceinline__ void store_lane_counts(const uint32_t (&packed)[8], int Hf, int lane, int32_t* __restrict__ out) {
+    uint32_t cnt[32], c16[16], c8[8];
+#pragma unroll
+    for (int h = 0; h < 32; ++h) cnt[h] = (packed[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c16[j] = u32_swap_add32(cnt[j], cnt[j + 16]);  // lanes < 32: hyp j; else j + 16
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c8[j] = u32_swap_add16(c16[j], c16[j + 8]);     // row q: hyp j + 8 q
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c8[j] = row_allsum(c8[j]);
+    const int i = lane & 15, q = lane >> 4;
+    uint32_t v = c8[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) v = i == j ? c8[j] : v;
+    const int h = i + 8 * q;
+    if (i < 8 && h < Hf) out[h] = (int32_t)v;
+}
+
 // The item's coefficients into the wave's LDS row (rows past H repeat the last: never counted).
 template <int NST>
 __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__ hc, int H, int lane) {
@@ -524,7 +630,7 @@ __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__
 
 // BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
 // -- for k_refine's tile skipping.
-template <int ORDER, int NST, bool BOX>
+template <int ORDER, int NST, bool BOX, bool LANE = false>
 __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
@@ -560,6 +666,19 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     }
     const uint32_t gsrc = (uint32_t)(uintptr_t)wbox[w];
     float tb = (lane & 15) < 3 ? __builtin_inff() : -__builtin_inff();  // BOX: this lane's tile-box value
+    if constexpr (LANE) {  // the first chunk, H <= 32: lane-private counters (score_sub_lane)
+        uint32_t cnt[8];  // 32 lane-private counters, 8 bits each
+#pragma unroll
+        for (int h = 0; h < 8; ++h) cnt[h] = 0;
+        for (int s = 0; s < kSubs; s += 2) {
+            load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
+            score_sub_lane<ORDER>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, cnt, tb, gb + s * kGPS * 8);
+            if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
+            score_sub_lane<ORDER>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, cnt, tb, gb + (s + 1) * kGPS * 8);
+        }
+        store_lane_counts(cnt, Hf, lane, tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0);
+        (void)rounds;
+    } else {
     // sub-steps in pairs: the next sub-step loads into the other register set while this one is
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
@@ -581,6 +700,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
             out[h] = row[0] + row[16] + row[32] + row[48];
         }
     }
+    }  // !LANE
     if constexpr (BOX) {
         // rows -> tile: value i of the four rows combined (xor 16, xor 32)
 #pragma unroll
@@ -1055,18 +1175,10 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
     return s;
 }
 
-// The refined plane from the nine accumulators (Eigen 3.2 `accu /= n`, then eigen33, A6/A7/A9).
-template <int ORDER, int DIV>
-__device__ float4 refine_plane(float a9[9], int n) {
-    const float fn = (float)n;
-    if constexpr (DIV == 0) {  // Eigen 3.2: accu /= n  ==>  accu * (1/n)
-        const float r = 1.0f / fn;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) a9[k] = a9[k] * r;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) a9[k] = a9[k] / fn;
-    }
+// The refined plane from the nine normalised accumulators (accu / n): PCL's float covariance, eigen33
+// and d = -(e, 0) . (centroid, 1) (A6/A7).
+template <int ORDER>
+__device__ float4 refine_plane_mean(const float a9[9]) {
     float cov[9];
     cov[0] = a9[0] - a9[6] * a9[6];
     cov[1] = a9[1] - a9[6] * a9[7];
@@ -1081,6 +1193,21 @@ __device__ float4 refine_plane(float a9[9], int n) {
     eigen33(cov, e);
     const float d = -1.0f * red4<ORDER>(e[0] * a9[6], e[1] * a9[7], e[2] * a9[8], 0.0f * 1.0f);
     return make_float4(e[0], e[1], e[2], d);
+}
+
+// The refined plane from the nine accumulators (Eigen 3.2 `accu /= n`, then eigen33, A6/A7/A9).
+template <int ORDER, int DIV>
+__device__ float4 refine_plane(float a9[9], int n) {
+    const float fn = (float)n;
+    if constexpr (DIV == 0) {  // Eigen 3.2: accu /= n  ==>  accu * (1/n)
+        const float r = 1.0f / fn;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = a9[k] * r;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = a9[k] / fn;
+    }
+    return refine_plane_mean<ORDER>(a9);
 }
 
 template <int ORDER, int DIV>
@@ -1128,6 +1255,117 @@ __global__ __launch_bounds__(192) void k_refine(
 #pragma unroll
         for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
         if (lane == 0) final_coef[f] = refine_plane<ORDER, DIV>(a9, lds_acquire(&L.W));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// A6 fast mode (PITT_COV_FAST): the winning model's inlier covariance in double, tree-reduced over
+// the whole chip instead of nine serial float chains per frame.
+//   k_cov_tiles  one wave per (frame, tile) where the winning hypothesis counted inliers (exact, from
+//                the scoring counts; other tiles hold none): PCL's predicate |d| < t (ORDER), then per
+//                lane sequential double sums of x, y, z, xx, xy, xz, yy, yz, zz over its 32 points
+//                (float products are exact in double), a fixed xor-shuffle tree over the wave, and
+//                the tile's partial [f][t] (9 sums + count) stored;
+//   k_cov_final  one wave per refined frame: lane l sums tiles l, l + 64, ... in order, the same tree,
+//                then accu_k = (float)(S_k / n) into PCL's float covariance and eigen33.
+// Deterministic (fixed association); differs from PCL's sequential float sums by their rounding only.
+struct CovPart {
+    double s[9];  // x, y, z, xx, xy, xz, yy, yz, zz
+    int32_t n;
+    int32_t pad;
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_cov_tiles(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
+    float thf, const int32_t* __restrict__ tile_counts, int hstride, int n_frames, int tiles_max,
+    CovPart* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    const int f = it / tiles_max, t = it - f * tiles_max;
+    if (f >= n_frames) return;
+    const FrameState s = st[f];
+    const FrameMeta m = meta[f];
+    if (t >= m.tiles || !s.has_model || !s.need_refine) return;
+    CovPart* out = part + (int64_t)f * tiles_max + t;
+    double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int cnt = 0;
+    if (tile_counts[((int64_t)f * tiles_max + t) * hstride + s.best_h] > 0) {
+        const float4 c = best_coef[f];
+        float tv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+        const int rem = (int)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
+        const int64_t p0 = m.off + (int64_t)t * kTile + lane;
+#pragma unroll 4
+        for (int g = 0; g < kTile / 64; ++g) {
+            const float x = X[p0 + 64 * g], y = Y[p0 + 64 * g], z = Z[p0 + 64 * g];
+            if (64 * g + lane < rem && fabsf(plane_dot<ORDER>(c, x, y, z)) < tv) {
+                const double dx = x, dy = y, dz = z;
+                a[0] += dx;
+                a[1] += dy;
+                a[2] += dz;
+                a[3] += dx * dx;
+                a[4] += dx * dy;
+                a[5] += dx * dz;
+                a[6] += dy * dy;
+                a[7] += dy * dz;
+                a[8] += dz * dz;
+                ++cnt;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a[k] = wave_sum_d(a[k]);
+    cnt = wave_sum_i(cnt);
+    if (lane < 9) {
+        double v = a[0];
+#pragma unroll
+        for (int k = 1; k < 9; ++k) v = lane == k ? a[k] : v;
+        out->s[lane] = v;
+    }
+    if (lane == 0) out->n = cnt;
+}
+
+template <int ORDER>
+__global__ __launch_bounds__(64) void k_cov_final(const FrameMeta* __restrict__ meta,
+                                                  const FrameState* __restrict__ st, const CovPart* __restrict__ part,
+                                                  int n_frames, int tiles_max, float4* __restrict__ final_coef) {
+    const int f = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (f >= n_frames) return;
+    const FrameState s = st[f];
+    if (!s.has_model || !s.need_refine) return;
+    const int tiles = meta[f].tiles;
+    double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int cnt = 0;
+    for (int t = lane; t < tiles; t += 64) {
+        const CovPart& p = part[(int64_t)f * tiles_max + t];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a[k] += p.s[k];
+        cnt += p.n;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a[k] = wave_sum_d(a[k]);
+    cnt = wave_sum_i(cnt);
+    if (lane == 0 && cnt > 0) {
+        // accu order of computeMeanAndCovarianceMatrix: xx, xy, xz, yy, yz, zz, x, y, z
+        const double n = (double)cnt;
+        float a9[9] = {(float)(a[3] / n), (float)(a[4] / n), (float)(a[5] / n), (float)(a[6] / n),
+                       (float)(a[7] / n), (float)(a[8] / n), (float)(a[0] / n), (float)(a[1] / n),
+                       (float)(a[2] / n)};
+        final_coef[f] = refine_plane_mean<ORDER>(a9);
     }
 }
 
@@ -1395,7 +1633,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         rec = ctx->prof_begin("k_score", 0.0);
         if (c == 0) ctx->prof_alias(rec, "k_score.first");  // the first chunk: every frame, H hypotheses
         score_recs.push_back(rec);
-        auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
+        auto kern = c == 0 ? (H <= 32 && ctx->lane_score ? k_score<ORDER, 1, true, true>
+                              : H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
                            : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
         // the first chunk scores every frame (one item per wave); later ones stride over a capped grid
         const int64_t all_blocks = ((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves;
@@ -1416,12 +1655,24 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        p->optimize ? 1 : 0, best_coef, final_coef);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
-    rec = ctx->prof_begin("k_refine", 0.0);
-    acct_recs[kAcRefine] = rec;
-    hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(192), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                       thf, tile_counts, hstride, tiles_max, final_coef, acct);
-    ctx->prof_end(rec);
     const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
+    if (p->cov_mode == PITT_COV_FAST) {  // A6 fast mode: double sums over the chip, fixed tree
+        CovPart* part = as<CovPart>(ctx->buf("cov_part", (size_t)nf * tiles_max * sizeof(CovPart)));
+        if (!part) return ctx->fail(PITT_E_NOMEM, "covariance partials");
+        rec = ctx->prof_begin("k_cov_tiles", 0.0);
+        hipLaunchKernelGGL((k_cov_tiles<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
+                           best_coef, thf, tile_counts, hstride, nf, tiles_max, part);
+        ctx->prof_end(rec);
+        rec = ctx->prof_begin("k_cov_final", 0.0);
+        hipLaunchKernelGGL((k_cov_final<ORDER>), dim3(nf), dim3(64), 0, sm, meta, st, part, nf, tiles_max, final_coef);
+        ctx->prof_end(rec);
+    } else {
+        rec = ctx->prof_begin("k_refine", 0.0);
+        acct_recs[kAcRefine] = rec;
+        hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(192), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+                           thf, tile_counts, hstride, tiles_max, final_coef, acct);
+        ctx->prof_end(rec);
+    }
     rec = ctx->prof_begin("k_sel_mark", 0.0);
     acct_recs[kAcSelMark] = rec;
     hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,

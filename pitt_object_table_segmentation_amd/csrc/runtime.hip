@@ -151,6 +151,8 @@ void pitt_sac_params_default(pitt_sac_params* p) {
     p->reduce_order = PITT_REDUCE_SSE2;
     p->div_mode = PITT_DIV_EIGEN32;
     p->sampler_slack = 1000;     // >= getSamples' 1000-draw limit (sac_model.hpp)
+    p->cov_mode = PITT_COV_EXACT;
+    p->pad = 0;
 }
 
 int pitt_create(pitt_ctx** out, int hip_device) {
@@ -203,6 +205,16 @@ int pitt_set_stream(pitt_ctx* ctx, void* s) {
 }
 
 void* pitt_get_stream(pitt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    if (!ctx) return PITT_E_INVALID;
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (bytes == 0) return PITT_OK;
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    PITT_HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, ctx->stream));
+    PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PITT_OK;
+}
 
 const char* pitt_last_error(pitt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 

@@ -239,9 +239,9 @@ __global__ __launch_bounds__(kBlock) void k_bbox_tilemin(const float* __restrict
     }
 }
 
-// out[0..7]: xMax, xMin, yMax, yMin, zsum (tile partials in tile order), zabs, q, exact(1/0).  The
-// host turns zsum into zMed and certifies it (zmed_certified); only an uncertifiable sum pays the
-// reference's sequential double loop (k_zsum_seq).
+// out[0..7]: xMax, xMin, yMax, yMin, zsum (tile partials in tile order), zabs, q, exact(1/0).
+// k_bbox_final reduces the tiles; k_onsupport_bounds (below) turns them into the on-support filter's
+// bounds on the device, so the support loop needs no host round trip for them.
 __global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, double* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     float mx = -INFINITY, my = -INFINITY, cx = INFINITY, cy = INFINITY;
@@ -261,47 +261,72 @@ __global__ void k_bbox_final(const BBoxTile* __restrict__ tiles, int64_t nt, dou
     out[4] = zs; out[5] = za; out[6] = q; out[7] = exact ? 1.0 : 0.0;
 }
 
-// supports_segmentation_srv.cpp:207,217: the reference's sequential double sum of z.
+// supports_segmentation_srv.cpp:207,217: the reference's sequential double sum of z -- only when
+// the parallel sum could not be certified (flag out[8] == 0 after k_onsupport_bounds), else a no-op.
 __global__ void k_zsum_seq(const float* __restrict__ z, int64_t n, double* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (out[8] != 0.0) return;
     double zs = 0.0;
     for (int64_t i = 0; i < n; ++i) zs += (double)z[i];
-    *out = zs;
+    out[4] = zs;
+    out[8] = 2.0;  // sequential
 }
 
 // zMed = zsum / n + off computed from a sum in another association: the sequential sum differs by
 // at most 2 (n - 1) u sum|z| (u = 2^-53, both sums' error bounds), the division and the addition
 // add a few ulps.  If no float lies within that bound of zMed, every `(double)z > zMed` test of
 // the on-support filter decides the same way for the sequential value: returns true and zMed.
-static bool zmed_certified(double zsum, double zabs, int64_t n, double off, double* zmed) {
-    const double u = std::ldexp(1.0, -53);
+__host__ __device__ inline bool zmed_certified(double zsum, double zabs, int64_t n, double off, double* zmed) {
+    const double u = 1.1102230246251565e-16;  // 2^-53
     const double m = zsum / (double)n + off;
     const double b = 2.0000001 * (double)(n - 1) * u * zabs / (double)n * (1.0 + 4.0 * u) +
-                     8.0 * u * (std::fabs(zsum) / (double)n + std::fabs(off) + std::fabs(m)) + 1e-300;
+                     8.0 * u * (fabs(zsum) / (double)n + fabs(off) + fabs(m)) + 1e-300;
     const double lo = m - b, hi = m + b;
-    if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
+    if (!isfinite(lo) || !isfinite(hi)) return false;
     float f = (float)hi;                    // the largest float <= hi
-    if ((double)f > hi) f = std::nextafter(f, -INFINITY);
+    if ((double)f > hi) f = nextafterf(f, -INFINITY);
     if ((double)f >= lo) return false;      // a float inside [lo, hi]: the sums' rounding could matter
     *zmed = m;
     return true;
 }
 
-struct OnSupport {
+// getPointOnPlane's bounds (supports_segmentation_srv.cpp:184-217) from k_bbox_final's reduction:
+// bb[0..3] -> x/y max and min shrunk by the edge offsets, bb[9] = zMed.  bb[8]: 1 when the parallel
+// z sum was exact or certified, 0 when the sequential sum must decide (k_zsum_seq, then
+// k_onsupport_zmed).
+__global__ void k_onsupport_bounds(double* __restrict__ bb, int64_t n, float ox, float oy, float oz) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double zmed = 0.0;
+    bool ok = true;
+    if (bb[7] != 0.0) zmed = bb[4] / (double)n + (double)oz;  // every partial sum exact
+    else ok = zmed_certified(bb[4], bb[5], n, (double)oz, &zmed);
+    bb[0] -= (double)ox;  // xMax
+    bb[1] += (double)ox;  // xMin
+    bb[2] -= (double)oy;  // yMax
+    bb[3] += (double)oy;  // yMin
+    bb[8] = ok ? 1.0 : 0.0;
+    bb[9] = zmed;
+}
+__global__ void k_onsupport_zmed(double* __restrict__ bb, int64_t n, float oz) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (bb[8] == 2.0) bb[9] = bb[4] / (double)n + (double)oz;
+}
+
+struct OnSupport {  // bounds read from the device (k_onsupport_bounds): bb[0] xMax, [1] xMin, [2] yMax, [3] yMin, [9] zMed
     const float *x, *y, *z;
     const int32_t* map;
     int level;
-    double xMin, xMax, yMin, yMax, zMed;
+    const double* bb;
     __device__ bool operator()(int64_t i) const {
         if (map[i] == level) return false;
         const double px = x[i], py = y[i], pz = z[i];
-        return px > xMin && px < xMax && pz > zMed && py > yMin && py < yMax;
+        return px > bb[1] && px < bb[0] && pz > bb[9] && py > bb[3] && py < bb[2];
     }
 };
 
 // ---- host helpers -------------------------------------------------------------------------------
 template <class Pred, class Act>
-static int run_compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total) {
+static int run_compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total, int32_t* total_dev = nullptr) {
     const int64_t nt = ctiles(n);
     int32_t* counts = (int32_t*)ctx->buf("cmp_counts", (size_t)std::max<int64_t>(nt, 1) * 4);
     int32_t* offs = (int32_t*)ctx->buf("cmp_offs", (size_t)(nt + 1) * 4);
@@ -316,6 +341,7 @@ static int run_compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* to
                            offs);
     }
     PITT_HIP_TRY(hipGetLastError());
+    if (total_dev) PITT_HIP_TRY(hipMemcpyAsync(total_dev, offs + nt, 4, hipMemcpyDeviceToDevice, s));
     if (total) {
         int32_t* h = (int32_t*)ctx->pinned("cmp_total", 16);
         PITT_HIP_TRY(hipMemcpyAsync(h, offs + nt, 4, hipMemcpyDeviceToHost, s));
@@ -358,21 +384,33 @@ static bool is_horizontal(const float c[4], const float axis[3], float var_th) {
     return (cx > lo && cx < hi) && (cy > lo && cy < hi) && (cz > lo && cz < hi);
 }
 
+// The support loop (findSupports, :241-361).  x/y/z: host SoA, or device SoA when dev_in.  Results:
+// host copies into `out` (pitt_find_supports), or device buffers of the context into `dout`
+// (pitt_find_supports_dev: nothing leaves HBM).  Host round trips per iteration: one -- the RANSAC
+// results the stop tests and the horizontality test read (:270-300); the removal, the index map,
+// the on-support bounds (k_onsupport_bounds) and the on-support compaction are stream-ordered.
 int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t N,
-                       const pitt_support_params* sp, pitt_support_list* out) {
+                       const pitt_support_params* sp, pitt_support_list* out, pitt_support_list_dev* dout,
+                       bool dev_in) {
     hipStream_t s = ctx->stream;
     ctx->keep_i32.clear();
     ctx->keep_f32.clear();
     ctx->keep_supports.clear();
-    out->n_supports = 0;
-    out->supports = nullptr;
-    out->iterations = 0;
+    ctx->keep_supports_dev.clear();
+    if (out) {
+        out->n_supports = 0;
+        out->supports = nullptr;
+        out->iterations = 0;
+    }
+    if (dout) {
+        dout->n_supports = 0;
+        dout->supports = nullptr;
+        dout->iterations = 0;
+    }
     const int64_t cap = std::max<int64_t>(kCTile, (N + kCTile - 1) / kCTile * kCTile);
-    auto plane3 = [&](const char* name) { return (float*)ctx->buf(name, (size_t)cap * 3 * sizeof(float)); };
+    auto plane3 = [&](const std::string& name) { return (float*)ctx->buf(name, (size_t)cap * 3 * sizeof(float)); };
     float* O = plane3("sup_orig");
     float* IT[2] = {plane3("sup_it0"), plane3("sup_it1")};
-    float* S = plane3("sup_s");
-    float* ON = plane3("sup_on");
     int32_t* INL = (int32_t*)ctx->buf("sup_inl", (size_t)cap * 4);
     int32_t* MAP[2] = {(int32_t*)ctx->buf("sup_map0", (size_t)cap * 4), (int32_t*)ctx->buf("sup_map1", (size_t)cap * 4)};
     const int64_t words = (cap + 31) / 32;
@@ -380,13 +418,18 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
     const int64_t ntmax = ctiles(cap);
     BBoxTile* BT = (BBoxTile*)ctx->buf("sup_bbox", (size_t)ntmax * sizeof(BBoxTile));
     float* PRE = (float*)ctx->buf("sup_pre", (size_t)ntmax * 2 * sizeof(float));
-    double* BB = (double*)ctx->buf("sup_bbout", 8 * sizeof(double));
-    if (!O || !IT[0] || !IT[1] || !S || !ON || !INL || !MAP[0] || !MAP[1] || !MEM || !BT || !PRE || !BB)
+    // per support (at most one per iteration; an iteration removes >= min_iterative_plane_percentage of N):
+    // bounds, on-support count
+    const int kMaxSup = 256;
+    double* BB = (double*)ctx->buf("sup_bbout", (size_t)kMaxSup * 16 * sizeof(double));
+    int32_t* NON = (int32_t*)ctx->buf("sup_non", (size_t)kMaxSup * 4);
+    if (!O || !IT[0] || !IT[1] || !INL || !MAP[0] || !MAP[1] || !MEM || !BT || !PRE || !BB || !NON)
         return ctx->fail(PITT_E_NOMEM, "support scratch");
-    // upload the original cloud (host SoA) -- iterativeCloud starts as its copy
-    PITT_HIP_TRY(hipMemcpyAsync(O, hx, (size_t)N * 4, hipMemcpyHostToDevice, s));
-    PITT_HIP_TRY(hipMemcpyAsync(O + cap, hy, (size_t)N * 4, hipMemcpyHostToDevice, s));
-    PITT_HIP_TRY(hipMemcpyAsync(O + 2 * cap, hz, (size_t)N * 4, hipMemcpyHostToDevice, s));
+    // the original cloud -- iterativeCloud starts as its copy
+    const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    PITT_HIP_TRY(hipMemcpyAsync(O, hx, (size_t)N * 4, kin, s));
+    PITT_HIP_TRY(hipMemcpyAsync(O + cap, hy, (size_t)N * 4, kin, s));
+    PITT_HIP_TRY(hipMemcpyAsync(O + 2 * cap, hz, (size_t)N * 4, kin, s));
     PITT_HIP_TRY(hipMemcpyAsync(IT[0], O, (size_t)cap * 3 * 4, hipMemcpyDeviceToDevice, s));
 
     pitt_sac_params p;
@@ -396,15 +439,16 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
     p.reduce_order = sp->reduce_order;
     p.div_mode = sp->div_mode;
 
-    struct Staged {
-        std::vector<int32_t> map;
-        std::vector<float> sup, on;
+    struct Found {
+        int32_t* map;
+        float *sup, *on;
+        int64_t n_sup;
         float coef[4];
     };
-    std::vector<Staged> staged;
+    std::vector<Found> found;
     int cur = 0, mcur = 0;
     int64_t Nk = N;
-    int level = -2, cnt = 0;
+    int level = -2, cnt = 0, iterations = 0;
     const float Nf = (float)N;
     while (true) {
         pitt_frames fr;
@@ -417,78 +461,64 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
         fr.n_frames = 1;
         fr.capacity = cap;
         pitt_plane_result r;
-        int rc = pitt_plane_segment_batch(ctx, &fr, &p, &r, INL);
+        int rc = pitt_plane_segment_batch(ctx, &fr, &p, &r, INL);  // the loop's one host round trip
         if (rc < 0) return rc;
         if (r.status < 0) return ctx->fail(r.status, "RANSAC inside the support loop failed");
-        out->iterations++;
+        ++iterations;
         const int64_t n_inl = r.n_coeff ? r.n_inliers : 0;
         if (n_inl == 0) break;                                                   // :270
         if ((float)Nk < Nf * sp->min_iterative_cloud_percentage) break;          // :274 (Q9)
         if ((float)n_inl < Nf * sp->min_iterative_plane_percentage) break;       // :278
+        const bool horizontal = is_horizontal(r.coefficients, sp->horizontal_axis, sp->horizontal_variance_threshold);
+        if (horizontal && (int)found.size() >= kMaxSup) return ctx->fail(PITT_E_INVALID, "more than 256 supports");
+        const int k = (int)found.size();
+        // the support cloud goes straight into its own buffer when the plane is a support
+        float* S = horizontal ? plane3("sup_s" + std::to_string(k)) : plane3("sup_s");
+        if (!S) return ctx->fail(PITT_E_NOMEM, "support scratch");
         // membership bitmask of the inliers (indices into the current iterative cloud)
         PITT_HIP_TRY(hipMemsetAsync(MEM, 0, (size_t)words * 4 + 16, s));
         hipLaunchKernelGGL(k_mark, dim3(ew_grid(n_inl)), dim3(256), 0, s, INL, n_inl, Nk, MEM,
                            (int32_t*)(MEM + words));
-        // removePlaneInliner: support = it[inl] ; it <- it \ inl
+        // removePlaneInliner: support = it[inl] ; it <- it \ inl (inliers unique: |it \ inl| = Nk - n_inl)
         hipLaunchKernelGGL(k_gather, dim3(ew_grid(n_inl)), dim3(256), 0, s, IT[cur], IT[cur] + cap, IT[cur] + 2 * cap,
                            INL, n_inl, S, S + cap, S + 2 * cap);
-        int64_t Nn = 0;
         rc = run_compact(ctx, Nk, NotMember{MEM},
                          CopyXYZ{IT[cur], IT[cur] + cap, IT[cur] + 2 * cap, IT[cur ^ 1], IT[cur ^ 1] + cap,
                                  IT[cur ^ 1] + 2 * cap},
-                         &Nn);
+                         nullptr);
         if (rc) return rc;
+        const int64_t Nn = Nk - n_inl;
         // index map w.r.t. the original cloud
         if (!cnt) hipLaunchKernelGGL(k_iota, dim3(ew_grid(N)), dim3(256), 0, s, MAP[mcur], N);
-        const bool horizontal = is_horizontal(r.coefficients, sp->horizontal_axis, sp->horizontal_variance_threshold);
         const int lv = horizontal ? level : -1;
         hipLaunchKernelGGL(k_map_tags, dim3(ew_grid(N)), dim3(256), 0, s, MAP[mcur], N, MEM, Nk, lv, MAP[mcur ^ 1]);
         rc = run_compact(ctx, N, MapRest{MAP[mcur], MEM, Nk, lv}, MapRank{MAP[mcur ^ 1]}, nullptr);
         if (rc) return rc;
         if (horizontal) {
-            Staged st;
+            Found fd;
+            fd.map = (int32_t*)ctx->buf("sup_m" + std::to_string(k), (size_t)cap * 4);
+            fd.on = plane3("sup_on" + std::to_string(k));
+            if (!fd.map || !fd.on) return ctx->fail(PITT_E_NOMEM, "support outputs");
+            fd.sup = S;
+            fd.n_sup = n_inl;
+            std::memcpy(fd.coef, r.coefficients, sizeof fd.coef);
+            PITT_HIP_TRY(hipMemcpyAsync(fd.map, MAP[mcur ^ 1], (size_t)N * 4, hipMemcpyDeviceToDevice, s));
+            double* bb = BB + 16 * k;
             const int64_t nt = ctiles(n_inl);
             hipLaunchKernelGGL(k_bbox_tilemax, dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, S, S + cap, n_inl, BT);
             hipLaunchKernelGGL(k_bbox_tilescan, dim3(1), dim3(64), 0, s, BT, nt, PRE);
             hipLaunchKernelGGL(k_bbox_tilemin, dim3(grid_for_tiles(nt)), dim3(kBlock), 0, s, S, S + cap, S + 2 * cap,
                                n_inl, PRE, BT);
-            hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, BT, nt, BB);
-            double* hb = (double*)ctx->pinned("sup_bb_h", 8 * sizeof(double));
-            PITT_HIP_TRY(hipMemcpyAsync(hb, BB, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
-            PITT_HIP_TRY(hipStreamSynchronize(s));
-            double xMax = hb[0], xMin = hb[1], yMax = hb[2], yMin = hb[3], zMed = 0.0;
-            xMax -= sp->edge_remove_offset[0];
-            xMin += sp->edge_remove_offset[0];
-            yMax -= sp->edge_remove_offset[1];
-            yMin += sp->edge_remove_offset[1];
-            const double off_z = sp->edge_remove_offset[2];
-            if (hb[7] != 0.0) {  // every partial sum exact: any association gives the sequential value
-                zMed = hb[4] / (double)n_inl + off_z;
-            } else if (!zmed_certified(hb[4], hb[5], n_inl, off_z, &zMed)) {
-                hipLaunchKernelGGL(k_zsum_seq, dim3(1), dim3(64), 0, s, S + 2 * cap, n_inl, BB + 4);
-                PITT_HIP_TRY(hipMemcpyAsync(hb, BB, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
-                PITT_HIP_TRY(hipStreamSynchronize(s));
-                zMed = hb[4] / (double)n_inl + off_z;
-                ++ctx->zsum_sequential;
-            }
-            int64_t n_on = 0;
-            rc = run_compact(ctx, N,
-                             OnSupport{O, O + cap, O + 2 * cap, MAP[mcur ^ 1], lv, xMin, xMax, yMin, yMax, zMed},
-                             CopyXYZ{O, O + cap, O + 2 * cap, ON, ON + cap, ON + 2 * cap}, &n_on);
+            hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, BT, nt, bb);
+            hipLaunchKernelGGL(k_onsupport_bounds, dim3(1), dim3(64), 0, s, bb, n_inl, sp->edge_remove_offset[0],
+                               sp->edge_remove_offset[1], sp->edge_remove_offset[2]);
+            // only an uncertifiable parallel z sum pays the reference's sequential loop (a no-op otherwise)
+            hipLaunchKernelGGL(k_zsum_seq, dim3(1), dim3(64), 0, s, S + 2 * cap, n_inl, bb);
+            hipLaunchKernelGGL(k_onsupport_zmed, dim3(1), dim3(64), 0, s, bb, n_inl, sp->edge_remove_offset[2]);
+            rc = run_compact(ctx, N, OnSupport{O, O + cap, O + 2 * cap, MAP[mcur ^ 1], lv, bb},
+                             CopyXYZ{O, O + cap, O + 2 * cap, fd.on, fd.on + cap, fd.on + 2 * cap}, nullptr, NON + k);
             if (rc) return rc;
-            st.map.resize((size_t)N);
-            st.sup.resize((size_t)n_inl * 3);
-            st.on.resize((size_t)n_on * 3);
-            PITT_HIP_TRY(hipMemcpyAsync(st.map.data(), MAP[mcur ^ 1], (size_t)N * 4, hipMemcpyDeviceToHost, s));
-            for (int c = 0; c < 3; ++c) {
-                PITT_HIP_TRY(hipMemcpyAsync(st.sup.data() + c * n_inl, S + c * cap, (size_t)n_inl * 4,
-                                            hipMemcpyDeviceToHost, s));
-                PITT_HIP_TRY(hipMemcpyAsync(st.on.data() + c * n_on, ON + c * cap, (size_t)n_on * 4,
-                                            hipMemcpyDeviceToHost, s));
-            }
-            PITT_HIP_TRY(hipStreamSynchronize(s));
-            std::memcpy(st.coef, r.coefficients, sizeof st.coef);
-            staged.push_back(std::move(st));
+            found.push_back(fd);
         }
         mcur ^= 1;
         cur ^= 1;
@@ -496,22 +526,70 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
         ++cnt;
         --level;
     }
-    for (Staged& st : staged) {
-        ctx->keep_i32.push_back(std::move(st.map));
-        ctx->keep_f32.push_back(std::move(st.sup));
-        ctx->keep_f32.push_back(std::move(st.on));
+    // sizes of the on-support clouds and the z-sum path taken, in one round trip
+    const int nsup = (int)found.size();
+    std::vector<int64_t> n_on((size_t)nsup, 0);
+    if (nsup > 0) {
+        int32_t* h = (int32_t*)ctx->pinned("sup_non_h", (size_t)kMaxSup * 4);
+        double* hb = (double*)ctx->pinned("sup_bb_h", (size_t)kMaxSup * 16 * sizeof(double));
+        PITT_HIP_TRY(hipMemcpyAsync(h, NON, (size_t)nsup * 4, hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipMemcpyAsync(hb, BB, (size_t)nsup * 16 * sizeof(double), hipMemcpyDeviceToHost, s));
+        PITT_HIP_TRY(hipStreamSynchronize(s));
+        for (int k = 0; k < nsup; ++k) {
+            n_on[(size_t)k] = h[k];
+            if (hb[16 * k + 8] == 2.0) ++ctx->zsum_sequential;
+        }
+    }
+    if (dout) {
+        for (int k = 0; k < nsup; ++k) {
+            const Found& fd = found[(size_t)k];
+            pitt_support_dev su;
+            su.n_points = (int32_t)N;
+            su.idx_map = fd.map;
+            std::memcpy(su.coefficients, fd.coef, sizeof su.coefficients);
+            su.n_support = fd.n_sup;
+            su.support_xyz = fd.sup;
+            su.n_on_support = n_on[(size_t)k];
+            su.on_support_xyz = fd.on;
+            su.stride = cap;
+            ctx->keep_supports_dev.push_back(su);
+        }
+        dout->n_supports = nsup;
+        dout->supports = ctx->keep_supports_dev.data();
+        dout->iterations = iterations;
+        return PITT_OK;
+    }
+    // host results: one copy per output at the end
+    for (int k = 0; k < nsup; ++k) {
+        const Found& fd = found[(size_t)k];
+        const int64_t ns = fd.n_sup, no = n_on[(size_t)k];
+        ctx->keep_i32.emplace_back((size_t)N);
+        ctx->keep_f32.emplace_back((size_t)ns * 3);
+        ctx->keep_f32.emplace_back((size_t)no * 3);
+        std::vector<float>& sup = ctx->keep_f32[ctx->keep_f32.size() - 2];
+        std::vector<float>& on = ctx->keep_f32.back();
+        PITT_HIP_TRY(hipMemcpyAsync(ctx->keep_i32.back().data(), fd.map, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+        for (int c = 0; c < 3; ++c) {
+            if (ns) PITT_HIP_TRY(hipMemcpyAsync(sup.data() + c * ns, fd.sup + c * cap, (size_t)ns * 4, hipMemcpyDeviceToHost, s));
+            if (no) PITT_HIP_TRY(hipMemcpyAsync(on.data() + c * no, fd.on + c * cap, (size_t)no * 4, hipMemcpyDeviceToHost, s));
+        }
+    }
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < nsup; ++k) {
+        const Found& fd = found[(size_t)k];
         pitt_support su;
         su.n_points = (int32_t)N;
-        su.idx_map = ctx->keep_i32.back().data();
-        std::memcpy(su.coefficients, st.coef, sizeof su.coefficients);
-        su.support_xyz = ctx->keep_f32[ctx->keep_f32.size() - 2].data();
-        su.n_support = (int64_t)ctx->keep_f32[ctx->keep_f32.size() - 2].size() / 3;
-        su.on_support_xyz = ctx->keep_f32.back().data();
-        su.n_on_support = (int64_t)ctx->keep_f32.back().size() / 3;
+        su.idx_map = ctx->keep_i32[(size_t)k].data();
+        std::memcpy(su.coefficients, fd.coef, sizeof su.coefficients);
+        su.support_xyz = ctx->keep_f32[(size_t)(2 * k)].data();
+        su.n_support = fd.n_sup;
+        su.on_support_xyz = ctx->keep_f32[(size_t)(2 * k + 1)].data();
+        su.n_on_support = n_on[(size_t)k];
         ctx->keep_supports.push_back(su);
     }
-    out->n_supports = (int32_t)ctx->keep_supports.size();
+    out->n_supports = nsup;
     out->supports = ctx->keep_supports.data();
+    out->iterations = iterations;
     return PITT_OK;
 }
 
@@ -553,7 +631,16 @@ int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const floa
     if (!p || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::find_supports_impl(ctx, x, y, z, n, p, out);
+    return pitt::find_supports_impl(ctx, x, y, z, n, p, out, nullptr, false);
+}
+
+int pitt_find_supports_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                           const pitt_support_params* p, pitt_support_list_dev* out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!p || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::find_supports_impl(ctx, x, y, z, n, p, nullptr, out, true);
 }
 
 }  // extern "C"

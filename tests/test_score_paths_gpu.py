@@ -1,0 +1,45 @@
+"""The first scoring chunk has two implementations: the survivor-list scorer
+(compaction, v_cmp -> s_bcnt1 -> v_writelane per surviving (group, hypothesis) pair) and the
+lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only, |d| - t sign bits
+added into lane-private counters).  $PITT_LANE_SCORE picks one when a context is created; the other
+is run here on the bit-exact parity tests of the plane path, so both stay exact."""
+import os
+
+import pytest
+
+import pitt_object_table_segmentation_amd as pitt
+import test_plane_gpu as P
+import test_shortcuts_gpu as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=["0", "1"])
+def path_ctx(request):
+    old = os.environ.get("PITT_LANE_SCORE")
+    os.environ["PITT_LANE_SCORE"] = request.param
+    try:
+        c = pitt.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PITT_LANE_SCORE"]
+        else:
+            os.environ["PITT_LANE_SCORE"] = old
+    yield c
+    c.close()
+
+
+CASES = [P.test_full_size_frames_bit_exact, P.test_support_service_parameters, P.test_ragged_batch_and_edge_frames,
+         P.test_no_optimize_and_thresholds, S.test_inliers_confined_to_one_tile, S.test_infinite_and_nan_coordinates]
+CASES += [getattr(S, n) for n in dir(S) if n.startswith("test_") and getattr(S, n) not in CASES
+          and getattr(S, n).__code__.co_argcount == 1]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c.__name__ for c in CASES])
+def test_both_scoring_paths_bit_exact(path_ctx, case):
+    case(path_ctx)
+
+
+def test_both_paths_reduce_orders(path_ctx):
+    for order in (pitt.REDUCE_SSE2, pitt.REDUCE_HADD, pitt.REDUCE_SEQ):
+        P.test_reduce_orders_and_division_modes(path_ctx, order, pitt.DIV_EIGEN32)

@@ -161,7 +161,8 @@ def test_sphere_handler(srv):
     try:
         ok, inl, coef, centroid = srv.ransac_sphere(xyz)
         want = orc.sphere_segment(*xyz.T, orc.sphere_params(radius_min=0.1))
-        assert ok and len(inl) == len(want["inliers"][want["inliers"] != 0])
+        ref = want["inliers"][want["inliers"] != 0]  # PCL's float LM: points at the shell may differ
+        assert ok and len(np.setxor1d(inl, ref)) <= max(2, len(ref) // 500)
     finally:
         srv.erase_param("/pitt/srv/sphere_segmentation/min_radius_limit")
     # normals of the wrong size: PCL clears the outputs

@@ -143,3 +143,81 @@ def test_extract_indices(ctx):
     keep = torch.ones(8000, dtype=torch.bool, device="cuda")
     keep[idx.long()] = False
     assert torch.equal(ny, y[keep]) and nx.numel() == 5000
+
+
+# ---- the device-resident entry points ------------------------------------------
+def _dev(*arrays):
+    return [torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda() for a in arrays]
+
+
+def _compare_supports_dev(dev, ref):
+    assert len(dev) == len(ref)
+    for d, r in zip(dev, ref):
+        assert np.array_equal(d["idx_map"].cpu().numpy(), r["idx_map"])
+        assert np.array_equal(d["coefficients"], r["coefficients"])
+        assert np.array_equal(d["support_cloud"].cpu().numpy(), r["support_cloud"])
+        assert np.array_equal(d["on_support_cloud"].cpu().numpy(), r["on_support_cloud"])
+
+
+@pytest.mark.parametrize("seed,views,w,h", [(11, 2, 160, 120), (12, 4, 160, 120), (13, 1, 320, 240)])
+def test_find_supports_dev_matches_oracle(ctx, seed, views, w, h):
+    x, y, z = pitt.synth_fused(seed, views, w, h)
+    _compare_supports_dev(ctx.find_supports_dev(*_dev(x, y, z)), orc.find_supports(x, y, z))
+
+
+def test_find_supports_fused_1p2m_device_resident(ctx):
+    """BASELINE config 5 through the device entry points: pitt_segment_objects_dev (supports, then
+    every support's clusters, nothing leaving HBM) against the oracle's supports and clusters."""
+    x, y, z = pitt.synth_fused(1000, 4)
+    ref = orc.find_supports(x, y, z)
+    sups, objs = ctx.segment_objects_dev(*_dev(x, y, z))
+    _compare_supports_dev(sups, ref)
+    want = []
+    for k, r in enumerate(ref):
+        on = r["on_support_cloud"]
+        if len(on) >= 30:
+            want += [(k, c) for c in orc.euclidean_clusters(*on.T)]
+    assert len(objs) == len(want) and len(objs) >= 2
+    for (k, idx, sums), (kr, c) in zip(objs, want):
+        assert k == kr
+        assert np.array_equal(idx.cpu().numpy(), c["inliers"])
+        assert np.array_equal(sums / np.float32(len(c["inliers"]) + 1), c["centroid"])
+    # the sizes-only form returns the same layout without reading anything back
+    n_on, sizes = ctx.segment_objects_dev(*_dev(x, y, z), copy=False)
+    assert n_on == [len(r["on_support_cloud"]) for r in ref] and sizes == [len(c["inliers"]) for _, c in want]
+
+
+def test_euclidean_clusters_dev_matches_host(ctx):
+    rng = np.random.default_rng(5)
+    blobs = [_blob(rng.uniform(-1, 1, 3) * 3, int(rng.integers(2, 8))) for _ in range(30)]
+    p = np.concatenate(blobs)[rng.permutation(sum(len(b) for b in blobs))]
+    host = ctx.euclidean_clusters(*p.T, tolerance=0.03, min_size=3, max_size=400)
+    dev = ctx.euclidean_clusters_dev(*_dev(*p.T), tolerance=0.03, min_size=3, max_size=400)
+    ref = orc.euclidean_clusters(*p.T, min_rate=3 / len(p), max_rate=400 / len(p))
+    assert len(dev) == len(host) == len(ref)
+    for (idx, sums), h, r in zip(dev, host, ref):
+        assert np.array_equal(idx.cpu().numpy(), h.indices) and np.array_equal(h.indices, r["inliers"])
+        assert np.array_equal(sums, h.sum_xyz)
+    assert ctx.euclidean_clusters_dev(*_dev(*np.zeros((3, 0), np.float32))) == []
+
+
+def test_preprocessing_chain_device_resident_into_objects(ctx):
+    """obj_segmentation.cpp:238-283 with the cloud never leaving HBM: PointCloud2 payload -> unpack ->
+    deep filter -> world transform -> supports -> clusters, against the oracle chain."""
+    from test_preprocess_gpu import _pc2, _pose
+    rng = np.random.default_rng(3)
+    x, y, z = pitt.synth_frame(0, 1200, 320, 240)
+    xyz = np.stack([x, y, z], 1)
+    buf, row_step = _pc2(xyz, 16, 0, (0, 4, 8), 320, 240, rng)
+    ux, uy, uz = ctx.unpack_pointcloud2(torch.from_numpy(buf).cuda(), 320, 240, 16, row_step)
+    closer, _, used = ctx.deep_filter(ux, uy, uz, further=False)
+    m = _pose(0.0, 35.0, (0.0, 0.0, 1.35))
+    wx, wy, wz = ctx.transform_cloud(*closer, m)
+    sups, objs = ctx.segment_objects_dev(wx.contiguous(), wy.contiguous(), wz.contiguous())
+    rc, _ = orc.deep_filter(x, y, z, used)
+    rw = orc.transform_cloud(*rc.T, m)
+    ref = orc.find_supports(*rw.T)
+    _compare_supports_dev(sups, ref)
+    want = [(k, c) for k, r in enumerate(ref) if len(r["on_support_cloud"]) >= 30
+            for c in orc.euclidean_clusters(*r["on_support_cloud"].T)]
+    assert [(k, len(c["inliers"])) for k, c in want] == [(k, len(i)) for k, i, _ in objs]

@@ -1,5 +1,6 @@
 """BASELINE config 5 on one GPU: find_supports + euclidean_clusters on the 1.2M-point fused scene,
-repeated, for rocprofv3 kernel traces (tools/gpu_config5_prof.sh) and quick timing.
+repeated, for rocprofv3 kernel traces (tools/gpu_r03.sh) and quick timing: the device-resident
+scene path (pitt_segment_objects_dev) and the host-array service path.
 
     python tools/config5_run.py [reps]
 """
@@ -14,8 +15,19 @@ import pitt_object_table_segmentation_amd as pitt  # noqa: E402
 
 
 def main(reps=5):
+    import torch
     x, y, z = pitt.synth_fused(1000, 4)
+    dx, dy, dz = (torch.from_numpy(a).cuda() for a in (x, y, z))
     with pitt.Context(0) as ctx:
+        ts = []
+        for r in range(reps + 1):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            n_on, sizes = ctx.segment_objects_dev(dx, dy, dz, copy=False)
+            if r:
+                ts.append((time.perf_counter() - t) * 1e3)
+        print(f"config5 device path: {len(n_on)} supports, {len(sizes)} clusters; {np.median(ts):.2f} ms "
+              f"(median of {reps})", flush=True)
         ts = []
         for r in range(reps + 1):
             t = time.perf_counter()
@@ -33,8 +45,8 @@ def main(reps=5):
                 ts.append(((t1 - t) * 1e3, (t2 - t1) * 1e3))
         sup_ms = np.median([a for a, _ in ts])
         cl_ms = np.median([b for _, b in ts])
-        print(f"config5: {len(sups)} supports, {ncl} clusters; find_supports {sup_ms:.2f} ms, clusters {cl_ms:.2f} ms "
-              f"(median of {reps})")
+        print(f"config5 host path: {len(sups)} supports, {ncl} clusters; find_supports {sup_ms:.2f} ms, "
+              f"clusters {cl_ms:.2f} ms (median of {reps})")
 
 
 if __name__ == "__main__":
