@@ -534,6 +534,7 @@ def main():
                 "algorithmic_bytes_per_launch": round(nbytes / max(1, launches), 1),
             },
             "kernels": kernels,
+            "hip_graphs": dict(zip(("captures", "replays"), ctxs[0].graph_stats())),
         }
     if rank == 0 and world == 1 and not args.no_extras:
         line["cov_fast"] = cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, args.steps, B)

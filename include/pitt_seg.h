@@ -130,6 +130,8 @@ int  pitt_set_stream(pitt_ctx* ctx, void* hip_stream);
 /* Copy bytes between any host / device addresses on the context's stream (synchronous): for FFI
  * callers without HIP bindings reading the device-resident outputs (pitt_*_dev). */
 int  pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes);
+/* Plane batches captured into HIP graphs / replayed from them on this context ($PITT_GRAPHS=0 off). */
+int  pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays);
 void* pitt_get_stream(pitt_ctx* ctx);
 const char* pitt_last_error(pitt_ctx* ctx);
 int  pitt_abi_version(void);

@@ -474,6 +474,12 @@ class Context:
             res.append(ClusterResult(idx, np.array(list(c.sum_xyz), np.float32)))
         return res
 
+    def graph_stats(self):
+        """(captures, replays) of the plane pipeline's HIP graphs on this context."""
+        c, r = ctypes.c_int64(), ctypes.c_int64()
+        self._check(lib.pitt_graph_stats(self.h, ctypes.byref(c), ctypes.byref(r)), "pitt_graph_stats")
+        return c.value, r.value
+
     # ---- device-resident support / cluster path (pitt_*_dev) ---------------------------------
     def _dev_copy(self, ptr, n: int, dtype, device):
         """A fresh device tensor holding n elements copied from a device address of the arena."""

@@ -67,6 +67,21 @@ struct pitt_ctx {
     // first scoring chunk with lane-private counters (k_score LANE); $PITT_LANE_SCORE overrides
     bool lane_score = pitt_env_flag("PITT_LANE_SCORE", false);
 
+    // HIP graphs of the plane pipeline: a batch's ~20 launches are captured once per (layout,
+    // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the
+    // GPU, otherwise bounds the pipelined throughput.  $PITT_GRAPHS=0 disables.
+    bool use_graphs = pitt_env_flag("PITT_GRAPHS", true);
+    uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
+    struct GraphEntry {
+        std::vector<uint64_t> key;
+        hipGraphExec_t exec = nullptr;
+        uint64_t last_use = 0;
+    };
+    std::vector<GraphEntry> graphs;
+    std::vector<std::vector<uint64_t>> graph_seen;  // keys launched once (captured on a repeat)
+    uint64_t graph_clock = 0;
+    int64_t graph_captures = 0, graph_replays = 0;
+
     // profiling
     bool prof = false;
     std::vector<pitt::ProfRec> pending;

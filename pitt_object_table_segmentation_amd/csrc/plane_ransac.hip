@@ -1615,19 +1615,33 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
     if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    CovPart* part = nullptr;
+    if (p->cov_mode == PITT_COV_FAST) {
+        part = as<CovPart>(ctx->buf("cov_part", (size_t)nf * tiles_max * sizeof(CovPart)));
+        if (!part) return ctx->fail(PITT_E_NOMEM, "covariance partials");
+    }
+    pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
+    ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
+    void* hacct = acct ? ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4) : nullptr;
+    if (!hres || !hstat || (acct && !hacct)) return ctx->fail(PITT_E_NOMEM, "pinned results");
 
+    // Everything below is stream-ordered device work with device-built work lists.  Its launches
+    // depend only on the key below, so a repeated batch layout is captured into a HIP graph and
+    // replayed with one launch (profiling runs launch directly: their events time each kernel).
+    const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
+    const double log_prob = std::log(1.0 - p->probability);
+    std::vector<int> acct_recs((size_t)kAcKernels, -1);
+    std::vector<int> score_recs;
+    auto enqueue = [&]() -> int {
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
 
     int rec;
-    std::vector<int> acct_recs((size_t)kAcKernels, -1);
     rec = ctx->prof_begin("k_hypothesize", 0.0);
     acct_recs[kAcHyp] = rec;
     hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta,
                        tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
                        counters, cstat, acct);
     ctx->prof_end(rec);
-    const double log_prob = std::log(1.0 - p->probability);
-    std::vector<int> score_recs;
     for (int c = 0, h0 = 0; c < nchunks; h0 += chunks[(size_t)c], ++c) {
         const int H = chunks[(size_t)c];
         rec = ctx->prof_begin("k_score", 0.0);
@@ -1655,10 +1669,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        p->optimize ? 1 : 0, best_coef, final_coef);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
-    const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
     if (p->cov_mode == PITT_COV_FAST) {  // A6 fast mode: double sums over the chip, fixed tree
-        CovPart* part = as<CovPart>(ctx->buf("cov_part", (size_t)nf * tiles_max * sizeof(CovPart)));
-        if (!part) return ctx->fail(PITT_E_NOMEM, "covariance partials");
         rec = ctx->prof_begin("k_cov_tiles", 0.0);
         hipLaunchKernelGGL((k_cov_tiles<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
                            best_coef, thf, tile_counts, hstride, nf, tiles_max, part);
@@ -1686,15 +1697,72 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
     PITT_HIP_TRY(hipGetLastError());
-    pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
-    ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
-    void* hacct = nullptr;
     if (acct) {
-        hacct = ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4);
         PITT_HIP_TRY(hipMemcpyAsync(hacct, acct, acct_bytes, hipMemcpyDeviceToHost, sm));
         PITT_HIP_TRY(hipMemcpyAsync((char*)hacct + acct_bytes, acct_tiles, tile_words * 2 * 4, hipMemcpyDeviceToHost, sm));
+    }
+    return PITT_OK;
+    };
+    if (ctx->use_graphs && !ctx->prof && sm != nullptr) {
+        const double log_prob_k = std::log(1.0 - p->probability);
+        uint64_t thb = 0, lpb = 0;
+        std::memcpy(&thb, &thf, sizeof thf);
+        std::memcpy(&lpb, &log_prob_k, sizeof lpb);
+        std::vector<uint64_t> key = {ctx->arena_gen, (uint64_t)(uintptr_t)sm, (uint64_t)nf, (uint64_t)tiles_max,
+                                     (uint64_t)(uintptr_t)fr->x, (uint64_t)(uintptr_t)fr->y, (uint64_t)(uintptr_t)fr->z,
+                                     (uint64_t)(uintptr_t)inliers_dev, (uint64_t)A, (uint64_t)hcap,
+                                     (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
+                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV)};
+        pitt_ctx::GraphEntry* hit = nullptr;
+        for (auto& g : ctx->graphs)
+            if (g.key == key) hit = &g;
+        if (!hit) {
+            // capture on the second sight of a key (a one-off layout, e.g. a support-loop iteration,
+            // launches directly: capture and instantiation cost more than one enqueue)
+            auto seen = std::find(ctx->graph_seen.begin(), ctx->graph_seen.end(), key);
+            if (seen == ctx->graph_seen.end()) {
+                ctx->graph_seen.push_back(key);
+                if (ctx->graph_seen.size() > 16) ctx->graph_seen.erase(ctx->graph_seen.begin());
+            } else {
+                hipGraph_t graph = nullptr;
+                PITT_HIP_TRY(hipStreamBeginCapture(sm, hipStreamCaptureModeRelaxed));
+                const int erc = enqueue();
+                const hipError_t ce = hipStreamEndCapture(sm, &graph);
+                if (erc) {
+                    if (graph) (void)hipGraphDestroy(graph);
+                    return erc;
+                }
+                PITT_HIP_TRY(ce);
+                hipGraphExec_t exec = nullptr;
+                const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(graph);
+                PITT_HIP_TRY(ie);
+                if (ctx->graphs.size() >= 8) {  // evict the least recently used
+                    auto lru = std::min_element(ctx->graphs.begin(), ctx->graphs.end(),
+                                                [](const pitt_ctx::GraphEntry& a, const pitt_ctx::GraphEntry& b) {
+                                                    return a.last_use < b.last_use;
+                                                });
+                    (void)hipGraphExecDestroy(lru->exec);
+                    ctx->graphs.erase(lru);
+                }
+                ctx->graphs.push_back({key, exec, 0});
+                hit = &ctx->graphs.back();
+                ++ctx->graph_captures;
+            }
+        }
+        if (hit) {
+            hit->last_use = ++ctx->graph_clock;
+            PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
+            ++ctx->graph_replays;
+        } else {
+            const int erc = enqueue();
+            if (erc) return erc;
+        }
+    } else {
+        const int erc = enqueue();
+        if (erc) return erc;
     }
     // completion (pitt_wait): copy results out, price the score launches
     ctx->inflight = true;

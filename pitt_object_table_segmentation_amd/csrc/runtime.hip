@@ -67,6 +67,7 @@ void* pitt_ctx::buf(const std::string& name, size_t bytes) {
             return nullptr;
         }
         b.bytes = nb;
+        ++arena_gen;  // captured graphs that hold the old pointer are stale
         if (name == "tables") pool_keys.clear();  // device table pool lost
     }
     return b.p;
@@ -181,6 +182,8 @@ void pitt_destroy(pitt_ctx* ctx) {
     (void)pitt::finish_batch(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& g : ctx->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto& kv : ctx->host_pinned)
@@ -205,6 +208,13 @@ int pitt_set_stream(pitt_ctx* ctx, void* s) {
 }
 
 void* pitt_get_stream(pitt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays) {
+    if (!ctx) return PITT_E_INVALID;
+    if (captures) *captures = ctx->graph_captures;
+    if (replays) *replays = ctx->graph_replays;
+    return PITT_OK;
+}
 
 int pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     if (!ctx) return PITT_E_INVALID;

@@ -43,3 +43,40 @@ def test_both_scoring_paths_bit_exact(path_ctx, case):
 def test_both_paths_reduce_orders(path_ctx):
     for order in (pitt.REDUCE_SSE2, pitt.REDUCE_HADD, pitt.REDUCE_SEQ):
         P.test_reduce_orders_and_division_modes(path_ctx, order, pitt.DIV_EIGEN32)
+
+
+def test_hip_graph_replay_bit_exact():
+    """Repeated batch layouts are captured into a HIP graph (second sight) and replayed (third on):
+    the replays give the same records and inlier lists as direct launches ($PITT_GRAPHS=0) and the
+    oracle (pipelining)."""
+    import numpy as np
+    import torch
+    frames = [pitt.synth_frame(s, seed, 320, 240) for s, seed in ((0, 7000), (1, 7001), (2, 7002), (0, 7003))]
+    b = pitt.FrameBatch.from_host(frames, device="cuda:0")
+    old = os.environ.get("PITT_GRAPHS")
+    try:
+        os.environ["PITT_GRAPHS"] = "0"
+        direct = pitt.Context(0)
+        os.environ["PITT_GRAPHS"] = "1"
+        graphed = pitt.Context(0)
+    finally:
+        if old is None:
+            del os.environ["PITT_GRAPHS"]
+        else:
+            os.environ["PITT_GRAPHS"] = old
+    try:
+        ref_inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+        ref = direct.plane_segment_batch(b, pitt.sac_params(), ref_inl)
+        for k in range(4):
+            inl = torch.full((b.capacity,), -7, dtype=torch.int32, device="cuda:0")
+            res = graphed.plane_segment_batch(b, pitt.sac_params(), inl)
+            assert res.tobytes() == ref.tobytes(), k
+            for o, r in zip(b.offsets, ref):
+                assert torch.equal(inl[o:o + r["n_inliers"]], ref_inl[o:o + r["n_inliers"]]), k
+        captures, replays = graphed.graph_stats()
+        assert captures == 1 and replays == 3
+        assert direct.graph_stats() == (0, 0)
+        P._check(graphed, frames, ref, [ref_inl.cpu().numpy()[o:o + r["n_inliers"]] for o, r in zip(b.offsets, ref)])
+    finally:
+        direct.close()
+        graphed.close()
