@@ -341,6 +341,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the clutter / PCIe / config-5 passes")
     ap.add_argument("--no-inliers", action="store_true", help="skip writing the final inlier lists")
     ap.add_argument("--pipeline", type=int, default=3, help="contexts/streams with batches in flight")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's); set before HIP starts")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for world > 1 (nccl = RCCL over xGMI; gloo: tests)")
     ap.add_argument("--all-ranks-device", type=int, default=-1,
@@ -348,6 +350,8 @@ def main():
     ap.add_argument("--dump-records", default="",
                     help="rank 0 writes the (gathered) records of batch slot 0's last step to this .npy")
     args = ap.parse_args()
+    if args.hw_queues > 0:  # hardware queues per process (one per in-flight context's stream); before HIP init
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
     import torch
     import torch.distributed as dist

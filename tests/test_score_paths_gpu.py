@@ -67,8 +67,9 @@ def test_hip_graph_replay_bit_exact():
     try:
         ref_inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
         ref = direct.plane_segment_batch(b, pitt.sac_params(), ref_inl)
+        inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")  # one output buffer: one layout key
         for k in range(4):
-            inl = torch.full((b.capacity,), -7, dtype=torch.int32, device="cuda:0")
+            inl.fill_(-7)
             res = graphed.plane_segment_batch(b, pitt.sac_params(), inl)
             assert res.tobytes() == ref.tobytes(), k
             for o, r in zip(b.offsets, ref):
