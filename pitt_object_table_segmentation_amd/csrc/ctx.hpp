@@ -43,10 +43,20 @@ struct ProfTotal {
 
 }  // namespace pitt
 
+#ifndef PITT_REFINE_PRODUCERS_DEFAULT
+#define PITT_REFINE_PRODUCERS_DEFAULT 1
+#endif
+
 // A boolean knob from the environment ("0" / "1"), read when a context is created.
 inline bool pitt_env_flag(const char* name, bool dflt) {
     const char* v = std::getenv(name);
     return v && *v ? (v[0] != '0') : dflt;
+}
+// A small integer knob from the environment, clamped to [lo, hi].
+inline int pitt_env_int(const char* name, int dflt, int lo, int hi) {
+    const char* v = std::getenv(name);
+    const int x = v && *v ? std::atoi(v) : dflt;
+    return x < lo ? lo : x > hi ? hi : x;
 }
 
 struct pitt_ctx {
@@ -66,6 +76,13 @@ struct pitt_ctx {
 
     // first scoring chunk with lane-private counters (k_score LANE); $PITT_LANE_SCORE overrides
     bool lane_score = pitt_env_flag("PITT_LANE_SCORE", false);
+    // producer waves of k_refine (1..4); $PITT_REFINE_PRODUCERS overrides
+    int refine_producers = pitt_env_int("PITT_REFINE_PRODUCERS", PITT_REFINE_PRODUCERS_DEFAULT, 1, 4);
+    // k_refine variant (bit 1: producers write inlier lanes only, as masked stores)
+    int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 3);
+    // $PITT_REFINE_DEBUG=1: k_refine records per-role cycles and spins, printed at completion
+    bool refine_debug = pitt_env_flag("PITT_REFINE_DEBUG", false);
+    void* refine_dbg_h = nullptr;
 
     // HIP graphs of the plane pipeline: a batch's ~20 launches are captured once per (layout,
     // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -835,25 +836,34 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
 }
 
 // ------------------------------------------------------------------------------------------
-// k_refine: optimizeModelCoefficients (A6/A7) for one frame, one 3-wave block per frame.
+// k_refine: optimizeModelCoefficients (A6/A7) for one frame, one (P + 2)-wave block per frame.
 //
-//   producer  streams the frame's tiles that hold inliers of the winning hypothesis (4 points per
-//             lane per 256-point step, a global_load_lds ring kRDepth steps deep), selects the
-//             inliers and appends their coordinates -- ascending -- to an LDS ring;
-//   former    forms the six products of each full 256-inlier block (xx, xy, xz, yy, yz, zz, each
-//             separately rounded as PCL) with all 64 lanes into a product slot;
-//   chain     lanes 0..8 run the nine float accumulators of computeMeanAndCovarianceMatrix in
-//             exact PCL order as pure dependent adds; lane 0 then divides (Eigen 3.2
-//             `accu /= n`), runs eigen33 and writes the refined plane.
+//   producers  P waves stream the frame's tiles that hold inliers of the winning hypothesis, step
+//              s going to producer s % P (4 points per lane per 256-point step, a global_load_lds
+//              ring kRDepth steps deep per producer); each selects the step's inliers on its own
+//              and, in step order (a ticket in LDS), appends their coordinates -- ascending -- to
+//              the inlier ring;
+//   former     forms the six products of each full 256-inlier block (xx, xy, xz, yy, yz, zz, each
+//              separately rounded as PCL) with all 64 lanes into a product slot;
+//   chain      lanes 0..8 run the nine float accumulators of computeMeanAndCovarianceMatrix in
+//              exact PCL order as pure dependent adds; lane 0 then divides (Eigen 3.2
+//              `accu /= n`), runs eigen33 and writes the refined plane.
 //
-// The waves hand over ring space through LDS counters (W: produced, F: formed, R: summed).  The
-// final inlier list of every frame (refined or not) is the job of k_sel_mark / k_sel_write.
+// The chain's 9 dependent float streams bound the frame at ~1.9 ns per inlier.  One producer
+// (~0.45 us per step) stalls the chain across the runs of steps with few inliers, which one ring
+// cannot buffer; P producers select P steps at once and serialise only the append.
+// The waves hand over ring space through LDS counters (WS: step ticket | produced, F: formed,
+// R: summed).  The final inlier list of every frame (refined or not) is the job of k_sel_mark /
+// k_sel_write.
 constexpr int kRChunk = 256;   // points per producer step (4 per lane)
 constexpr int kRSlot = 3 * kRChunk;          // floats per raw ring slot (x, y, z)
-constexpr int kRDepth = 6;     // raw steps in flight (12 measured the same: the producer is
-                               // compute-bound, ~436 us per batch without the chain)
-constexpr int kRRing = 1024;   // compacted-inlier ring (points, a power of two; 4096 measured the same)
+constexpr int kRDepth = 4;     // raw steps in flight per producer
+#ifndef PITT_REFINE_RING
+#define PITT_REFINE_RING 1024
+#endif
+constexpr int kRRing = PITT_REFINE_RING;  // compacted-inlier ring (points, a power of two)
 constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
+// producer waves: k_refine<.., P> is instantiated for P = 1..4, pitt_ctx::refine_producers picks
 
 constexpr int kRMaxTiles = (1 << 21) / kTile;  // tile list capacity (frames up to 2M points)
 constexpr int kRStepsPerTile = kTile / kRChunk;
@@ -866,11 +876,15 @@ constexpr int kPS = kRBlk + 4;   // product stream stride, floats
 
 constexpr int kRProdSlots = 2;   // product blocks formed ahead of the chain
 
+template <int P>
 struct RefineLds {
-    float pool[kRDepth * kRSlot + 3 * kRS];  // raw[kRDepth] | cx | cy | cz (stride kRS)
+    float pool[P * kRDepth * kRSlot + 3 * kRS];  // raw[P][kRDepth] | cx | cy | cz (stride kRS)
     float prod[kRProdSlots][6 * kPS];    // xx, xy, xz, yy, yz, zz of the next chain blocks
     int tl[kRMaxTiles];             // the pass's tiles that can hold inliers, ascending
-    int W, R, F, done, total;  // produced, consumed (chain), formed (products)
+    // produced inliers (low word) | steps appended (high word), written as one 64-bit LDS store:
+    // the former and the chain read the low word, a producer waits for its step's ticket
+    alignas(8) unsigned long long WS;
+    int R, F, done, total, nact;    // consumed (chain), formed (products)
     float4 coef;
 };
 
@@ -897,7 +911,8 @@ __device__ __forceinline__ bool box_misses_slab(const float* __restrict__ b, flo
 // The tile list in LDS (ascending): tiles where the winning hypothesis counted inliers during
 // scoring (exact).  Returns the number of tiles, or -1 (stream every tile) for frames beyond the
 // list's capacity.
-__device__ __forceinline__ int refine_tiles(RefineLds& L, int tiles, int lane,
+template <class LDS>
+__device__ __forceinline__ int refine_tiles(LDS& L, int tiles, int lane,
                                             const int32_t* __restrict__ best_counts, int hstride) {
     if (tiles > kRMaxTiles) return -1;
     int nact = 0;
@@ -923,7 +938,8 @@ struct StepCursor {
     int base = 0;
 };
 
-__device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact, StepCursor& cur) {
+template <class LDS>
+__device__ __forceinline__ int refine_step(LDS& L, int s, int nact, StepCursor& cur) {
     if (nact < 0) return s;
     const int ti = s / kRStepsPerTile;
     if (ti != cur.tile) {
@@ -936,7 +952,8 @@ __device__ __forceinline__ int refine_step(RefineLds& L, int s, int nact, StepCu
     return cur.base + s % kRStepsPerTile;
 }
 
-__device__ __forceinline__ float* ring_x(RefineLds& L) { return L.pool + kRDepth * kRSlot; }
+template <int P>
+__device__ __forceinline__ float* ring_x(RefineLds<P>& L) { return L.pool + P * kRDepth * kRSlot; }
 
 typedef __attribute__((address_space(3))) volatile int lds_vint;  // ds_read/ds_write, not flat
 
@@ -956,29 +973,50 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
     asm volatile("" ::: "memory");
 }
 
-// Pass step c into ring slot (c - sb) % DEPTH; steps past the range [sb, se) re-read its last step
-// so that every iteration issues the same three loads (the waits below are fixed vmcnt counts).
-template <int DEPTH>
-__device__ __forceinline__ void refine_issue(RefineLds& L, float* raw, const float* xs, const float* ys,
-                                             const float* zs, int c, int sb, int se, int nact, int lane,
+// The 64-bit ticket word, read and written in asm (see refine_step: a visible LDS access in the
+// producer would wait for its in-flight global_load_lds writes).
+__device__ __forceinline__ unsigned long long lds_ticket_read(const unsigned long long* p) {
+    unsigned long long v;
+    asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_ticket_write(unsigned long long* p, unsigned long long v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
+}
+__device__ __forceinline__ int lds_read_asm(const int* p) {
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)p) : "memory");
+    return v;
+}
+
+// Producer q's local step j (pass step sb + q + j P) into its ring slot j % kRDepth; steps past
+// the range re-read the pass's last step so that every iteration issues the same three loads (the
+// waits below are fixed vmcnt counts).
+template <class LDS>
+__device__ __forceinline__ void refine_issue(LDS& L, float* raw, const float* xs, const float* ys,
+                                             const float* zs, int j, int step, int se, int nact, int lane,
                                              StepCursor& cur) {
     typedef __attribute__((address_space(3))) void* lds_ptr;
-    const int cc = refine_step(L, min(c, se - 1), nact, cur);
-    float* b = raw + ((c - sb) % DEPTH) * kRSlot;
+    const int cc = refine_step(L, min(step, se - 1), nact, cur);
+    float* b = raw + (j % kRDepth) * kRSlot;
     const int64_t o = (int64_t)cc * kRChunk + lane * 4;
     __builtin_amdgcn_global_load_lds(xs + o, (lds_ptr)(b), 16, 0, 0);
     __builtin_amdgcn_global_load_lds(ys + o, (lds_ptr)(b + kRChunk), 16, 0, 0);
     __builtin_amdgcn_global_load_lds(zs + o, (lds_ptr)(b + 2 * kRChunk), 16, 0, 0);
 }
 
-// Producer: one pass over the frame's listed steps [sb, se) with plane c, appending the inliers'
-// coordinates to the LDS ring for the former and the chain.  Returns the inlier count.
-template <int ORDER, int DEPTH>
-__device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const float* xs, const float* ys,
-                                             const float* zs, int64_t n, float4 c, float thf, int lane,
-                                             int nact, int sb, int se) {
-    int wpos = 0;
-    if (se <= sb) return 0;
+// Producer q of P: pass steps sb + q, sb + q + P, ... below se with plane c.  Each step's inliers
+// are selected independently; the append waits for the step's ticket (the previous step's
+// producer has appended), so the ring receives the inliers in ascending order.  The producer of
+// the pass's last step publishes the total and `done`.
+template <int ORDER, int P>
+__device__ __forceinline__ void refine_stream(RefineLds<P>& L, int q, const float* xs, const float* ys,
+                                              const float* zs, int64_t n, float4 c, float thf, int lane,
+                                              int nact, int sb, int se, uint32_t& spin_ticket, uint32_t& spin_ring,
+                                              bool masked) {
+    const int nj = se - sb > q ? (se - sb - q + P - 1) / P : 0;
+    if (nj == 0) return;
+    float* raw = L.pool + q * kRDepth * kRSlot;
     float* rx = ring_x(L);
     float tv;  // threshold and plane in VGPRs: a VALU op reading an SGPR issues at half rate
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
@@ -986,18 +1024,17 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
     StepCursor ic, pc;  // issue and process cursors
     int rfree = 0;      // the chain's ring position as last read
 #pragma unroll
-    for (int k = 0; k < DEPTH - 1; ++k) refine_issue<DEPTH>(L, raw, xs, ys, zs, sb + k, sb, se, nact, lane, ic);
-    for (int st = sb; st < se; ++st) {
+    for (int k = 0; k < kRDepth - 1; ++k) refine_issue(L, raw, xs, ys, zs, k, sb + q + k * P, se, nact, lane, ic);
+    for (int j = 0; j < nj; ++j) {
+        const int st = sb + q + j * P;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot refilled next are done
-        refine_issue<DEPTH>(L, raw, xs, ys, zs, st + DEPTH - 1, sb, se, nact, lane, ic);
-        // step st landed: younger are the DEPTH - 1 steps issued since (3 loads each; the producer
+        refine_issue(L, raw, xs, ys, zs, j + kRDepth - 1, st + (kRDepth - 1) * P, se, nact, lane, ic);
+        // step j landed: younger are the kRDepth - 1 steps issued since (3 loads each; the producer
         // issues no other vector-memory op, so the count is exact)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (kRDepth - 1)) : "memory");
         __builtin_amdgcn_sched_barrier(0);
-        // the slot's reads in asm: the compiler treats any LDS read as aliasing the ring's
-        // in-flight global_load_lds writes and would wait for all of them (vmcnt(0))
         const int ch = refine_step(L, st, nact, pc);  // the frame's step
-        const uint32_t b = (uint32_t)(uintptr_t)(raw + ((st - sb) % DEPTH) * kRSlot + lane * 4);
+        const uint32_t b = (uint32_t)(uintptr_t)(raw + (j % kRDepth) * kRSlot + lane * 4);
         float4 x4, y4, z4;
         asm volatile(
             "ds_read_b128 %0, %3\n"
@@ -1015,13 +1052,13 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
         if (s0 + kRChunk > n) {  // the frame's last step: points past its end never count
             const int lim = (int)(n - s0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (p0 + q >= lim) px[q] = __builtin_nanf("");
+            for (int k = 0; k < 4; ++k)
+                if (p0 + k >= lim) px[k] = __builtin_nanf("");
         }
         uint32_t bits = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            bits |= (fabsf(plane_dot<ORDER>(c, px[q], py[q], pz[q])) < tv ? 1u : 0u) << q;
+        for (int k = 0; k < 4; ++k)
+            bits |= (fabsf(plane_dot<ORDER>(c, px[k], py[k], pz[k])) < tv ? 1u : 0u) << k;
         // ascending positions: exclusive prefix of the per-lane counts (0..4) from their bit slices
         const int cnt = __builtin_popcount(bits);
         const uint64_t b0 = __builtin_amdgcn_ballot_w64((cnt & 1) != 0);
@@ -1032,26 +1069,61 @@ __device__ __forceinline__ int refine_stream(RefineLds& L, float* raw, const flo
                         2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b1 & lo), 0u)) +
                         4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(b2 & lo), 0u));
         const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+        // the step's ticket: every earlier step has been appended
+        const unsigned long long key = (unsigned long long)(uint32_t)(st - sb);
+        unsigned long long ws;
+        if constexpr (P == 1) {
+            ws = (key << 32) | (uint32_t)lds_ticket_read(&L.WS);  // own previous step: no wait
+        } else {
+            // uniform (one LDS word): compared in SGPRs, no divergent loop
+            while ((uint32_t)__builtin_amdgcn_readfirstlane((int)((ws = lds_ticket_read(&L.WS)) >> 32)) != (uint32_t)key)
+            {
+                __builtin_amdgcn_s_sleep(0);
+                ++spin_ticket;
+            }
+        }
+        const int wpos = (int)(uint32_t)ws;
         // ring space: the chain's position is re-read only when the cached one is too old
         if (wpos + tot - rfree > kRRing) {
-            while (wpos + tot - (rfree = lds_acquire(&L.R)) > kRRing) __builtin_amdgcn_s_sleep(1);
+            while (wpos + tot - (rfree = lds_read_asm(&L.R)) > kRRing) {
+                __builtin_amdgcn_s_sleep(1);
+                ++spin_ring;
+            }
         }
         int k = wpos + pre;
-        // branch-free: a point that is not an inlier writes into the streams' padding (never read)
+        if (masked) {  // PITT_REFINE_MODE bit 1: only inlier lanes write (LDS cost per active lane)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = (bits >> q) & 1u;
-            const int r = in ? (k & (kRRing - 1)) : kRRing;
-            rx[r] = px[q];
-            rx[kRS + r] = py[q];
-            rx[2 * kRS + r] = pz[q];
-            k += in ? 1 : 0;
+            for (int e = 0; e < 4; ++e) {
+                if ((bits >> e) & 1u) {
+                    const int r = k & (kRRing - 1);
+                    rx[r] = px[e];
+                    rx[kRS + r] = py[e];
+                    rx[2 * kRS + r] = pz[e];
+                    ++k;
+                }
+            }
+        } else {
+            // branch-free: a point that is not an inlier writes into the streams' padding (never read)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool in = (bits >> e) & 1u;
+                const int r = in ? (k & (kRRing - 1)) : kRRing;
+                rx[r] = px[e];
+                rx[kRS + r] = py[e];
+                rx[2 * kRS + r] = pz[e];
+                k += in ? 1 : 0;
+            }
         }
-        if (lane == 0) lds_release(&L.W, wpos + tot);
-        wpos += tot;
+        // after the step's writes (LDS executes a wave's operations in order)
+        if (lane == 0) {
+            lds_ticket_write(&L.WS, ((key + 1) << 32) | (uint32_t)(wpos + tot));
+            if (st == se - 1) {
+                L.total = wpos + tot;
+                lds_release(&L.done, 1);
+            }
+        }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read steps land before the pool is reused
-    return wpos;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read steps land before the block ends
 }
 
 // 16 dependent adds, back to back, in order.
@@ -1088,16 +1160,18 @@ __device__ __forceinline__ void chain32(float& s, const f4v (&v)[8]) {
 
 // Former wave: the six product streams of each full 256-inlier block (formed by all 64 lanes,
 // separately rounded as PCL) into a product slot, up to kRProdSlots blocks ahead of the chain.
-__device__ __forceinline__ void refine_form(RefineLds& L, int lane) {
+template <int P>
+__device__ __forceinline__ void refine_form(RefineLds<P>& L, int lane, uint32_t& spins) {
     float* rx = ring_x(L);
     int rf = 0, rc = 0;  // formed; the chain's position as last read
     while (true) {
-        const int w = lds_acquire(&L.W);
+        const int w = lds_acquire(reinterpret_cast<int*>(&L.WS));
         if (w - rf >= kRBlk) {
             if (rf - rc >= kRProdSlots * kRBlk) {  // the slot is still being summed
                 rc = lds_acquire(&L.R);
                 if (rf - rc >= kRProdSlots * kRBlk) {
                     __builtin_amdgcn_s_sleep(1);
+                    ++spins;
                     continue;
                 }
             }
@@ -1117,16 +1191,19 @@ __device__ __forceinline__ void refine_form(RefineLds& L, int lane) {
             if (lane == 0) lds_release(&L.F, rf);  // after the block's writes (in-order LDS)
             continue;
         }
-        if (lds_acquire(&L.done) && lds_acquire(&L.W) - rf < kRBlk) break;  // the rest is the chain's tail
+        if (lds_acquire(&L.done) && lds_acquire(reinterpret_cast<int*>(&L.WS)) - rf < kRBlk) break;  // the rest is the chain's tail
         __builtin_amdgcn_s_sleep(1);
+        spins += 1u << 16;  // waiting for inliers (high half) vs for a free product slot (low half)
     }
 }
 
 // Chain wave: lane k < 9 accumulates stream k of computeMeanAndCovarianceMatrix (xx, xy, xz, yy,
 // yz, zz, x, y, z) in ascending inlier order as pure dependent adds, 64 elements per batched read:
 // the products from the former's slots, x, y, z from the inlier ring.  Lanes >= 9 repeat lane 0's
-// stream (uniform control flow; results unused).  The last partial block goes element by element.
-__device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
+// stream (uniform control flow: limiting the reads to 9 active lanes measured slower,
+// tools/microbench/chain_rate.hip).  The last partial block goes element by element.
+template <int P>
+__device__ __forceinline__ float refine_chain(RefineLds<P>& L, int lane, uint32_t& spins, long long& busy, bool timed) {
     const int k = lane < 9 ? lane : 0;
     float* rx = ring_x(L);
     float s = 0.0f;
@@ -1134,10 +1211,12 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
     while (true) {
         const int formed = lds_acquire(&L.F);
         if (formed - r >= kRBlk) {
+            const long long tb = timed ? clock64() : 0;
             const int q = r & (kRRing - 1);
             const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
-            // in asm: the compiler would otherwise sink each read to just before its use)
+            // in asm: the compiler would otherwise sink each read to just before its use).  A
+            // variant that also read the next block ahead of the boundary measured slower.
             const uint32_t pa = (uint32_t)(uintptr_t)p;
             f4v A[8], B[8];
             lds_read32(A, pa);
@@ -1156,10 +1235,11 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
             }
             r += kRBlk;
             if (lane == 0) lds_release(&L.R, r);
+            if (timed) busy += clock64() - tb;
             continue;
         }
         if (lds_acquire(&L.done)) {
-            const int wf = lds_acquire(&L.W);
+            const int wf = lds_acquire(reinterpret_cast<int*>(&L.WS));
             if (wf - r < kRBlk) {  // every full block summed: the tail element by element
                 const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRS : rx + 2 * kRS;
                 const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRS : rx + 2 * kRS;
@@ -1171,6 +1251,7 @@ __device__ __forceinline__ float refine_chain(RefineLds& L, int lane) {
             }
         }
         __builtin_amdgcn_s_sleep(1);
+        ++spins;
     }
     return s;
 }
@@ -1210,13 +1291,15 @@ __device__ float4 refine_plane(float a9[9], int n) {
     return refine_plane_mean<ORDER>(a9);
 }
 
-template <int ORDER, int DIV>
-__global__ __launch_bounds__(192) void k_refine(
+template <int ORDER, int DIV, int P>
+__global__ __launch_bounds__(64 * (P + 2)) void k_refine(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
-    int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct) {
-    __shared__ RefineLds L;
+    int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct,
+    unsigned long long* __restrict__ rdbg, int mode) {
+    __shared__ RefineLds<P> L;
+    const long long t_start = rdbg ? clock64() : 0;
     const int f = blockIdx.x;
     const FrameState s = st[f];
     if (!s.has_model || !s.need_refine) return;
@@ -1226,35 +1309,61 @@ __global__ __launch_bounds__(192) void k_refine(
     const float* xs = X + m.off;
     const float* ys = Y + m.off;
     const float* zs = Z + m.off;
-    if (threadIdx.x == 0) {
-        L.W = 0;
-        L.R = 0;
-        L.F = 0;
-        L.done = 0;
-        L.coef = best_coef[f];
-    }
-    __syncthreads();
     if (wave == 0) {
-        const float4 cb = L.coef;
         const int nact = refine_tiles(L, m.tiles, lane, tile_counts + (int64_t)f * tiles_max * hstride + s.best_h,
                                       hstride);
         const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
-        const int total = refine_stream<ORDER, kRDepth>(L, L.pool, xs, ys, zs, m.n, cb, thf, lane, nact, 0, nsteps);
-        // the listed tiles' points, their count words, the plane in and out
-        if (lane == 0)
-            acct_add(acct, kAcRefine, (unsigned long long)nsteps * kRChunk * 12ull + (unsigned long long)m.tiles * 4ull + 32ull);
         if (lane == 0) {
-            L.total = total;
-            lds_release(&L.done, 1);
+            L.WS = 0ull;
+            L.R = 0;
+            L.F = 0;
+            L.done = nsteps == 0 ? 1 : 0;  // nothing to stream: no producer publishes
+            L.total = 0;
+            L.nact = nact;
+            L.coef = best_coef[f];
+            // the listed tiles' points, their count words, the plane in and out
+            acct_add(acct, kAcRefine, (unsigned long long)nsteps * kRChunk * 12ull + (unsigned long long)m.tiles * 4ull + 32ull);
         }
-    } else if (wave == 1) {
-        refine_form(L, lane);
+    }
+    __syncthreads();
+    if (wave < P) {
+        const int nact = L.nact;
+        const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+        uint32_t spin_ticket = 0, spin_ring = 0;
+        refine_stream<ORDER, P>(L, wave, xs, ys, zs, m.n, L.coef, thf, lane, nact, 0, nsteps, spin_ticket, spin_ring,
+                                (mode & 2) != 0);
+        if (rdbg && lane == 0 && wave < 2) {  // PITT_REFINE_DEBUG: cycles and spin counts per role
+            unsigned long long* d = rdbg + (int64_t)f * 16 + 4 + 4 * wave;
+            d[0] = (unsigned long long)(clock64() - t_start);
+            d[1] = spin_ticket;
+            d[2] = spin_ring;
+            d[3] = (unsigned long long)nsteps;
+        }
+    } else if (wave == P) {
+        __builtin_amdgcn_s_setprio(2);
+        uint32_t spins = 0;
+        refine_form(L, lane, spins);
+        if (rdbg && lane == 0) {
+            rdbg[(int64_t)f * 16 + 2] = (unsigned long long)(clock64() - t_start);
+            rdbg[(int64_t)f * 16 + 3] = spins;
+        }
     } else {
-        const float acc = refine_chain(L, lane);
+        // the chain bounds the frame: first call on its SIMD's issue slots
+        __builtin_amdgcn_s_setprio(3);
+        uint32_t spins = 0;
+        long long busy = 0;
+        const float acc = refine_chain(L, lane, spins, busy, rdbg != nullptr);
         float a9[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
-        if (lane == 0) final_coef[f] = refine_plane<ORDER, DIV>(a9, lds_acquire(&L.W));
+        const int n_in = lds_acquire(reinterpret_cast<int*>(&L.WS));
+        if (lane == 0) final_coef[f] = refine_plane<ORDER, DIV>(a9, n_in);
+        if (rdbg && lane == 0) {
+            rdbg[(int64_t)f * 16 + 0] = (unsigned long long)(clock64() - t_start);
+            rdbg[(int64_t)f * 16 + 1] = spins;
+            rdbg[(int64_t)f * 16 + 12] = (unsigned long long)n_in;
+            rdbg[(int64_t)f * 16 + 13] = (unsigned long long)busy;
+        }
     }
 }
 
@@ -1624,6 +1733,13 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
     void* hacct = acct ? ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4) : nullptr;
     if (!hres || !hstat || (acct && !hacct)) return ctx->fail(PITT_E_NOMEM, "pinned results");
+    // $PITT_REFINE_DEBUG: k_refine's per-role cycles and spin counts, summarised on stderr by pitt_wait
+    unsigned long long* rdbg = nullptr;
+    if (ctx->refine_debug) {
+        rdbg = as<unsigned long long>(ctx->buf("refine_dbg", (size_t)nf * 16 * 8));
+        ctx->refine_dbg_h = ctx->pinned("refine_dbg_h", (size_t)nf * 16 * 8);
+        if (!rdbg || !ctx->refine_dbg_h) return ctx->fail(PITT_E_NOMEM, "refine debug");
+    }
 
     // Everything below is stream-ordered device work with device-built work lists.  Its launches
     // depend only on the key below, so a repeated batch layout is captured into a HIP graph and
@@ -1680,8 +1796,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     } else {
         rec = ctx->prof_begin("k_refine", 0.0);
         acct_recs[kAcRefine] = rec;
-        hipLaunchKernelGGL((k_refine<ORDER, DIV>), dim3(nf), dim3(192), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                           thf, tile_counts, hstride, tiles_max, final_coef, acct);
+        const int P = ctx->refine_producers;
+        auto kern = P == 1 ? k_refine<ORDER, DIV, 1> : P == 2 ? k_refine<ORDER, DIV, 2>
+                  : P == 3 ? k_refine<ORDER, DIV, 3> : k_refine<ORDER, DIV, 4>;
+        hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+                           thf, tile_counts, hstride, tiles_max, final_coef, acct, rdbg, ctx->refine_mode);
         ctx->prof_end(rec);
     }
     rec = ctx->prof_begin("k_sel_mark", 0.0);
@@ -1699,6 +1818,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     PITT_HIP_TRY(hipGetLastError());
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
+    if (rdbg) PITT_HIP_TRY(hipMemcpyAsync(ctx->refine_dbg_h, rdbg, (size_t)nf * 16 * 8, hipMemcpyDeviceToHost, sm));
     if (acct) {
         PITT_HIP_TRY(hipMemcpyAsync(hacct, acct, acct_bytes, hipMemcpyDeviceToHost, sm));
         PITT_HIP_TRY(hipMemcpyAsync((char*)hacct + acct_bytes, acct_tiles, tile_words * 2 * 4, hipMemcpyDeviceToHost, sm));
@@ -1714,7 +1834,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uintptr_t)fr->x, (uint64_t)(uintptr_t)fr->y, (uint64_t)(uintptr_t)fr->z,
                                      (uint64_t)(uintptr_t)inliers_dev, (uint64_t)A, (uint64_t)hcap,
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
-                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV)};
+                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV),
+                                     (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode};
         pitt_ctx::GraphEntry* hit = nullptr;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
@@ -1789,6 +1910,27 @@ int finish_batch(pitt_ctx* ctx) {
     ctx->inflight = false;
     PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     std::memcpy(ctx->inflight_results, ctx->inflight_hres, (size_t)ctx->inflight_frames * sizeof(pitt_plane_result));
+    if (ctx->refine_debug && ctx->refine_dbg_h) {  // mean / max over the refined frames, cycles
+        const unsigned long long* d = (const unsigned long long*)ctx->refine_dbg_h;
+        double sum[16] = {0}, mx[16] = {0};
+        int cnt = 0;
+        for (int f = 0; f < ctx->inflight_frames; ++f) {
+            if (d[f * 16] == 0) continue;
+            ++cnt;
+            for (int k = 0; k < 16; ++k) {
+                sum[k] += (double)d[f * 16 + k];
+                mx[k] = std::max(mx[k], (double)d[f * 16 + k]);
+            }
+        }
+        if (cnt) {
+            static const char* names[14] = {"chain_cyc", "chain_spin", "form_cyc", "form_spin(hi:data lo:slot)",
+                                            "p0_cyc", "p0_ticket", "p0_ring", "steps", "p1_cyc", "p1_ticket",
+                                            "p1_ring", "p1_steps", "inliers", "chain_busy"};
+            std::fprintf(stderr, "[refine_debug] frames %d producers %d\n", cnt, ctx->refine_producers);
+            for (int k = 0; k < 14; ++k)
+                std::fprintf(stderr, "[refine_debug] %-28s mean %14.1f max %14.1f\n", names[k], sum[k] / cnt, mx[k]);
+        }
+    }
     const ChunkStat* hstat = (const ChunkStat*)ctx->inflight_hstat;
     for (size_t c = 0; c < ctx->inflight_score_recs.size(); ++c)
         ctx->prof_set_bytes(ctx->inflight_score_recs[c],

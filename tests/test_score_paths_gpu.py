@@ -2,7 +2,9 @@
 (compaction, v_cmp -> s_bcnt1 -> v_writelane per surviving (group, hypothesis) pair) and the
 lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only, |d| - t sign bits
 added into lane-private counters).  $PITT_LANE_SCORE picks one when a context is created; the other
-is run here on the bit-exact parity tests of the plane path, so both stay exact."""
+is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
+producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel and appending in
+step order): every count must give the same ascending inlier stream, hence the same floats."""
 import os
 
 import pytest
@@ -14,17 +16,22 @@ import test_shortcuts_gpu as S
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["0", "1"])
+VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
+            {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}]
+
+
+@pytest.fixture(scope="module", params=VARIANTS, ids=lambda v: "-".join(f"{k[5:].lower()}{x}" for k, x in v.items()))
 def path_ctx(request):
-    old = os.environ.get("PITT_LANE_SCORE")
-    os.environ["PITT_LANE_SCORE"] = request.param
+    old = {k: os.environ.get(k) for k in request.param}
+    os.environ.update(request.param)
     try:
         c = pitt.Context(0)
     finally:
-        if old is None:
-            del os.environ["PITT_LANE_SCORE"]
-        else:
-            os.environ["PITT_LANE_SCORE"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     yield c
     c.close()
 
