@@ -464,6 +464,52 @@ int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, const float*
 int pitt_axis_height_host(pitt_ctx* ctx, const float* xyz16, int64_t n, const float coef[6], int32_t mode,
                           float* height, int32_t* idx1, int32_t* idx2, float centroid[3]);
 
+/* --- primitive classification of a frame's clusters --------------------------------------- */
+/* The loop of ransac_segmentation.cpp:230-302 (clustersAcquisition) for all of a frame's clusters in
+ * one call: per cluster the normals (PCManager::estimateNormal, k = 50), the sphere, cylinder, cone and
+ * plane services as their handlers run them (sphere_segmentation_srv.cpp:29-96,
+ * cylinder_segmentation_srv.cpp:82-216, cone_segmentation_srv.cpp:83-216, plane_segmentation_srv.cpp:
+ * 27-74: the same RANSAC, refinement, selection and axis-height post-processing), the responses'
+ * inlier lists without index 0 (PCManager::inlierToVectorMsg, Q1), and the arbitration on their sizes
+ * (:265-302).  The clusters move through every stage together: the host synchronises once per stage
+ * for the frame (about 30 times), not per cluster and service.  Replaces the per-cluster service calls
+ * of clustersAcquisition (:239-258). */
+enum { PITT_SHAPE_UNKNOWN = 0, PITT_SHAPE_PLANE = 1, PITT_SHAPE_SPHERE = 2, PITT_SHAPE_CONE = 3,
+       PITT_SHAPE_CYLINDER = 4 };  /* TXT_*_SHAPE_TAG, ransac_segmentation.cpp:42-46 */
+enum { PITT_SRV_SPHERE = 0, PITT_SRV_CYLINDER = 1, PITT_SRV_CONE = 2, PITT_SRV_PLANE = 3 };
+typedef struct {
+    int32_t              k;                 /* normal neighbours: 50 (pc_manager.cpp:18), 1..64 */
+    float                viewpoint[3];      /* the normals' viewpoint: the origin (PCL default) */
+    pitt_sac_params      plane;             /* plane service: pitt_sac_params_default */
+    pitt_sphere_params   sphere;            /* the services' defaults (pitt_classify_params_default) */
+    pitt_cylinder_params cylinder;
+    pitt_cone_params     cone;
+    float                cone_over_cylinder; /* DEFAULT_CONE_OVER_CYLINDER_PRIORITY 0.9 (:37) */
+    int32_t              pad;
+} pitt_classify_params;
+void pitt_classify_params_default(pitt_classify_params* p);
+typedef struct {
+    int64_t n_points;
+    int32_t tag;              /* PITT_SHAPE_*: the arbitration */
+    int32_t inliers[4];       /* [PITT_SRV_*] the response's inlier count (index 0 dropped, Q1) */
+    int32_t status[4];        /* PITT_OK (a model) / PITT_NO_MODEL / error */
+    int32_t hypotheses[4];    /* the services' RANSAC iterations */
+    int32_t n_coef[4];        /* response coefficients: 4 / 4 with a model (else 0); cylinder and cone
+                                 7 + height with a model, else just the height -1 */
+    float   sphere[4];        /* centre, radius */
+    float   cylinder[8];      /* axis point, direction, radius, height */
+    float   cone[8];          /* apex, direction, opening angle, height */
+    float   plane[4];
+    float   centroid[4][3];   /* the responses' x/y/z_centroid (plane: 0; without inliers: 0) */
+    float   est_centroid[3];  /* the chosen primitive's centroid (TrackedShape x/y/z_est_centroid) */
+    int32_t pad;
+} pitt_cluster_shape;
+/* x/y/z: device (or host) SoA; cluster c = points [offsets[c], offsets[c] + counts[c]) (host arrays).
+ * out: host [n_clusters]. */
+int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float* y, const float* z, const int64_t* offsets,
+                           const int64_t* counts, int32_t n_clusters, const pitt_classify_params* params,
+                           pitt_cluster_shape* out);
+
 /* --- synthetic organised clouds (tools; deterministic from scene_seed) ---------------------- */
 enum { PITT_SCENE_TABLE = 0, PITT_SCENE_CLUTTER = 1, PITT_SCENE_TABLE_NAN = 2 };
 /* 640x480 Kinect-like pinhole cloud in the camera optical frame, row-major pixel order.

@@ -13,6 +13,8 @@
  *   pitt_srv_ransac_cone      <-> ransacConeDetaction     cone_segmentation_srv.cpp:83
  *   pitt_srv_call_ransac_plane <-> callRansacPlaneSegmentation  ransac_segmentation.cpp:175-199
  *   pitt_srv_arbitrate        <-> clustersAcquisition's arbitration  ransac_segmentation.cpp:265-302
+ *   pitt_srv_classify_clusters <-> clustersAcquisition's loop over a frame's clusters (normals, the four
+ *                               services, the arbitration)            ransac_segmentation.cpp:230-302
  * Clouds are PCL PointXYZ arrays (x, y, z, pad: 16-byte stride), host memory.
  * Handler calls return 1 when the handler returns true, 0 when false, < 0 on an ABI error.
  */
@@ -88,6 +90,14 @@ int pitt_srv_call_ransac_plane(pitt_srv* srv, const float* xyz16, int64_t n, int
  * 4 cylinder; :42-46) or PITT_E_INVALID for a negative count. */
 int pitt_srv_arbitrate(int64_t sphere_inliers, int64_t cylinder_inliers, int64_t cone_inliers,
                        int64_t plane_inliers);
+
+/* clustersAcquisition's loop (ransac_segmentation.cpp:230-302) over n_clusters clusters of one SoA
+ * (device or host x/y/z; cluster c = [offsets[c], offsets[c] + counts[c]), host arrays): the four
+ * services with the parameters their handlers read, one pass for all clusters (pitt_classify_clusters).
+ * out: host [n_clusters].  Returns the pitt status. */
+int pitt_srv_classify_clusters(pitt_srv* srv, const float* x, const float* y, const float* z,
+                               const int64_t* offsets, const int64_t* counts, int32_t n_clusters,
+                               pitt_cluster_shape* out);
 
 /* used_out: the response's used_* fields in declaration order:
  * cloud%, plane%, max var, min var, max iter, distance th, normal weight, axis[3], offset[3] */

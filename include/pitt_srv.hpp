@@ -242,6 +242,15 @@ public:
     // priority over the cylinder, :37, compared in float), then cylinder, plane, sphere; all zero or
     // no rule -> unknown.  Tags as ransac_segmentation.cpp:42-46.
     static int arbitratePrimitive(size_t sphereInl, size_t cylinderInl, size_t coneInl, size_t planeInl);
+    // ransac_segmentation.cpp:230-302 for all of a frame's clusters in one pass (pitt_classify_clusters)
+    // with the parameters the four handlers read; returns the pitt status
+    int classifyClusters(const float* x, const float* y, const float* z, const int64_t* offsets,
+                         const int64_t* counts, int32_t n, pitt_cluster_shape* out);
+    // the parameters each primitive handler reads from the parameter server on every call
+    pitt_sac_params planeParams();
+    pitt_sphere_params sphereParams();
+    pitt_cylinder_params cylinderParams();
+    pitt_cone_params coneParams();
     // obj_segmentation.cpp:143-207 + :261-312: supports (request fields from params, -1 = default),
     // then clusters per support; one ClustersOutput per support with at least one cluster.
     std::vector<pitt_msgs::ClustersOutput> segmentObjects(const pitt_msgs::PointCloud& world_cloud,

@@ -96,6 +96,26 @@ class ConeParams(ctypes.Structure):
                 ("pad", ctypes.c_int32)]
 
 
+class ClassifyParams(ctypes.Structure):
+    """pitt_classify_params (include/pitt_seg.h)."""
+    _fields_ = [("k", ctypes.c_int32), ("viewpoint", ctypes.c_float * 3), ("plane", SacParams),
+                ("sphere", SphereParams), ("cylinder", CylinderParams), ("cone", ConeParams),
+                ("cone_over_cylinder", ctypes.c_float), ("pad", ctypes.c_int32)]
+
+
+class ClusterShape(ctypes.Structure):
+    """pitt_cluster_shape (include/pitt_seg.h)."""
+    _fields_ = [("n_points", ctypes.c_int64), ("tag", ctypes.c_int32), ("inliers", ctypes.c_int32 * 4),
+                ("status", ctypes.c_int32 * 4), ("hypotheses", ctypes.c_int32 * 4), ("n_coef", ctypes.c_int32 * 4),
+                ("sphere", ctypes.c_float * 4), ("cylinder", ctypes.c_float * 8), ("cone", ctypes.c_float * 8),
+                ("plane", ctypes.c_float * 4), ("centroid", (ctypes.c_float * 3) * 4),
+                ("est_centroid", ctypes.c_float * 3), ("pad", ctypes.c_int32)]
+
+
+SHAPE_UNKNOWN, SHAPE_PLANE, SHAPE_SPHERE, SHAPE_CONE, SHAPE_CYLINDER = 0, 1, 2, 3, 4
+SRV_SPHERE, SRV_CYLINDER, SRV_CONE, SRV_PLANE = 0, 1, 2, 3
+
+
 class SupportParams(ctypes.Structure):
     _fields_ = [
         ("min_iterative_cloud_percentage", ctypes.c_float),
@@ -246,6 +266,9 @@ SIGNATURES = {
     "pitt_profile_get": (_i32, [_vp, ctypes.c_char_p, _i64p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_double)]),
     "pitt_profile_reset": (_i32, [_vp]),
+    "pitt_classify_params_default": (None, [ctypes.POINTER(ClassifyParams)]),
+    "pitt_classify_clusters": (_i32, [_vp, _vp, _vp, _vp, _i64p, _i64p, _i32, ctypes.POINTER(ClassifyParams),
+                                      ctypes.POINTER(ClusterShape)]),
 }
 
 
@@ -291,6 +314,7 @@ SIGNATURES.update({
     "pitt_srv_segment_objects": (_i32, [_vp, _f32p, _i64, _i64, _i32p]),
     "pitt_srv_output_size": (_i32, [_vp, _i32, _i32p]),
     "pitt_srv_output_cluster": (_i32, [_vp, _i32, _i32, _i32p, _i64p, _f32p]),
+    "pitt_srv_classify_clusters": (_i32, [_vp, _vp, _vp, _vp, _i64p, _i64p, _i32, ctypes.POINTER(ClusterShape)]),
 })
 
 

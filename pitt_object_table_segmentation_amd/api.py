@@ -547,6 +547,23 @@ class Context:
                  np.array(list(out.objects[i].sum_xyz), np.float32)) for i in range(out.n_objects)]
         return sups, objs
 
+    # ---- primitive classification -----------------------------------------------------------
+    def classify_clusters(self, x, y, z, offsets, counts, params: Optional[L.ClassifyParams] = None):
+        """pitt_classify_clusters (ransac_segmentation.cpp:230-302 for all of a frame's clusters in one
+        pass): device (or host) SoA, cluster c = [offsets[c], offsets[c] + counts[c]).  Returns one dict
+        per cluster: tag, inliers / status / hypotheses / coefficients / centroid per service (sphere,
+        cylinder, cone, plane) and the chosen primitive's est_centroid."""
+        offsets = np.ascontiguousarray(np.asarray(offsets, np.int64))
+        counts = np.ascontiguousarray(np.asarray(counts, np.int64))
+        nc = len(counts)
+        prm = params or classify_params()
+        out = (L.ClusterShape * max(nc, 1))()
+        ptr = (lambda a: a.data_ptr()) if hasattr(x, "data_ptr") else (lambda a: np.ascontiguousarray(a, np.float32).ctypes.data)
+        keep = [x, y, z] if hasattr(x, "data_ptr") else [np.ascontiguousarray(a, np.float32) for a in (x, y, z)]
+        self._check(lib.pitt_classify_clusters(self.h, *(ptr(a) for a in keep), _i64(offsets), _i64(counts), nc,
+                                               ctypes.byref(prm), out), "pitt_classify_clusters")
+        return [_shape_dict(out[c]) for c in range(nc)]
+
     # ---- profiling --------------------------------------------------------------------------
     def profile(self, on: bool = True) -> None:
         lib.pitt_profile_enable(self.h, 1 if on else 0)
@@ -559,6 +576,34 @@ class Context:
         self._check(lib.pitt_profile_get(self.h, kernel.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(b)),
                     "pitt_profile_get")
         return n.value, ms.value, b.value
+
+
+def classify_params(**kw) -> L.ClassifyParams:
+    """pitt_classify_params_default (the four services' handler defaults, k = 50), fields overridden by
+    keyword (e.g. k=50, cone_over_cylinder=0.9)."""
+    p = L.ClassifyParams()
+    lib.pitt_classify_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+SERVICE_NAMES = ("sphere", "cylinder", "cone", "plane")
+SHAPE_NAMES = {L.SHAPE_UNKNOWN: "unknown", L.SHAPE_PLANE: "plane", L.SHAPE_SPHERE: "sphere", L.SHAPE_CONE: "cone",
+               L.SHAPE_CYLINDER: "cylinder"}  # returnPrimitiveNameFromTag, ransac_segmentation.cpp:210-218
+
+
+def _i64(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def _shape_dict(o) -> dict:
+    coef = [np.array(o.sphere[:o.n_coef[0]], np.float32), np.array(o.cylinder[:o.n_coef[1]], np.float32),
+            np.array(o.cone[:o.n_coef[2]], np.float32), np.array(o.plane[:o.n_coef[3]], np.float32)]
+    return dict(n_points=o.n_points, tag=o.tag, shape=SHAPE_NAMES.get(o.tag, "unknown"),
+                inliers=list(o.inliers), status=list(o.status), hypotheses=list(o.hypotheses), coefficients=coef,
+                centroid=np.array([list(c) for c in o.centroid], np.float32),
+                est_centroid=np.array(list(o.est_centroid), np.float32))
 
 
 def _cloud16(xyz: np.ndarray) -> np.ndarray:
@@ -681,6 +726,20 @@ class Services:
         if rc < 0:
             raise PittError(rc, "pitt_srv_arbitrate")
         return rc
+
+    def classify_clusters(self, x, y, z, offsets, counts):
+        """clustersAcquisition's loop (ransac_segmentation.cpp:230-302) for all clusters in one pass, with
+        the parameters the four handlers read (pitt_srv_classify_clusters); as Context.classify_clusters."""
+        offsets = np.ascontiguousarray(np.asarray(offsets, np.int64))
+        counts = np.ascontiguousarray(np.asarray(counts, np.int64))
+        nc = len(counts)
+        out = (L.ClusterShape * max(nc, 1))()
+        keep = [x, y, z] if hasattr(x, "data_ptr") else [np.ascontiguousarray(a, np.float32) for a in (x, y, z)]
+        ptrs = [a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data for a in keep]
+        rc = lib.pitt_srv_classify_clusters(self.h, *ptrs, _i64(offsets), _i64(counts), nc, out)
+        if rc < 0:
+            raise PittError(rc, f"classify_clusters: {lib.pitt_last_error(self.ctx.h).decode()}")
+        return [_shape_dict(out[c]) for c in range(nc)]
 
     def find_supports(self, cloud: np.ndarray, n_normals: Optional[int] = None, **req):
         c = _cloud16(cloud)

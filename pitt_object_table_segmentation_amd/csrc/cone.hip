@@ -30,6 +30,7 @@
 #include "ctx.hpp"
 #include "device_common.hpp"
 #include "lm.hpp"
+#include "prim_ransac.hpp"
 #include "vec4.hpp"
 
 #pragma clang fp contract(off)
@@ -206,6 +207,62 @@ struct ConeResidual {
     }
 };
 
+// prim_ransac.hpp traits of the cone service
+struct ConeModelT {
+    using Coef = Coef7;
+    using Prep = ConePrep;
+    static constexpr int kSample = 3;
+    static constexpr const char* kName = "k_cone";
+    static constexpr double kModelBytes = 72.0, kCountBytes = 24.0;
+    static constexpr bool kDevicePrep = true;  // isModelValid and the model constants need device math
+    int max_iterations;
+    double probability;
+    uint32_t seed;
+    int optimize;
+    ConeCfg cfg;
+    static void to_out(const Coef7& c, float* o) {
+        for (int k = 0; k < 7; ++k) o[k] = c.c[k];
+    }
+    void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, Coef7* coef, int32_t* flag) const {
+        hipLaunchKernelGGL(k_cone_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, c.nx, c.ny,
+                           c.nz, tab, A, cfg.amin, cfg.amax, coef, flag);
+    }
+    void launch_count(hipStream_t s, const PrimCloud& c, const Coef7* coef, const int32_t* flag, int a0, int nh,
+                      int32_t* cnt) const {
+        hipLaunchKernelGGL(k_cone_count, dim3((unsigned)((c.n + 1023) / 1024), (unsigned)nh), dim3(256), 0, s, c.x,
+                           c.y, c.z, c.nx, c.ny, c.nz, c.n, coef, flag, a0, cfg, cnt);
+    }
+    void prep_host(const Coef7&, ConePrep*) const {}
+    void launch_prep(hipStream_t s, const Coef7& m, ConePrep* out) const {
+        hipLaunchKernelGGL(k_cone_prepare, dim3(1), dim3(1), 0, s, m, cfg, out);
+    }
+    static bool prep_valid(const ConePrep& p) { return p.valid != 0; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const Coef7&, const ConePrep& q, int32_t* tc, int32_t* to,
+                       int g) const {
+        ConeIn pred{c.x, c.y, c.z, c.nx, c.ny, c.nz, q.q, cfg};
+        hipLaunchKernelGGL(k_pred_count<ConeIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
+        hipLaunchKernelGGL((k_pred_apply<ConeIn, ConeWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,
+                           ConeWriteIdx{c.inliers}, c.n, to);
+    }
+    // any inliers: the refinement (fewer than 7: the model unchanged, its direction normalised)
+    static int refine_kind(int64_t n_inliers) { return n_inliers > 0 ? 1 : 0; }
+    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const Coef7& bc, int64_t n_inl,
+                      Coef7* out) const {
+        if (n_inl >= 7) return launch_lm7(ctx, s, ConeResidual{}, c.x, c.y, c.z, c.inliers, n_inl, bc, out);
+        hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
+        return PITT_OK;
+    }
+};
+
+// A batch of cone services (pitt_classify_clusters): one host synchronisation per phase.
+int cone_batch(pitt_ctx* ctx, const pitt_cone_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
+    const ConeModelT m{p->max_iterations, p->probability, p->seed, p->optimize,
+                       ConeCfg{p->normal_distance_weight, p->threshold, p->min_angle, p->max_angle, p->eps_angle,
+                               p->axis[0], p->axis[1], p->axis[2], p->eigen33}};
+    return prim_ransac_batch(ctx, m, cl, nc, res);
+}
+
 }  // namespace pitt
 
 extern "C" int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
@@ -215,139 +272,18 @@ extern "C" int pitt_cone_segment(pitt_ctx* ctx, const float* x, const float* y, 
     if (!ctx) return PITT_E_INVALID;
     if (!p || !n_inliers || !coef_out || n < 0 || (n > 0 && (!x || !y || !z || !nx || !ny || !nz || !inliers)))
         return ctx->fail(PITT_E_INVALID, "null argument");
-    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
-    if (p->max_iterations < 0 || !(p->probability > 0 && p->probability < 1))
-        return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
     *n_inliers = 0;
     if (hypotheses) *hypotheses = 0;
     for (int k = 0; k < 7; ++k) coef_out[k] = 0;
-    if (n < 3) return PITT_NO_MODEL;  // getSamples: "Can not select 3 unique points"
-    hipStream_t s = ctx->stream;
-    const ConeCfg cfg{p->normal_distance_weight, p->threshold, p->min_angle, p->max_angle, p->eps_angle,
-                      p->axis[0], p->axis[1], p->axis[2], p->eigen33};
-    const int64_t max_skip = (int64_t)p->max_iterations * 10;
-    const int64_t A = (int64_t)p->max_iterations + 1 + max_skip;
-    if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
-    const std::vector<int32_t>& tab = sampler_table(ctx, n, p->seed, A, 3);
-    int32_t* dtab = (int32_t*)ctx->buf("cone_table", (size_t)A * 12);
-    Coef7* dcoef = (Coef7*)ctx->buf("cone_coef", (size_t)A * sizeof(Coef7));
-    int32_t* dflag = (int32_t*)ctx->buf("cone_flag", (size_t)A * 4);
-    int32_t* dcnt = (int32_t*)ctx->buf("cone_cnt", (size_t)A * 4);
-    const int64_t nt = ctiles(n);
-    int32_t* tc = (int32_t*)ctx->buf("cone_tc", (size_t)(nt + 1) * 4);
-    int32_t* to = (int32_t*)ctx->buf("cone_to", (size_t)(nt + 1) * 4);
-    Coef7* dref = (Coef7*)ctx->buf("cone_ref", sizeof(Coef7));
-    ConePrep* dprep = (ConePrep*)ctx->buf("cone_prep", sizeof(ConePrep));
-    if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref || !dprep)
-        return ctx->fail(PITT_E_NOMEM, "cone scratch");
-    PITT_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), (size_t)A * 12, hipMemcpyHostToDevice, s));
-    int rec = ctx->prof_begin("k_cone_model", (double)A * 72.0);
-    hipLaunchKernelGGL(k_cone_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, x, y, z, nx, ny, nz, dtab,
-                       (int)A, p->min_angle, p->max_angle, dcoef, dflag);
-    ctx->prof_end(rec);
-    PITT_HIP_TRY(hipGetLastError());
-    std::vector<int32_t> hflag((size_t)A), hcnt;
-    PITT_HIP_TRY(hipMemcpyAsync(hflag.data(), dflag, (size_t)A * 4, hipMemcpyDeviceToHost, s));
-    PITT_HIP_TRY(hipStreamSynchronize(s));
-    // RandomSampleConsensus::computeModel replayed over chunks of device counts
-    int iterations = 0, n_best = -INT32_MAX;
-    double k = 1.0;
-    const double log_probability = std::log(1.0 - p->probability);
-    const double one_over_indices = 1.0 / (double)n;
-    int64_t skipped = 0;
-    int best = -1;
-    int64_t a = 0;
-    int chunk = 32;
-    bool done = false;
-    const int64_t ntc = (n + 1023) / 1024;
-    while (!done && a < A) {
-        const int64_t a1 = std::min<int64_t>(A, a + chunk);
-        const int nh = (int)(a1 - a);
-        PITT_HIP_TRY(hipMemsetAsync(dcnt + a, 0, (size_t)nh * 4, s));
-        rec = ctx->prof_begin("k_cone_count", (double)nh * (double)n * 24.0);
-        hipLaunchKernelGGL(k_cone_count, dim3((unsigned)ntc, (unsigned)nh), dim3(256), 0, s, x, y, z, nx, ny, nz, n,
-                           dcoef, dflag, (int)a, cfg, dcnt + a);
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        hcnt.resize((size_t)nh);
-        PITT_HIP_TRY(hipMemcpyAsync(hcnt.data(), dcnt + a, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        for (int64_t i = a; i < a1; ++i) {
-            if (!(iterations < k && skipped < max_skip)) {
-                done = true;
-                break;
-            }
-            if (hflag[(size_t)i] == 0) {
-                ++skipped;
-                continue;
-            }
-            const int n_in = hcnt[(size_t)(i - a)];
-            if (n_in > n_best) {
-                n_best = n_in;
-                best = (int)i;
-                const double w = (double)n_best * one_over_indices;
-                double p_no = 1.0 - std::pow(w, 3.0);
-                p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
-                p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
-                k = log_probability / std::log(p_no);
-            }
-            ++iterations;
-            if (iterations > p->max_iterations) {
-                done = true;
-                break;
-            }
-        }
-        a = a1;
-        chunk = std::min(chunk * 2, 256);
-    }
-    if (hypotheses) *hypotheses = iterations;
-    if (best < 0) return PITT_NO_MODEL;
-    Coef7 bc;
-    PITT_HIP_TRY(hipMemcpy(&bc, dcoef + best, sizeof bc, hipMemcpyDeviceToHost));
-    int32_t* hto = (int32_t*)ctx->pinned("cone_to_h", 16);
-    Coef7* href = (Coef7*)ctx->pinned("cone_ref_h", sizeof(Coef7));
-    ConePrep* hprep = (ConePrep*)ctx->pinned("cone_prep_h", sizeof(ConePrep));
-    if (!hto || !href || !hprep) return ctx->fail(PITT_E_NOMEM, "cone pinned");
-    const int g = grid_for_tiles(nt);
-    auto select = [&](const Coef7& m) -> int {
-        *n_inliers = 0;
-        hipLaunchKernelGGL(k_cone_prepare, dim3(1), dim3(1), 0, s, m, cfg, dprep);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hprep, dprep, sizeof(ConePrep), hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        if (!hprep->valid) return PITT_OK;
-        ConeIn pred{x, y, z, nx, ny, nz, hprep->q, cfg};
-        hipLaunchKernelGGL(k_pred_count<ConeIn>, dim3(g), dim3(kBlock), 0, s, pred, n, tc);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, nt, to);
-        hipLaunchKernelGGL((k_pred_apply<ConeIn, ConeWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,
-                           ConeWriteIdx{inliers}, n, to);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hto, to + nt, 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        *n_inliers = hto[0];
-        return PITT_OK;
-    };
-    int rc = select(bc);
+    const PrimCloud c{x, y, z, nx, ny, nz, n, inliers};
+    PrimResult r;
+    const int rc = cone_batch(ctx, p, &c, 1, &r);
     if (rc != PITT_OK) return rc;
-    Coef7 outc = bc;
-    if (p->optimize && *n_inliers > 0) {
-        if (*n_inliers >= 7) {
-            rec = ctx->prof_begin("k_cone_lm", (double)*n_inliers * 12.0);
-            const int lrc = launch_lm7(ctx, s, ConeResidual{}, x, y, z, inliers, *n_inliers, bc, dref);
-            if (lrc != PITT_OK) return lrc;
-            ctx->prof_end(rec);
-        } else {
-            hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, dref);
-        }
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(Coef7), hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        outc = *href;
-        rc = select(outc);
-        if (rc != PITT_OK) return rc;
-    }
-    for (int r = 0; r < 7; ++r) coef_out[r] = outc.c[r];
+    if (hypotheses) *hypotheses = r.hypotheses;
+    if (r.status != PITT_OK) return r.status;
+    *n_inliers = r.n_inliers;
+    for (int k = 0; k < 7; ++k) coef_out[k] = r.coef[k];
     return PITT_OK;
 }
 

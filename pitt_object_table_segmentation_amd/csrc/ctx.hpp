@@ -88,6 +88,7 @@ struct pitt_ctx {
     // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the
     // GPU, otherwise bounds the pipelined throughput.  $PITT_GRAPHS=0 disables.
     bool use_graphs = pitt_env_flag("PITT_GRAPHS", true);
+    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 64, 1, 1 << 30);  // smaller batches launch directly
     uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
     struct GraphEntry {
         std::vector<uint64_t> key;

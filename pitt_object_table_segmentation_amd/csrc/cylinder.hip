@@ -32,6 +32,7 @@
 #include "ctx.hpp"
 #include "device_common.hpp"
 #include "lm.hpp"
+#include "prim_ransac.hpp"
 #include "vec4.hpp"
 
 #pragma clang fp contract(off)
@@ -166,6 +167,67 @@ struct CylResidual {
     }
 };
 
+// prim_ransac.hpp traits of the cylinder service
+struct CylPrep {
+    int32_t valid;
+};
+struct CylModel {
+    using Coef = CylCoef;
+    using Prep = CylPrep;
+    static constexpr int kSample = 2;
+    static constexpr const char* kName = "k_cyl";
+    static constexpr double kModelBytes = 48.0, kCountBytes = 24.0;
+    static constexpr bool kDevicePrep = false;
+    int max_iterations;
+    double probability;
+    uint32_t seed;
+    int optimize;
+    double rmin, rmax, w, th;
+    int eigen33;
+    static void to_out(const CylCoef& c, float* o) {
+        for (int k = 0; k < 7; ++k) o[k] = c.c[k];
+    }
+    void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, CylCoef* coef, int32_t* flag) const {
+        hipLaunchKernelGGL(k_cyl_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, c.nx, c.ny,
+                           c.nz, tab, A, rmin, rmax, coef, flag);
+    }
+    void launch_count(hipStream_t s, const PrimCloud& c, const CylCoef* coef, const int32_t* flag, int a0, int nh,
+                      int32_t* cnt) const {
+        hipLaunchKernelGGL(k_cyl_count, dim3((unsigned)((c.n + 1023) / 1024), (unsigned)nh), dim3(256), 0, s, c.x, c.y,
+                           c.z, c.nx, c.ny, c.nz, c.n, coef, flag, a0, w, th, eigen33, rmin, rmax, cnt);
+    }
+    // selectWithinDistance: none for a model outside the radius limits
+    void prep_host(const CylCoef& m, CylPrep* p) const {
+        p->valid = !((rmin != -DBL_MAX && m.c[6] < rmin) || (rmax != DBL_MAX && m.c[6] > rmax));
+    }
+    void launch_prep(hipStream_t, const CylCoef&, CylPrep*) const {}
+    static bool prep_valid(const CylPrep& p) { return p.valid != 0; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const CylCoef& m, const CylPrep&, int32_t* tc, int32_t* to,
+                       int g) const {
+        CylIn pred{c.x, c.y, c.z, c.nx, c.ny, c.nz, m, w, th, eigen33};
+        hipLaunchKernelGGL(k_pred_count<CylIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
+        hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,
+                           CylWriteIdx{c.inliers}, c.n, to);
+    }
+    // any inliers: the least-squares refinement (7 or more: Eigen's LM refuses m < n, the model then
+    // stays and only the direction is normalised)
+    static int refine_kind(int64_t n_inliers) { return n_inliers > 0 ? 1 : 0; }
+    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const CylCoef& bc, int64_t n_inl,
+                      CylCoef* out) const {
+        if (n_inl >= 7) return launch_lm7(ctx, s, CylResidual{}, c.x, c.y, c.z, c.inliers, n_inl, bc, out);
+        hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
+        return PITT_OK;
+    }
+};
+
+// A batch of cylinder services (pitt_classify_clusters): one host synchronisation per phase.
+int cylinder_batch(pitt_ctx* ctx, const pitt_cylinder_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
+    const CylModel m{p->max_iterations, p->probability, p->seed, p->optimize, p->radius_min, p->radius_max,
+                     p->normal_distance_weight, p->threshold, (int)p->eigen33};
+    return prim_ransac_batch(ctx, m, cl, nc, res);
+}
+
 }  // namespace pitt
 
 extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, const float* nx,
@@ -175,135 +237,18 @@ extern "C" int pitt_cylinder_segment(pitt_ctx* ctx, const float* x, const float*
     if (!ctx) return PITT_E_INVALID;
     if (!p || !n_inliers || !coef_out || n < 0 || (n > 0 && (!x || !y || !z || !nx || !ny || !nz || !inliers)))
         return ctx->fail(PITT_E_INVALID, "null argument");
-    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
-    if (p->max_iterations < 0 || !(p->probability > 0 && p->probability < 1))
-        return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
     *n_inliers = 0;
     if (hypotheses) *hypotheses = 0;
     for (int k = 0; k < 7; ++k) coef_out[k] = 0;
-    if (n < 2) return PITT_NO_MODEL;  // getSamples: "Can not select 2 unique points"
-    hipStream_t s = ctx->stream;
-    const int64_t max_skip = (int64_t)p->max_iterations * 10;
-    const int64_t A = (int64_t)p->max_iterations + 1 + max_skip;
-    if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
-    const std::vector<int32_t>& tab = sampler_table(ctx, n, p->seed, A, 2);
-    int32_t* dtab = (int32_t*)ctx->buf("cyl_table", (size_t)A * 8);
-    CylCoef* dcoef = (CylCoef*)ctx->buf("cyl_coef", (size_t)A * sizeof(CylCoef));
-    int32_t* dflag = (int32_t*)ctx->buf("cyl_flag", (size_t)A * 4);
-    int32_t* dcnt = (int32_t*)ctx->buf("cyl_cnt", (size_t)A * 4);
-    const int64_t nt = ctiles(n);
-    int32_t* tc = (int32_t*)ctx->buf("cyl_tc", (size_t)(nt + 1) * 4);
-    int32_t* to = (int32_t*)ctx->buf("cyl_to", (size_t)(nt + 1) * 4);
-    CylCoef* dref = (CylCoef*)ctx->buf("cyl_ref", sizeof(CylCoef));
-    if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref) return ctx->fail(PITT_E_NOMEM, "cylinder scratch");
-    PITT_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), (size_t)A * 8, hipMemcpyHostToDevice, s));
-    int rec = ctx->prof_begin("k_cyl_model", (double)A * 48.0);
-    hipLaunchKernelGGL(k_cyl_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, x, y, z, nx, ny, nz, dtab, (int)A,
-                       p->radius_min, p->radius_max, dcoef, dflag);
-    ctx->prof_end(rec);
-    PITT_HIP_TRY(hipGetLastError());
-    std::vector<int32_t> hflag((size_t)A), hcnt;
-    PITT_HIP_TRY(hipMemcpyAsync(hflag.data(), dflag, (size_t)A * 4, hipMemcpyDeviceToHost, s));
-    PITT_HIP_TRY(hipStreamSynchronize(s));
-    int iterations = 0, n_best = -INT32_MAX;
-    double k = 1.0;
-    const double log_probability = std::log(1.0 - p->probability);
-    const double one_over_indices = 1.0 / (double)n;
-    int64_t skipped = 0;
-    int best = -1;
-    int64_t a = 0;
-    int chunk = 32;
-    bool done = false;
-    const int64_t ntc = (n + 1023) / 1024;
-    while (!done && a < A) {
-        const int64_t a1 = std::min<int64_t>(A, a + chunk);
-        const int nh = (int)(a1 - a);
-        PITT_HIP_TRY(hipMemsetAsync(dcnt + a, 0, (size_t)nh * 4, s));
-        rec = ctx->prof_begin("k_cyl_count", (double)nh * (double)n * 24.0);
-        hipLaunchKernelGGL(k_cyl_count, dim3((unsigned)ntc, (unsigned)nh), dim3(256), 0, s, x, y, z, nx, ny, nz, n, dcoef,
-                           dflag, (int)a, p->normal_distance_weight, p->threshold, (int)p->eigen33, p->radius_min,
-                           p->radius_max,
-                           dcnt + a);
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        hcnt.resize((size_t)nh);
-        PITT_HIP_TRY(hipMemcpyAsync(hcnt.data(), dcnt + a, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        for (int64_t i = a; i < a1; ++i) {
-            if (!(iterations < k && skipped < max_skip)) {
-                done = true;
-                break;
-            }
-            if (hflag[(size_t)i] == 0) {
-                ++skipped;
-                continue;
-            }
-            const int n_in = hcnt[(size_t)(i - a)];
-            if (n_in > n_best) {
-                n_best = n_in;
-                best = (int)i;
-                const double w = (double)n_best * one_over_indices;
-                double p_no = 1.0 - std::pow(w, 2.0);
-                p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
-                p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
-                k = log_probability / std::log(p_no);
-            }
-            ++iterations;
-            if (iterations > p->max_iterations) {
-                done = true;
-                break;
-            }
-        }
-        a = a1;
-        chunk = std::min(chunk * 2, 256);
-    }
-    if (hypotheses) *hypotheses = iterations;
-    if (best < 0) return PITT_NO_MODEL;
-    CylCoef bc;
-    PITT_HIP_TRY(hipMemcpy(&bc, dcoef + best, sizeof bc, hipMemcpyDeviceToHost));
-    int32_t* hto = (int32_t*)ctx->pinned("cyl_to_h", 16);
-    CylCoef* href = (CylCoef*)ctx->pinned("cyl_ref_h", sizeof(CylCoef));
-    if (!hto || !href) return ctx->fail(PITT_E_NOMEM, "cylinder pinned");
-    const int g = grid_for_tiles(nt);
-    auto select = [&](const CylCoef& m) -> int {
-        const bool valid = !((p->radius_min != -DBL_MAX && m.c[6] < p->radius_min) ||
-                             (p->radius_max != DBL_MAX && m.c[6] > p->radius_max));
-        if (!valid) {
-            *n_inliers = 0;
-            return PITT_OK;
-        }
-        CylIn pred{x, y, z, nx, ny, nz, m, p->normal_distance_weight, p->threshold, (int)p->eigen33};
-        hipLaunchKernelGGL(k_pred_count<CylIn>, dim3(g), dim3(kBlock), 0, s, pred, n, tc);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, nt, to);
-        hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, CylWriteIdx{inliers}, n,
-                           to);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hto, to + nt, 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        *n_inliers = hto[0];
-        return PITT_OK;
-    };
-    int rc = select(bc);
+    const PrimCloud c{x, y, z, nx, ny, nz, n, inliers};
+    PrimResult r;
+    const int rc = cylinder_batch(ctx, p, &c, 1, &r);
     if (rc != PITT_OK) return rc;
-    CylCoef outc = bc;
-    if (p->optimize && *n_inliers > 0) {
-        rec = ctx->prof_begin("k_cyl_lm", (double)*n_inliers * 12.0);
-        if (*n_inliers >= 7) {
-            const int lrc = launch_lm7(ctx, s, CylResidual{}, x, y, z, inliers, *n_inliers, bc, dref);
-            if (lrc != PITT_OK) return lrc;
-        } else {  // Eigen's LM refuses m < n: the model stays, the direction is normalised
-            hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, dref);
-        }
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(href, dref, sizeof(CylCoef), hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        outc = *href;
-        rc = select(outc);
-        if (rc != PITT_OK) return rc;
-    }
-    for (int r = 0; r < 7; ++r) coef_out[r] = outc.c[r];
+    if (hypotheses) *hypotheses = r.hypotheses;
+    if (r.status != PITT_OK) return r.status;
+    *n_inliers = r.n_inliers;
+    for (int k = 0; k < 7; ++k) coef_out[k] = r.coef[k];
     return PITT_OK;
 }
 

@@ -481,6 +481,147 @@ static int normals_impl(pitt_ctx* ctx, const float* x, const float* y, const flo
     return PITT_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// A batch of small clouds (a frame's clusters, pitt_classify_clusters): PCManager::estimateNormal on
+// each cluster on its own, all clusters in one pass.  The k nearest finite points of a query are taken
+// from its own cluster by exhaustive search (the same candidates, distances, nn_select and final
+// (distance, index) sort as k_knn: identical lists), so no per-cluster grid set-up and no host round
+// trip.  Clusters of more than kSegBrute points go through normals_impl one by one.
+constexpr int64_t kSegBrute = 16384;
+
+__global__ void k_seg_finite(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+                             const int64_t* __restrict__ off, const int64_t* __restrict__ cnt, int k,
+                             int32_t* __restrict__ kk) {
+    const int c = blockIdx.x;
+    __shared__ int part[kBlock / 64];
+    int f = 0;
+    for (int64_t i = threadIdx.x; i < cnt[c]; i += kBlock) {
+        const int64_t j = off[c] + i;
+        f += fin3(X[j], Y[j], Z[j]) ? 1 : 0;
+    }
+    f = wave_sum_i(f);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+        kk[c] = t < k ? t : k;
+    }
+}
+
+// one wave per query; queries numbered over the clusters (qpre: exclusive prefix of the counts)
+template <int KMAX>
+__global__ __launch_bounds__(64 * kNnWaves) void k_knn_seg(const float* __restrict__ X, const float* __restrict__ Y,
+                                                           const float* __restrict__ Z, const int64_t* __restrict__ off,
+                                                           const int64_t* __restrict__ cnt,
+                                                           const int64_t* __restrict__ qpre, int nc,
+                                                           const int32_t* __restrict__ kks, int k,
+                                                           int32_t* __restrict__ nn, int32_t* __restrict__ nn_cnt) {
+    __shared__ uint32_t s_d[kNnWaves][kNnCap];
+    __shared__ int32_t s_i[kNnWaves][kNnCap];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    uint32_t* bd = s_d[w];
+    int32_t* bi = s_i[w];
+    const int64_t total = qpre[nc];
+    for (int64_t qi = (int64_t)blockIdx.x * kNnWaves + w; qi < total; qi += (int64_t)gridDim.x * kNnWaves) {
+        int lo = 0, hi = nc - 1;  // the cluster: last c with qpre[c] <= qi
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (qpre[mid] <= qi) lo = mid;
+            else hi = mid - 1;
+        }
+        const int c = lo;
+        const int64_t base = off[c], n = cnt[c];
+        const int64_t q = base + (qi - qpre[c]);
+        const int kk = kks[c];
+        const float qx = X[q], qy = Y[q], qz = Z[q];
+        if (n > kSegBrute || !fin3(qx, qy, qz) || kk < 1) {  // large clusters: normals_impl
+            if (lane == 0 && n <= kSegBrute) nn_cnt[q] = 0;
+            continue;
+        }
+        int fill = 0;
+        for (int64_t t0 = 0; t0 < n; t0 += 64) {
+            if (fill + 64 > kNnCap) fill = nn_select(bd, bi, fill, kk, lane);
+            const int64_t t = t0 + lane;
+            bool ok = false;
+            float d2 = 0.0f;
+            if (t < n) {
+                const float px = X[base + t], py = Y[base + t], pz = Z[base + t];
+                ok = fin3(px, py, pz);
+                const float dx = qx - px, dy = qy - py, dz = qz - pz;
+                d2 = (dx * dx + dy * dy) + dz * dz;  // FLANN L2_Simple
+            }
+            const uint64_t b = __builtin_amdgcn_ballot_w64(ok);
+            const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            if (ok) {
+                bd[fill + pre] = __float_as_uint(d2);
+                bi[fill + pre] = (int32_t)(base + t);
+            }
+            fill += __builtin_popcountll(b);
+        }
+        fill = nn_select(bd, bi, fill, kk, lane);
+        uint64_t key = lane < fill ? ((uint64_t)bd[lane] << 32) | (uint32_t)bi[lane] : ~0ull;
+#pragma unroll
+        for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const uint32_t plo = __shfl_xor((uint32_t)key, stride, 64);
+                const uint32_t phi = __shfl_xor((uint32_t)(key >> 32), stride, 64);
+                const uint64_t p = ((uint64_t)phi << 32) | plo;
+                const bool up = (lane & size) == 0 || size == 64;
+                const bool lower = (lane & stride) == 0;
+                key = (lower == up) ? (key < p ? key : p) : (key > p ? key : p);
+            }
+        }
+        if (lane < fill) nn[q * k + lane] = (int32_t)(uint32_t)key;
+        if (lane == 0) nn_cnt[q] = fill;
+    }
+}
+
+// Normals of nc clusters laid out in one device SoA of n_total points (cluster c at off[c], cnt[c]
+// points; other points are never neighbours and get no normal written).  off / cnt: host arrays.
+int normals_batch(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n_total, const int64_t* off,
+                  const int64_t* cnt, int nc, int k, const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+    hipStream_t s = ctx->stream;
+    if (nc == 0 || n_total == 0) return PITT_OK;
+    if (k < 1 || k > kNnMaxK) return ctx->fail(PITT_E_INVALID, "k must be in [1, 64]");
+    int64_t* dm = (int64_t*)ctx->buf("nrmb_meta", (size_t)(3 * nc + 1) * 8);
+    int64_t* hm = (int64_t*)ctx->pinned("nrmb_meta_h", (size_t)(3 * nc + 1) * 8);
+    int32_t* kk = (int32_t*)ctx->buf("nrmb_kk", (size_t)nc * 4);
+    int32_t* nnd = (int32_t*)ctx->buf("nrmb_nn", (size_t)n_total * k * 4);
+    int32_t* cntd = (int32_t*)ctx->buf("nrmb_cnt", (size_t)n_total * 4);
+    if (!dm || !hm || !kk || !nnd || !cntd) return ctx->fail(PITT_E_NOMEM, "batched normals scratch");
+    for (int c = 0; c < nc; ++c) {
+        hm[c] = off[c];
+        hm[nc + c] = cnt[c];
+    }
+    hm[2 * nc] = 0;
+    for (int c = 0; c < nc; ++c) hm[2 * nc + c + 1] = hm[2 * nc + c] + cnt[c];
+    PITT_HIP_TRY(hipMemcpyAsync(dm, hm, (size_t)(3 * nc + 1) * 8, hipMemcpyHostToDevice, s));
+    PITT_HIP_TRY(hipMemsetAsync(cntd, 0, (size_t)n_total * 4, s));
+    int rec = ctx->prof_begin("k_knn_seg", (double)hm[3 * nc] * (12.0 + 4.0 * k));
+    hipLaunchKernelGGL(k_seg_finite, dim3(nc), dim3(kBlock), 0, s, x, y, z, dm, dm + nc, k, kk);
+    const int kb = (int)std::max<int64_t>(1, std::min<int64_t>((hm[3 * nc] + kNnWaves - 1) / kNnWaves, 65536));
+    hipLaunchKernelGGL(k_knn_seg<kNnMaxK>, dim3(kb), dim3(64 * kNnWaves), 0, s, x, y, z, dm, dm + nc, dm + 2 * nc, nc,
+                       kk, k, nnd, cntd);
+    ctx->prof_end(rec);
+    PITT_HIP_TRY(hipGetLastError());
+    rec = ctx->prof_begin("k_normals", (double)n_total * 28.0);
+    hipLaunchKernelGGL(k_normals, dim3(std::max<int64_t>(1, std::min<int64_t>((n_total + kBlock - 1) / kBlock, 8192))),
+                       dim3(kBlock), 0, s, x, y, z, n_total, nnd, cntd, k, vp[0], vp[1], vp[2], nx, ny, nz, curv);
+    ctx->prof_end(rec);
+    PITT_HIP_TRY(hipGetLastError());
+    // large clusters: the grid path, one at a time
+    for (int c = 0; c < nc; ++c) {
+        if (cnt[c] <= kSegBrute) continue;
+        const int rc = normals_impl(ctx, x + off[c], y + off[c], z + off[c], cnt[c], k, vp, nx + off[c], ny + off[c],
+                                    nz + off[c], curv + off[c], nullptr, nullptr);
+        if (rc != PITT_OK) return rc;
+    }
+    return PITT_OK;
+}
+
 }  // namespace pitt
 
 extern "C" int pitt_normal_estimation(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

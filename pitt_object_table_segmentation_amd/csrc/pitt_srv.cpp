@@ -60,9 +60,10 @@ void to_soa(const pitt_msgs::PointCloud& c, std::vector<float>& x, std::vector<f
 }
 }  // namespace
 
-// plane_segmentation_srv.cpp:27-74
-bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
-                                                pitt_msgs::PrimitiveSegmentation::Response& res) {
+// The parameter reads of the four primitive handlers (each service reads its own on every call).
+// plane_segmentation_srv.cpp:27-74 (the normal weight, eps and opening angles do not reach
+// SACMODEL_PLANE, A1)
+pitt_sac_params SegmentationServices::planeParams() {
     int maxIterations;
     double normalDistanceWeight, distanceThreshold, epsAngleTh, minOpeningAngle, maxOpeningAngle;
     params_.param(srvm::PARAM_NAME_PLANE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
@@ -77,6 +78,99 @@ bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation
     pitt_sac_params_default(&p);
     p.threshold = distanceThreshold;
     p.max_iterations = maxIterations;
+    return p;
+}
+
+// cylinder_segmentation_srv.cpp:82-126
+pitt_cylinder_params SegmentationServices::cylinderParams() {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
+        maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_CYLINDER_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
+    params_.param(srvm::PARAM_NAME_CYLINDER_DISTANCE_TH, distanceThreshold, 0.008);
+    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_CYLINDER_MIN_RADIUS_LIMIT, minRadiusLimit, 0.005);
+    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
+    params_.param(srvm::PARAM_NAME_CYLINDER_EPS_ANGLE_TH, epsAngleTh, 0.0001);
+    params_.param(srvm::PARAM_NAME_CYLINDER_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 50.0);
+    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 180.0);
+    (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;
+
+    pitt_cylinder_params p;
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    p.optimize = 1;
+    p.probability = 0.99;
+    p.radius_min = minRadiusLimit;
+    p.radius_max = maxRadiusLimit;
+    p.normal_distance_weight = normalDistanceWeight;
+    p.seed = 12345u;
+    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain, SURVEY s8c)
+    return p;
+}
+
+// cone_segmentation_srv.cpp:83-127
+pitt_cone_params SegmentationServices::coneParams() {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
+        maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_CONE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.0006);
+    params_.param(srvm::PARAM_NAME_CONE_DISTANCE_TH, distanceThreshold, 0.0055);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_CONE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.001);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
+    params_.param(srvm::PARAM_NAME_CONE_EPS_ANGLE_TH, epsAngleTh, 0.4);
+    params_.param(srvm::PARAM_NAME_CONE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 10.0);
+    params_.param(srvm::PARAM_NAME_CONE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 170.0);
+    (void)minRadiusLimit; (void)maxRadiusLimit;
+
+    pitt_cone_params p;
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    p.optimize = 1;
+    p.probability = 0.99;
+    p.normal_distance_weight = normalDistanceWeight;
+    p.min_angle = minOpeningAngle / 180.0 * M_PI;
+    p.max_angle = maxOpeningAngle / 180.0 * M_PI;
+    p.eps_angle = epsAngleTh;
+    p.axis[0] = p.axis[1] = p.axis[2] = 0.0f;
+    p.seed = 12345u;
+    p.pad = 0;
+    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain, SURVEY s8c)
+    return p;
+}
+
+// sphere_segmentation_srv.cpp:29-73
+pitt_sphere_params SegmentationServices::sphereParams() {
+    int maxIterations;
+    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
+        maxOpeningAngle;
+    params_.param(srvm::PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
+    params_.param(srvm::PARAM_NAME_SPHERE_DISTANCE_TH, distanceThreshold, 0.007);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT, maxIterations, 1000);
+    params_.param(srvm::PARAM_NAME_SPHERE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.005);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
+    params_.param(srvm::PARAM_NAME_SPHERE_EPS_ANGLE_TH, epsAngleTh, 0.0);
+    params_.param(srvm::PARAM_NAME_SPHERE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 100.0);
+    params_.param(srvm::PARAM_NAME_SPHERE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 180.0);
+    (void)normalDistanceWeight; (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;
+
+    pitt_sphere_params p;
+    p.threshold = distanceThreshold;
+    p.max_iterations = maxIterations;
+    p.optimize = 1;
+    p.probability = 0.99;
+    p.radius_min = minRadiusLimit;
+    p.radius_max = maxRadiusLimit;
+    p.seed = 12345u;
+    p.pad = 0;
+    return p;
+}
+
+// plane_segmentation_srv.cpp:27-74
+bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
+                                                pitt_msgs::PrimitiveSegmentation::Response& res) {
+    const pitt_sac_params p = planeParams();
     std::vector<int32_t> inl(req.cloud.size());
     int64_t n_inl = 0;
     float coef[4] = {0, 0, 0, 0};
@@ -103,29 +197,7 @@ bool SegmentationServices::ransacPlaneDetaction(pitt_msgs::PrimitiveSegmentation
 // the height (pushed after the 7 coefficients) and the centroid (:129-200).
 bool SegmentationServices::ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
                                                    pitt_msgs::PrimitiveSegmentation::Response& res) {
-    int maxIterations;
-    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
-        maxOpeningAngle;
-    params_.param(srvm::PARAM_NAME_CYLINDER_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
-    params_.param(srvm::PARAM_NAME_CYLINDER_DISTANCE_TH, distanceThreshold, 0.008);
-    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_ITERATION_LIMIT, maxIterations, 1000);
-    params_.param(srvm::PARAM_NAME_CYLINDER_MIN_RADIUS_LIMIT, minRadiusLimit, 0.005);
-    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
-    params_.param(srvm::PARAM_NAME_CYLINDER_EPS_ANGLE_TH, epsAngleTh, 0.0001);
-    params_.param(srvm::PARAM_NAME_CYLINDER_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 50.0);
-    params_.param(srvm::PARAM_NAME_CYLINDER_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 180.0);
-    (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;
-
-    pitt_cylinder_params p;
-    p.threshold = distanceThreshold;
-    p.max_iterations = maxIterations;
-    p.optimize = 1;
-    p.probability = 0.99;
-    p.radius_min = minRadiusLimit;
-    p.radius_max = maxRadiusLimit;
-    p.normal_distance_weight = normalDistanceWeight;
-    p.seed = 12345u;
-    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain, SURVEY s8c)
+    const pitt_cylinder_params p = cylinderParams();
     const size_t n = req.cloud.size();
     std::vector<int32_t> inl(n + 1);
     int64_t n_inl = 0;
@@ -168,32 +240,7 @@ bool SegmentationServices::ransacCylinderDetaction(pitt_msgs::PrimitiveSegmentat
 // the 7 coefficients) and the centroid, apex + 3/4 height along the unit axis (:129-200).
 bool SegmentationServices::ransacConeDetaction(pitt_msgs::PrimitiveSegmentation::Request& req,
                                                    pitt_msgs::PrimitiveSegmentation::Response& res) {
-    int maxIterations;
-    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
-        maxOpeningAngle;
-    params_.param(srvm::PARAM_NAME_CONE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.0006);
-    params_.param(srvm::PARAM_NAME_CONE_DISTANCE_TH, distanceThreshold, 0.0055);
-    params_.param(srvm::PARAM_NAME_CONE_MAX_ITERATION_LIMIT, maxIterations, 1000);
-    params_.param(srvm::PARAM_NAME_CONE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.001);
-    params_.param(srvm::PARAM_NAME_CONE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
-    params_.param(srvm::PARAM_NAME_CONE_EPS_ANGLE_TH, epsAngleTh, 0.4);
-    params_.param(srvm::PARAM_NAME_CONE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 10.0);
-    params_.param(srvm::PARAM_NAME_CONE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 170.0);
-    (void)minRadiusLimit; (void)maxRadiusLimit;
-
-    pitt_cone_params p;
-    p.threshold = distanceThreshold;
-    p.max_iterations = maxIterations;
-    p.optimize = 1;
-    p.probability = 0.99;
-    p.normal_distance_weight = normalDistanceWeight;
-    p.min_angle = minOpeningAngle / 180.0 * M_PI;
-    p.max_angle = maxOpeningAngle / 180.0 * M_PI;
-    p.eps_angle = epsAngleTh;
-    p.axis[0] = p.axis[1] = p.axis[2] = 0.0f;
-    p.eigen33 = 0;
-    p.seed = 12345u;
-    p.eigen33 = 0;  // Eigen 3.2 (the reference's ROS Indigo toolchain, SURVEY s8c)
+    const pitt_cone_params p = coneParams();
     const size_t n = req.cloud.size();
     std::vector<int32_t> inl(n + 1);
     int64_t n_inl = 0;
@@ -234,28 +281,7 @@ bool SegmentationServices::ransacConeDetaction(pitt_msgs::PrimitiveSegmentation:
 // the plain sphere model: the normal weight, eps angle and opening angles are read but unused.
 bool SegmentationServices::ransacSphereDetection(pitt_msgs::PrimitiveSegmentation::Request& req,
                                                  pitt_msgs::PrimitiveSegmentation::Response& res) {
-    int maxIterations;
-    double normalDistanceWeight, distanceThreshold, minRadiusLimit, maxRadiusLimit, epsAngleTh, minOpeningAngle,
-        maxOpeningAngle;
-    params_.param(srvm::PARAM_NAME_SPHERE_NORMAL_DISTANCE_WEIGHT, normalDistanceWeight, 0.001);
-    params_.param(srvm::PARAM_NAME_SPHERE_DISTANCE_TH, distanceThreshold, 0.007);
-    params_.param(srvm::PARAM_NAME_SPHERE_MAX_ITERATION_LIMIT, maxIterations, 1000);
-    params_.param(srvm::PARAM_NAME_SPHERE_MIN_RADIUS_LIMIT, minRadiusLimit, 0.005);
-    params_.param(srvm::PARAM_NAME_SPHERE_MAX_RADIUS_LIMIT, maxRadiusLimit, 0.500);
-    params_.param(srvm::PARAM_NAME_SPHERE_EPS_ANGLE_TH, epsAngleTh, 0.0);
-    params_.param(srvm::PARAM_NAME_SPHERE_MIN_OPENING_ANGLE_DEGREE, minOpeningAngle, 100.0);
-    params_.param(srvm::PARAM_NAME_SPHERE_MAX_OPENING_ANGLE_DEGREE, maxOpeningAngle, 180.0);
-    (void)normalDistanceWeight; (void)epsAngleTh; (void)minOpeningAngle; (void)maxOpeningAngle;
-
-    pitt_sphere_params p;
-    p.threshold = distanceThreshold;
-    p.max_iterations = maxIterations;
-    p.optimize = 1;
-    p.probability = 0.99;
-    p.radius_min = minRadiusLimit;
-    p.radius_max = maxRadiusLimit;
-    p.seed = 12345u;
-    p.pad = 0;
+    const pitt_sphere_params p = sphereParams();
     std::vector<int32_t> inl(req.cloud.size() + 1);
     int64_t n_inl = 0;
     float coef[4] = {0, 0, 0, 0};
@@ -400,6 +426,21 @@ bool SegmentationServices::callRansacPlaneSegmentation(const pitt_msgs::PointClo
         }
     }
     return false;
+}
+
+// clustersAcquisition's per-cluster loop (ransac_segmentation.cpp:230-302) for all clusters at once:
+// the four services with the parameters their handlers read, normals with k = 50 (pc_manager.cpp:18).
+int SegmentationServices::classifyClusters(const float* x, const float* y, const float* z, const int64_t* offsets,
+                                           const int64_t* counts, int32_t n, pitt_cluster_shape* out) {
+    pitt_classify_params prm;
+    pitt_classify_params_default(&prm);
+    prm.plane = planeParams();
+    prm.sphere = sphereParams();
+    prm.cylinder = cylinderParams();
+    prm.cone = coneParams();
+    prm.cone_over_cylinder = DEFAULT_CONE_OVER_CYLINDER_PRIORITY;
+    status_ = pitt_classify_clusters(ctx_, x, y, z, offsets, counts, n, &prm, out);
+    return status_;
 }
 
 // ransac_segmentation.cpp:265-302.  size_t counts as the reference's; the cone rule compares
@@ -605,6 +646,12 @@ int pitt_srv_call_ransac_plane(pitt_srv* s, const float* xyz16, int64_t n, int64
     if (ok && coefficients_out && !out.response.coefficients.empty())
         std::memcpy(coefficients_out, out.response.coefficients.data(), out.response.coefficients.size() * 4);
     return ok ? 1 : 0;
+}
+
+int pitt_srv_classify_clusters(pitt_srv* s, const float* x, const float* y, const float* z, const int64_t* offsets,
+                               const int64_t* counts, int32_t n_clusters, pitt_cluster_shape* out) {
+    if (!s) return PITT_E_INVALID;
+    return s->svc.classifyClusters(x, y, z, offsets, counts, n_clusters, out);
 }
 
 int pitt_srv_arbitrate(int64_t sphere_inliers, int64_t cylinder_inliers, int64_t cone_inliers, int64_t plane_inliers) {

@@ -1825,7 +1825,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     return PITT_OK;
     };
-    if (ctx->use_graphs && !ctx->prof && sm != nullptr) {
+    // Graphs only for the pipelined batch layouts (enough frames that the enqueue cost matters).  A
+    // replayed one-frame graph interleaved with the primitive services' direct launches on the same
+    // stream faulted (tests/test_classify_gpu.py under pytest, not reproduced in isolation; DESIGN.md
+    // s6), so service-sized batches always launch directly.
+    if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
         const double log_prob_k = std::log(1.0 - p->probability);
         uint64_t thb = 0, lpb = 0;
         std::memcpy(&thb, &thf, sizeof thf);

@@ -238,6 +238,242 @@ __global__ void k_axis_final(const float* __restrict__ qx, const float* __restri
     *out = o;
 }
 
+// ------------------------------------------------------------------------------------------
+// A batch of axis-height jobs (pitt_classify_clusters: the cylinder and cone services' post-processing
+// for every cluster with a model), the same kernels' arithmetic with a job index, no host round trip
+// until the results: the smallest s whose sqrt is the height (s_lo) is found on the device.
+struct AxisJob {
+    AxisGeo G;
+    int64_t off;   // the job's points in the SoA
+    int64_t qoff;  // its projected copy in the scratch (jobs may share points: a cylinder and a cone)
+    int64_t n;
+    int64_t tp0;   // the job's first tile pair in the tile-maximum array
+    int32_t mode;
+    int32_t pad;
+};
+struct AxisWork {
+    uint32_t smax_bits;  // largest s + 1 (0: no pair)
+    float s_lo;
+    unsigned long long first;
+};
+
+__global__ __launch_bounds__(256) void k_axis_project_b(const float* __restrict__ X, const float* __restrict__ Y,
+                                                        const float* __restrict__ Z, const AxisJob* __restrict__ jobs,
+                                                        float* __restrict__ qx, float* __restrict__ qy,
+                                                        float* __restrict__ qz) {
+    const AxisJob& J = jobs[blockIdx.y];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = J.off + i, q = J.qoff + i;
+        const float vx = X[k] - J.G.a1[0], vy = Y[k] - J.G.a1[1], vz = Z[k] - J.G.a1[2];
+        const float g = (vx * J.G.u[0] + vy * J.G.u[1] + vz * J.G.u[2]) / J.G.gdiv;
+        qx[q] = J.G.a1[0] + g * J.G.u[0];
+        qy[q] = J.G.a1[1] + g * J.G.u[1];
+        qz[q] = J.G.a1[2] + g * J.G.u[2];
+    }
+}
+
+// k_pair_scan over job blockIdx.y's tile pairs (blocks past its count return)
+template <bool FIRST>
+__global__ __launch_bounds__(kPairTile) void k_pair_scan_b(const float* __restrict__ qx, const float* __restrict__ qy,
+                                                           const float* __restrict__ qz,
+                                                           const AxisJob* __restrict__ jobs, AxisWork* __restrict__ work,
+                                                           float* __restrict__ tile_max_all) {
+    __shared__ float4 jq[kPairTile];
+    __shared__ float red[kPairTile / 64];
+    __shared__ unsigned long long redk[kPairTile / 64];
+    const AxisJob& J = jobs[blockIdx.y];
+    AxisWork* w = work + blockIdx.y;
+    const int64_t n = J.n;
+    const int64_t tiles = (n + kPairTile - 1) / kPairTile;
+    if ((int64_t)blockIdx.x >= tiles * (tiles + 1) / 2) return;
+    float* tile_max = tile_max_all + J.tp0;
+    if (FIRST && !(w->smax_bits && tile_max[blockIdx.x] >= w->s_lo)) return;
+    const float* px = qx + J.qoff;
+    const float* py = qy + J.qoff;
+    const float* pz = qz + J.qoff;
+    int ti, tj;
+    pair_tile(blockIdx.x, ti, tj);
+    const int64_t j0 = (int64_t)tj * kPairTile;
+    const int t = threadIdx.x;
+    if (j0 + t < n) jq[t] = make_float4(px[j0 + t], py[j0 + t], pz[j0 + t], 0.0f);
+    __syncthreads();
+    const int64_t i = (int64_t)ti * kPairTile + t;
+    const int jn = (int)std::min<int64_t>(kPairTile, std::min<int64_t>(n - j0, i - j0));
+    float best = -1.0f;
+    unsigned long long key = ~0ull;
+    if (i < n && jn > 0) {
+        const float xi = px[i], yi = py[i], zi = pz[i];
+        if constexpr (!FIRST) {
+            for (int j = 0; j < jn; ++j) {
+                const float4 q = jq[j];
+                best = vmaxf(best, pair_s(xi, yi, zi, q.x, q.y, q.z));
+            }
+        } else {
+            const float s_lo = w->s_lo;
+            for (int j = 0; j < jn; ++j) {
+                const float4 q = jq[j];
+                if (pair_s(xi, yi, zi, q.x, q.y, q.z) >= s_lo) {
+                    key = (unsigned long long)i * (unsigned long long)n + (unsigned long long)(j0 + j);
+                    break;
+                }
+            }
+        }
+    }
+    const int lane = t & 63, wv = t >> 6;
+    if constexpr (!FIRST) {
+        for (int o = 32; o > 0; o >>= 1) best = vmaxf(best, __shfl_xor(best, o, 64));
+        if (lane == 0) red[wv] = best;
+        __syncthreads();
+        if (t == 0) {
+            float m = red[0];
+            for (int k = 1; k < kPairTile / 64; ++k) m = vmaxf(m, red[k]);
+            tile_max[blockIdx.x] = m;
+            if (m >= 0.0f) atomicMax(&w->smax_bits, __float_as_uint(m) + 1u);
+        }
+    } else {
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(key, o, 64);
+            key = v < key ? v : key;
+        }
+        if (lane == 0) redk[wv] = key;
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long m = redk[0];
+            for (int k = 1; k < kPairTile / 64; ++k) m = redk[k] < m ? redk[k] : m;
+            if (m != ~0ull) atomicMin(&w->first, m);
+        }
+    }
+}
+
+// per job: smax = 0, first = ~0; then s_lo, the smallest float whose (correctly rounded) sqrt is the
+// height (a positive float's next value towards zero is its bit pattern minus one)
+__global__ void k_axis_init_b(AxisWork* __restrict__ work, int nj) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nj) work[j] = AxisWork{0u, 0.0f, ~0ull};
+}
+__global__ void k_axis_slo_b(AxisWork* __restrict__ work, int nj) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nj || !work[j].smax_bits) return;
+    const float smax = __uint_as_float(work[j].smax_bits - 1u);
+    const float hgt = sqrtf(smax);
+    float lo = smax;
+    while (lo > 0.0f && sqrtf(__uint_as_float(__float_as_uint(lo) - 1u)) == hgt) lo = __uint_as_float(__float_as_uint(lo) - 1u);
+    work[j].s_lo = lo;
+}
+
+__global__ void k_axis_final_b(const float* __restrict__ qx, const float* __restrict__ qy, const float* __restrict__ qz,
+                               const AxisJob* __restrict__ jobs, const AxisWork* __restrict__ work, int nj,
+                               AxisOut* __restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nj) return;
+    const AxisJob& J = jobs[j];
+    const AxisWork& w = work[j];
+    AxisOut o;
+    o.height = -1.0f;
+    o.idx1 = o.idx2 = -1;
+    if (w.smax_bits) {
+        o.height = sqrtf(__uint_as_float(w.smax_bits - 1u));
+        o.idx1 = (int32_t)(w.first / (unsigned long long)J.n);
+        o.idx2 = (int32_t)(w.first % (unsigned long long)J.n);
+    }
+    if (J.mode == PITT_AXIS_CYLINDER) {
+        const float nan = __builtin_nanf("");
+        const bool ok = o.idx1 >= 0;
+        const int64_t a = J.qoff + o.idx1, b = J.qoff + o.idx2;
+        o.centroid[0] = ok ? (qx[a] + qx[b]) / 2 : nan;
+        o.centroid[1] = ok ? (qy[a] + qy[b]) / 2 : nan;
+        o.centroid[2] = ok ? (qz[a] + qz[b]) / 2 : nan;
+    } else {
+        o.centroid[0] = J.G.c[0] + 3.0f / 4.0f * o.height * J.G.d[0];
+        o.centroid[1] = J.G.c[1] + 3.0f / 4.0f * o.height * J.G.d[1];
+        o.centroid[2] = J.G.c[2] + 3.0f / 4.0f * o.height * J.G.d[2];
+    }
+    out[j] = o;
+}
+
+// the axis geometry, host float arithmetic in the reference's order (:53-79, :143-144)
+static AxisGeo axis_geo(const float coef[6]) {
+    AxisGeo G;
+    const float norm = std::sqrt(coef[3] * coef[3] + coef[4] * coef[4] + coef[5] * coef[5]);
+    for (int k = 0; k < 3; ++k) {
+        G.c[k] = coef[k];
+        G.d[k] = coef[3 + k] / norm;
+        G.a1[k] = coef[k] + G.d[k] * -1.0f;
+    }
+    for (int k = 0; k < 3; ++k) G.u[k] = (coef[k] + G.d[k] * 1.0f) - G.a1[k];
+    G.gdiv = G.u[0] * G.u[0] + G.u[1] * G.u[1] + G.u[2] * G.u[2];
+    return G;
+}
+
+// Jobs over one device SoA of n_total points: job j = points [off[j], off[j] + n[j]), model coef6[j]
+// (6 floats, host), mode[j].  Outputs (host): height, idx1, idx2, centroid per job.  One host sync.
+int axis_height_batch(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n_total,
+                      const int64_t* off, const int64_t* n, const float* coef6, const int32_t* mode, int nj,
+                      float* height, int32_t* idx1, int32_t* idx2, float* centroid3) {
+    if (nj == 0) return PITT_OK;
+    hipStream_t s = ctx->stream;
+    AxisJob* hj = (AxisJob*)ctx->pinned("axb_jobs_h", (size_t)nj * sizeof(AxisJob));
+    AxisOut* ho = (AxisOut*)ctx->pinned("axb_out_h", (size_t)nj * sizeof(AxisOut));
+    AxisJob* dj = (AxisJob*)ctx->buf("axb_jobs", (size_t)nj * sizeof(AxisJob));
+    AxisWork* dw = (AxisWork*)ctx->buf("axb_work", (size_t)nj * sizeof(AxisWork));
+    AxisOut* dout = (AxisOut*)ctx->buf("axb_out", (size_t)nj * sizeof(AxisOut));
+    int64_t q_total = 0;
+    for (int j = 0; j < nj; ++j) q_total += n[j];
+    const size_t nb = (size_t)std::max<int64_t>(q_total, 1) * 4;
+    float* qx = (float*)ctx->buf("axb_qx", nb);
+    float* qy = (float*)ctx->buf("axb_qy", nb);
+    float* qz = (float*)ctx->buf("axb_qz", nb);
+    if (!hj || !ho || !dj || !dw || !dout || !qx || !qy || !qz) return ctx->fail(PITT_E_NOMEM, "axis batch scratch");
+    int64_t tp_total = 0, tp_max = 0, n_max = 0, qo = 0;
+    for (int j = 0; j < nj; ++j) {
+        if (n[j] > 0x7fffffff || off[j] < 0 || off[j] + n[j] > n_total)
+            return ctx->fail(PITT_E_INVALID, "axis height job out of range");
+        hj[j].G = axis_geo(coef6 + 6 * j);
+        hj[j].off = off[j];
+        hj[j].qoff = qo;
+        qo += n[j];
+        hj[j].n = n[j];
+        hj[j].tp0 = tp_total;
+        hj[j].mode = mode[j];
+        hj[j].pad = 0;
+        const int64_t tiles = (n[j] + kPairTile - 1) / kPairTile, tp = tiles * (tiles + 1) / 2;
+        tp_total += tp;
+        tp_max = std::max(tp_max, tp);
+        n_max = std::max(n_max, n[j]);
+    }
+    if (tp_max > 0x7fffffff || nj > 65535) return ctx->fail(PITT_E_INVALID, "axis height: too many jobs / tiles");
+    float* tmax = (float*)ctx->buf("axb_tile_max", (size_t)std::max<int64_t>(tp_total, 1) * 4);
+    if (!tmax) return ctx->fail(PITT_E_NOMEM, "axis batch tile maxima");
+    PITT_HIP_TRY(hipMemcpyAsync(dj, hj, (size_t)nj * sizeof(AxisJob), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_axis_init_b, dim3((nj + 63) / 64), dim3(64), 0, s, dw, nj);
+    if (n_max > 0 && tp_max > 0) {
+        int rec = ctx->prof_begin("k_axis_project", (double)q_total * 24.0);
+        hipLaunchKernelGGL(k_axis_project_b, dim3((unsigned)std::min<int64_t>((n_max + 255) / 256, 1024), (unsigned)nj),
+                           dim3(256), 0, s, x, y, z, dj, qx, qy, qz);
+        ctx->prof_end(rec);
+        rec = ctx->prof_begin("k_pair_max", 0.0);
+        hipLaunchKernelGGL(k_pair_scan_b<false>, dim3((unsigned)tp_max, (unsigned)nj), dim3(kPairTile), 0, s, qx, qy, qz,
+                           dj, dw, tmax);
+        ctx->prof_end(rec);
+        hipLaunchKernelGGL(k_axis_slo_b, dim3((nj + 63) / 64), dim3(64), 0, s, dw, nj);
+        rec = ctx->prof_begin("k_pair_first", 0.0);
+        hipLaunchKernelGGL(k_pair_scan_b<true>, dim3((unsigned)tp_max, (unsigned)nj), dim3(kPairTile), 0, s, qx, qy, qz,
+                           dj, dw, tmax);
+        ctx->prof_end(rec);
+    }
+    hipLaunchKernelGGL(k_axis_final_b, dim3((nj + 63) / 64), dim3(64), 0, s, qx, qy, qz, dj, dw, nj, dout);
+    PITT_HIP_TRY(hipGetLastError());
+    PITT_HIP_TRY(hipMemcpyAsync(ho, dout, (size_t)nj * sizeof(AxisOut), hipMemcpyDeviceToHost, s));
+    PITT_HIP_TRY(hipStreamSynchronize(s));
+    for (int j = 0; j < nj; ++j) {
+        height[j] = ho[j].height;
+        idx1[j] = ho[j].idx1;
+        idx2[j] = ho[j].idx2;
+        for (int k = 0; k < 3; ++k) centroid3[3 * j + k] = ho[j].centroid[k];
+    }
+    return PITT_OK;
+}
+
 }  // namespace pitt
 
 extern "C" int pitt_axis_height(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

@@ -24,6 +24,9 @@ const std::vector<int32_t>& sampler_table(pitt_ctx* ctx, int64_t n, uint32_t see
     auto key = std::make_tuple(n, seed, attempts, k);
     auto it = ctx->tables.find(key);
     if (it != ctx->tables.end()) return it->second;
+    // bounded: a tracking session sees a new cluster size almost every frame.  Callers copy a table
+    // out before asking for the next one, so dropping the cache here invalidates nothing in use.
+    if (ctx->tables.size() >= 512) ctx->tables.clear();
     std::vector<int32_t> t((size_t)attempts * k);
     std::mt19937 mt(seed);  // boost::mt19937 and std::mt19937 produce the same stream
     std::unordered_map<int64_t, int64_t> sh;
@@ -57,7 +60,11 @@ float float_threshold(double th) {
 void* pitt_ctx::buf(const std::string& name, size_t bytes) {
     pitt::DevBuf& b = bufs[name];
     if (b.bytes < bytes || !b.p) {
-        if (b.p) (void)hipFree(b.p);
+        // work queued on the stream may still use the old block: let it drain before freeing
+        if (b.p) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(b.p);
+        }
         size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
         nb = (nb + ((size_t)1 << 21) - 1) & ~(((size_t)1 << 21) - 1);
         if (nb == 0) nb = (size_t)1 << 21;
@@ -76,7 +83,13 @@ void* pitt_ctx::buf(const std::string& name, size_t bytes) {
 void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
     auto& e = host_pinned[name];
     if (e.second < bytes || !e.first) {
-        if (e.first) (void)hipHostFree(e.first);
+        // an async copy queued on the stream may still read or write the old block; cached graphs
+        // hold its address in their copy nodes
+        if (e.first) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipHostFree(e.first);
+        }
+        ++arena_gen;
         size_t nb = std::max<size_t>(bytes, 4096);
         if (hipHostMalloc(&e.first, nb, hipHostMallocDefault) != hipSuccess) {
             e.first = nullptr;

@@ -32,6 +32,7 @@
 #include "ctx.hpp"
 #include "device_common.hpp"
 #include "lm.hpp"
+#include "prim_ransac.hpp"
 
 #pragma clang fp contract(off)
 
@@ -152,6 +153,68 @@ struct SphLmModel {
     }
 };
 
+// prim_ransac.hpp traits of the sphere service
+struct SphPrep {
+    int32_t valid;
+};
+struct SphModel {
+    using Coef = float4;
+    using Prep = SphPrep;
+    static constexpr int kSample = 4;
+    static constexpr const char* kName = "k_sph";
+    static constexpr double kModelBytes = 48.0, kCountBytes = 12.0;
+    static constexpr bool kDevicePrep = false;
+    int max_iterations;
+    double probability;
+    uint32_t seed;
+    int optimize;
+    double rmin, rmax;
+    float t;
+    static void to_out(const float4& c, float* o) {
+        o[0] = c.x, o[1] = c.y, o[2] = c.z, o[3] = c.w;
+    }
+    void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, float4* coef, int32_t* flag) const {
+        hipLaunchKernelGGL(k_sph_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, tab, A, rmin,
+                           rmax, coef, flag);
+    }
+    void launch_count(hipStream_t s, const PrimCloud& c, const float4* coef, const int32_t* flag, int a0, int nh,
+                      int32_t* cnt) const {
+        hipLaunchKernelGGL(k_sph_count, dim3((unsigned)ctiles(c.n), (unsigned)nh), dim3(256), 0, s, c.x, c.y, c.z, c.n,
+                           coef, flag, a0, t, cnt);
+    }
+    // selectWithinDistance: none for a model outside the radius limits
+    void prep_host(const float4& c, SphPrep* p) const {
+        p->valid = !((rmin != -DBL_MAX && (double)c.w < rmin) || (rmax != DBL_MAX && (double)c.w > rmax));
+    }
+    void launch_prep(hipStream_t, const float4&, SphPrep*) const {}
+    static bool prep_valid(const SphPrep& p) { return p.valid != 0; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const float4& m, const SphPrep&, int32_t* tc, int32_t* to,
+                       int g) const {
+        SphIn pred{c.x, c.y, c.z, m, t};
+        hipLaunchKernelGGL(k_pred_count<SphIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
+        hipLaunchKernelGGL((k_pred_apply<SphIn, WriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, WriteIdx{c.inliers}, c.n,
+                           to);
+    }
+    // more than 4 inliers: Levenberg-Marquardt in double, the whole iteration in one launch (the
+    // oracle's sphere_refine; fixed reduction order, so the same bits on every run)
+    static int refine_kind(int64_t n_inliers) { return n_inliers > 4 ? 1 : 0; }
+    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const float4& bc, int64_t n_inl,
+                      float4* out) const {
+        return launch_lm(ctx, s, SphLmModel{bc}, c.x, c.y, c.z, c.inliers, n_inl, out);
+    }
+};
+
+SphModel sph_model(const pitt_sphere_params* p) {
+    return SphModel{p->max_iterations, p->probability, p->seed, p->optimize, p->radius_min, p->radius_max,
+                    float_threshold(p->threshold)};
+}
+
+// A batch of sphere services (pitt_classify_clusters): one host synchronisation per phase.
+int sphere_batch(pitt_ctx* ctx, const pitt_sphere_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
+    return prim_ransac_batch(ctx, sph_model(p), cl, nc, res);
+}
+
 }  // namespace pitt
 
 extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
@@ -161,138 +224,18 @@ extern "C" int pitt_sphere_segment(pitt_ctx* ctx, const float* x, const float* y
     if (!ctx) return PITT_E_INVALID;
     if (!p || !n_inliers || !coef_out || n < 0 || (n > 0 && (!x || !y || !z || !inliers)))
         return ctx->fail(PITT_E_INVALID, "null argument");
-    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
-    if (p->max_iterations < 0 || !(p->probability > 0 && p->probability < 1))
-        return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
     *n_inliers = 0;
     if (hypotheses) *hypotheses = 0;
     for (int k = 0; k < 4; ++k) coef_out[k] = 0;
-    if (n < 4) return PITT_NO_MODEL;  // getSamples: "Can not select 4 unique points"
-    hipStream_t s = ctx->stream;
-    const float t = float_threshold(p->threshold);
-    // attempts: every iteration draws once; skipped draws (m11 == 0) are at most max_skip
-    const int64_t max_skip = (int64_t)p->max_iterations * 10;
-    const int64_t A = (int64_t)p->max_iterations + 1 + max_skip;
-    if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
-    const std::vector<int32_t>& tab = sampler_table(ctx, n, p->seed, A, 4);
-    int32_t* dtab = (int32_t*)ctx->buf("sph_table", (size_t)A * 16);
-    float4* dcoef = (float4*)ctx->buf("sph_coef", (size_t)A * 16);
-    int32_t* dflag = (int32_t*)ctx->buf("sph_flag", (size_t)A * 4);
-    int32_t* dcnt = (int32_t*)ctx->buf("sph_cnt", (size_t)A * 4);
-    const int64_t nt = ctiles(n);
-    int32_t* tc = (int32_t*)ctx->buf("sph_tc", (size_t)(nt + 1) * 4);
-    int32_t* to = (int32_t*)ctx->buf("sph_to", (size_t)(nt + 1) * 4);
-    double* part = (double*)ctx->buf("sph_part", 64);
-    if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !part) return ctx->fail(PITT_E_NOMEM, "sphere scratch");
-    PITT_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), (size_t)A * 16, hipMemcpyHostToDevice, s));
-    int rec = ctx->prof_begin("k_sph_model", (double)A * 48.0);
-    hipLaunchKernelGGL(k_sph_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, x, y, z, dtab, (int)A,
-                       p->radius_min, p->radius_max, dcoef, dflag);
-    ctx->prof_end(rec);
-    PITT_HIP_TRY(hipGetLastError());
-    std::vector<int32_t> hflag((size_t)A), hcnt;
-    PITT_HIP_TRY(hipMemcpyAsync(hflag.data(), dflag, (size_t)A * 4, hipMemcpyDeviceToHost, s));
-    PITT_HIP_TRY(hipStreamSynchronize(s));
-    // RandomSampleConsensus::computeModel over chunks of attempts (32, 64, 128, then 256 at a time)
-    int iterations = 0, n_best = -INT32_MAX;
-    double k = 1.0;
-    const double log_probability = std::log(1.0 - p->probability);
-    const double one_over_indices = 1.0 / (double)n;
-    int64_t skipped = 0;
-    int best = -1;
-    int64_t a = 0;
-    int chunk = 32;
-    bool done = false;
-    while (!done && a < A) {
-        const int64_t a1 = std::min<int64_t>(A, a + chunk);
-        const int nh = (int)(a1 - a);
-        PITT_HIP_TRY(hipMemsetAsync(dcnt + a, 0, (size_t)nh * 4, s));
-        rec = ctx->prof_begin("k_sph_count", (double)nh * (double)n * 12.0);
-        hipLaunchKernelGGL(k_sph_count, dim3((unsigned)nt, (unsigned)nh), dim3(256), 0, s, x, y, z, n, dcoef, dflag,
-                           (int)a, t, dcnt + a);
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        hcnt.resize((size_t)nh);
-        PITT_HIP_TRY(hipMemcpyAsync(hcnt.data(), dcnt + a, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        for (int64_t i = a; i < a1; ++i) {
-            if (!(iterations < k && skipped < max_skip)) {
-                done = true;
-                break;
-            }
-            if (hflag[(size_t)i] == 0) {
-                ++skipped;
-                continue;
-            }
-            const int n_in = hcnt[(size_t)(i - a)];  // 0 for a model outside the radius limits
-            if (n_in > n_best) {
-                n_best = n_in;
-                best = (int)i;
-                const double w = (double)n_best * one_over_indices;
-                double p_no = 1.0 - std::pow(w, 4.0);
-                p_no = std::max(std::numeric_limits<double>::epsilon(), p_no);
-                p_no = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no);
-                k = log_probability / std::log(p_no);
-            }
-            ++iterations;
-            if (iterations > p->max_iterations) {
-                done = true;
-                break;
-            }
-        }
-        a = a1;
-        chunk = std::min(chunk * 2, 256);
-    }
-    if (hypotheses) *hypotheses = iterations;
-    if (best < 0) return PITT_NO_MODEL;
-    float4 bc;
-    PITT_HIP_TRY(hipMemcpy(&bc, dcoef + best, 16, hipMemcpyDeviceToHost));
-    int32_t* hto = (int32_t*)ctx->pinned("sph_to_h", 16);
-    if (!hto) return ctx->fail(PITT_E_NOMEM, "sphere pinned");
-    const int g = grid_for_tiles(nt);
-    // selectWithinDistance (none for a model outside the radius limits)
-    auto select = [&](float4 c) -> int {
-        const bool valid = !((p->radius_min != -DBL_MAX && (double)c.w < p->radius_min) ||
-                             (p->radius_max != DBL_MAX && (double)c.w > p->radius_max));
-        if (!valid) {
-            *n_inliers = 0;
-            return PITT_OK;
-        }
-        SphIn pred{x, y, z, c, t};
-        hipLaunchKernelGGL(k_pred_count<SphIn>, dim3(g), dim3(kBlock), 0, s, pred, n, tc);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, nt, to);
-        hipLaunchKernelGGL((k_pred_apply<SphIn, WriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, WriteIdx{inliers}, n, to);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hto, to + nt, 4, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        *n_inliers = hto[0];
-        return PITT_OK;
-    };
-    int rc = select(bc);
+    const PrimCloud c{x, y, z, nullptr, nullptr, nullptr, n, inliers};
+    PrimResult r;
+    const int rc = sphere_batch(ctx, p, &c, 1, &r);
     if (rc != PITT_OK) return rc;
-    float out[4] = {bc.x, bc.y, bc.z, bc.w};
-    if (p->optimize && *n_inliers > 4) {
-        // Levenberg-Marquardt in double, the whole iteration in one 1024-thread block (the oracle's
-        // sphere_refine; fixed reduction order, so the same bits on every run)
-        float4* dref = (float4*)part;
-        rec = ctx->prof_begin("k_sph_lm", (double)*n_inliers * 12.0);
-        const int lrc = launch_lm(ctx, s, SphLmModel{bc}, x, y, z, inliers, *n_inliers, dref);
-        if (lrc != PITT_OK) return lrc;
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        float4* hr = (float4*)ctx->pinned("sph_ref_h", 16);
-        if (!hr) return ctx->fail(PITT_E_NOMEM, "sphere pinned");
-        PITT_HIP_TRY(hipMemcpyAsync(hr, dref, 16, hipMemcpyDeviceToHost, s));
-        PITT_HIP_TRY(hipStreamSynchronize(s));
-        out[0] = hr->x;
-        out[1] = hr->y;
-        out[2] = hr->z;
-        out[3] = hr->w;
-        rc = select(make_float4(out[0], out[1], out[2], out[3]));
-        if (rc != PITT_OK) return rc;
-    }
-    for (int r = 0; r < 4; ++r) coef_out[r] = out[r];
+    if (hypotheses) *hypotheses = r.hypotheses;
+    if (r.status != PITT_OK) return r.status;
+    *n_inliers = r.n_inliers;
+    for (int k = 0; k < 4; ++k) coef_out[k] = r.coef[k];
     return PITT_OK;
 }
 

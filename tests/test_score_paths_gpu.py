@@ -60,17 +60,19 @@ def test_hip_graph_replay_bit_exact():
     import torch
     frames = [pitt.synth_frame(s, seed, 320, 240) for s, seed in ((0, 7000), (1, 7001), (2, 7002), (0, 7003))]
     b = pitt.FrameBatch.from_host(frames, device="cuda:0")
-    old = os.environ.get("PITT_GRAPHS")
+    old = {k: os.environ.get(k) for k in ("PITT_GRAPHS", "PITT_GRAPH_MIN_FRAMES")}
     try:
         os.environ["PITT_GRAPHS"] = "0"
         direct = pitt.Context(0)
         os.environ["PITT_GRAPHS"] = "1"
+        os.environ["PITT_GRAPH_MIN_FRAMES"] = "1"  # graphs for this 4-frame layout (default: 64 frames and up)
         graphed = pitt.Context(0)
     finally:
-        if old is None:
-            del os.environ["PITT_GRAPHS"]
-        else:
-            os.environ["PITT_GRAPHS"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         ref_inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
         ref = direct.plane_segment_batch(b, pitt.sac_params(), ref_inl)
