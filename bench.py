@@ -330,6 +330,106 @@ def config5_pass(pitt, ctx, threads, reps=5):
             "matches_oracle": bool(same)}
 
 
+def synth_clusters(seed=0):
+    """Ten table-top clusters of mixed kinds and sizes (300-3,600 points, 10-20 % clutter): spheres,
+    cylinders, cones and boxes with 1 mm noise -- the shapes clustersAcquisition classifies."""
+    rng = np.random.default_rng(seed)
+
+    def clutter(n, c):
+        return rng.uniform(-0.12, 0.12, (n, 3)) + c
+
+    def sphere(n, c, r):
+        d = rng.normal(size=(n, 3))
+        return d / np.linalg.norm(d, axis=1)[:, None] * r + c
+
+    def frame(axis):
+        a = np.asarray(axis, float) / np.linalg.norm(axis)
+        u = np.cross(a, [1.0, 0.0, 0.0] if abs(a[0]) < 0.9 else [0.0, 1.0, 0.0])
+        u /= np.linalg.norm(u)
+        return a, u, np.cross(a, u)
+
+    def cylinder(n, c, r, h, axis=(0.1, 0.2, 1.0)):
+        a, u, v = frame(axis)
+        t, ph = rng.uniform(0, h, n), rng.uniform(0, 2 * np.pi, n)
+        return c + t[:, None] * a + r * (np.cos(ph)[:, None] * u + np.sin(ph)[:, None] * v)
+
+    def cone(n, c, half_deg, h, axis=(0.1, 0.2, 1.0)):
+        a, u, v = frame(axis)
+        t, ph = rng.uniform(0.03, h, n), rng.uniform(0, 2 * np.pi, n)
+        r = t * np.tan(np.radians(half_deg))
+        return c + t[:, None] * a + r[:, None] * (np.cos(ph)[:, None] * u + np.sin(ph)[:, None] * v)
+
+    def box(n, c):
+        face = rng.integers(0, 3, n)
+        q = rng.uniform(-0.05, 0.05, (n, 2))
+        p = np.zeros((n, 3))
+        p[face == 0] = np.c_[q, np.full(n, 0.05)][face == 0]
+        p[face == 1] = np.c_[q[:, 0], np.full(n, -0.05), q[:, 1]][face == 1]
+        p[face == 2] = np.c_[np.full(n, 0.05), q][face == 2]
+        return p + c
+
+    specs = [(sphere, 900, (0.3, -0.2, 1.1), 0.05), (cylinder, 1200, (0.3, -0.1, 0.9), 0.04, 0.15),
+             (cone, 1000, (0.3, -0.1, 1.1), 25.0, 0.15), (box, 1500, (0.3, -0.1, 1.0)),
+             (sphere, 300, (0.1, 0.2, 1.2), 0.03), (cylinder, 600, (0.0, 0.1, 0.8), 0.03, 0.12),
+             (box, 400, (-0.2, 0.1, 1.0)), (cone, 2500, (-0.1, -0.2, 1.0), 35.0, 0.15),
+             (sphere, 2000, (0.2, 0.3, 1.3), 0.08), (cylinder, 3000, (-0.3, 0.0, 0.9), 0.05, 0.2)]
+    out = []
+    for f, n, c, *a in specs:
+        pts = np.concatenate([f(n, np.asarray(c), *a), clutter(n // 6, np.asarray(c))])
+        pts += rng.normal(0, 0.001, pts.shape)
+        out.append(pts[rng.permutation(len(pts))].astype(np.float32))
+    return out
+
+
+def classify_pass(pitt, ctx, reps=5):
+    """clustersAcquisition (ransac_segmentation.cpp:230-302) on a frame of ten clusters: normals (k = 50),
+    the sphere / cylinder / cone / plane services and the arbitration, batched through
+    pitt_srv_classify_clusters (one host synchronisation per stage for the frame), against the
+    reference's per-cluster loop through the per-cluster services on the same device (median of `reps`
+    after 1 warm-up; counts and tags compared)."""
+    import torch
+    srv = pitt.Services(ctx)
+    cl = synth_clusters(0)
+    cnt = np.array([len(c) for c in cl], np.int64)
+    off = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
+    xyz = np.concatenate(cl)
+    d = [torch.from_numpy(np.ascontiguousarray(xyz[:, k])).cuda() for k in range(3)]
+
+    def batched():
+        return srv.classify_clusters(*d, off, cnt)
+
+    def loop():
+        res = []
+        for P in cl:
+            dd = [torch.from_numpy(np.ascontiguousarray(P[:, k])).cuda() for k in range(3)]
+            nx, ny, nz, _ = ctx.normal_estimation(*dd, k=50)
+            N = torch.stack([nx, ny, nz], 1).cpu().numpy()
+            r = [srv.ransac_sphere(P), srv.ransac_cylinder(P, N), srv.ransac_cone(P, N), srv.ransac_plane(P)]
+            counts = [len(q[1]) if q[0] else 0 for q in r]
+            res.append((counts, pitt.Services.arbitrate(*counts)))
+        return res
+
+    def median_ms(fn):
+        out = fn()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            ts.append((time.perf_counter() - t) * 1e3)
+        return round(float(np.median(ts)), 2), out
+
+    b_ms, got = median_ms(batched)
+    l_ms, ref = median_ms(loop)
+    same = all(g["inliers"] == c and g["tag"] == t for g, (c, t) in zip(got, ref))
+    srv.close()
+    return {"clusters": len(cl), "points": int(cnt.sum()), "ms_per_frame": b_ms,
+            "statistic": f"median of {reps} after 1 warm-up",
+            "path": "pitt_srv_classify_clusters (device SoA in, one pass for all clusters)",
+            "per_cluster_loop_ms": l_ms, "per_cluster_loop": "normals + 4 service calls per cluster (the reference's loop)",
+            "tags": [g["shape"] for g in got], "matches_per_cluster_services": bool(same)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -553,6 +653,8 @@ def main():
         log(f"[rank 0] config2: {line['config2']}")
         line["config5"] = config5_pass(pitt, ctx, threads)
         log(f"[rank 0] config5: {line['config5']}")
+        line["classify"] = classify_pass(pitt, ctx)
+        log(f"[rank 0] classify: {line['classify']}")
     else:
         clutter_frames = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -7,8 +7,10 @@
 // frame, not once per cluster and service:
 //   staging      the clusters into one tile-padded device SoA (NaN padding)           no sync
 //   normals      normals_batch: exhaustive k-NN inside each cluster, then k_normals   no sync
-//   plane        the plane service's SACSegmentation for every cluster: one plane batch   1 sync
-//   sphere / cylinder / cone   prim_ransac_batch (sphere.hip, cylinder.hip, cone.hip)  ~5 + chunks each
+//   plane        the plane service's SACSegmentation for every cluster: one plane batch on an
+//                auxiliary context's stream, overlapping the next three                 1 sync
+//   sphere / cylinder / cone   one prim_ransac_lockstep of the three models' runs (sphere.hip,
+//                cylinder.hip, cone.hip): each phase's synchronisation serves all three  ~6 + chunks
 //   axis height  the cylinder and cone services' post-processing, axis_height_batch    1 sync
 //   responses    PCManager::inlierToVectorMsg drops inlier index 0 (Q1): the first inlier of every
 //                list read back in one copy                                          1 sync
@@ -20,6 +22,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <string>
 #include <vector>
 
 #include "compact.hpp"
@@ -31,9 +35,12 @@ namespace pitt {
 int finish_batch(pitt_ctx* ctx);
 int normals_batch(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n_total, const int64_t* off,
                   const int64_t* cnt, int nc, int k, const float vp[3], float* nx, float* ny, float* nz, float* curv);
-int sphere_batch(pitt_ctx* ctx, const pitt_sphere_params* p, const PrimCloud* cl, int nc, PrimResult* res);
-int cylinder_batch(pitt_ctx* ctx, const pitt_cylinder_params* p, const PrimCloud* cl, int nc, PrimResult* res);
-int cone_batch(pitt_ctx* ctx, const pitt_cone_params* p, const PrimCloud* cl, int nc, PrimResult* res);
+std::unique_ptr<PrimRunBase> sphere_run(pitt_ctx* ctx, const pitt_sphere_params* p, const PrimCloud* cl, int nc,
+                                        PrimResult* res);
+std::unique_ptr<PrimRunBase> cylinder_run(pitt_ctx* ctx, const pitt_cylinder_params* p, const PrimCloud* cl, int nc,
+                                          PrimResult* res);
+std::unique_ptr<PrimRunBase> cone_run(pitt_ctx* ctx, const pitt_cone_params* p, const PrimCloud* cl, int nc,
+                                      PrimResult* res);
 int axis_height_batch(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n_total,
                       const int64_t* off, const int64_t* n, const float* coef6, const int32_t* mode, int nj,
                       float* height, int32_t* idx1, int32_t* idx2, float* centroid3);
@@ -150,7 +157,20 @@ extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float
     rc = normals_batch(ctx, sx, sy, sz, total, soff.data(), cnt.data(), nc, prm->k, prm->viewpoint, nx, ny, nz, curv);
     if (rc != PITT_OK) return rc;
 
-    // --- plane service ---
+    // --- plane service: its batch on the auxiliary context's stream, overlapping the other services
+    //     (the staged clusters are ready once this stream's work so far has run: an event orders it) ---
+    if (!ctx->aux) {
+        if (pitt_create(&ctx->aux, ctx->device) != PITT_OK || !ctx->aux) return ctx->fail(PITT_E_HIP, "auxiliary context");
+        ctx->aux->use_graphs = false;
+    }
+    {
+        hipEvent_t staged = nullptr;
+        PITT_HIP_TRY(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
+        PITT_HIP_TRY(hipEventRecord(staged, s));
+        const hipError_t we = hipStreamWaitEvent(ctx->aux->stream, staged, 0);
+        (void)hipEventDestroy(staged);
+        PITT_HIP_TRY(we);
+    }
     std::vector<pitt_plane_result> pr((size_t)nc);
     pitt_frames fr;
     fr.x = sx;
@@ -161,24 +181,49 @@ extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float
     fr.n_frames = nc;
     fr.capacity = total;
     int32_t* inl_plane = inl + 3 * total;
-    rc = pitt_plane_segment_batch(ctx, &fr, &prm->plane, pr.data(), inl_plane);
-    if (rc < 0) return rc;
+    rc = pitt_plane_segment_batch_async(ctx->aux, &fr, &prm->plane, pr.data(), inl_plane);
+    if (rc < 0) return ctx->fail(rc, std::string("plane batch: ") + pitt_last_error(ctx->aux));
+    // the batch writes into pr when it completes: never leave this function with it in flight
+    struct AuxWait {
+        pitt_ctx* a;
+        ~AuxWait() { (void)pitt_wait(a); }
+    } aux_wait{ctx->aux};
 
-    // --- sphere, cylinder, cone services ---
-    std::vector<PrimCloud> cl((size_t)nc);
+    // --- sphere, cylinder, cone services, in lockstep (each synchronisation serves all three) ---
+    std::vector<PrimCloud> cls[3];
     std::vector<PrimResult> rs((size_t)nc), ry((size_t)nc), rk((size_t)nc);
-    auto clouds = [&](int srv) {
+    for (int srv = 0; srv < 3; ++srv) {
+        cls[srv].resize((size_t)nc);
         for (int c = 0; c < nc; ++c) {
             const int64_t o = soff[(size_t)c];
-            cl[(size_t)c] = PrimCloud{sx + o, sy + o, sz + o, nx + o, ny + o, nz + o, cnt[(size_t)c], inl + srv * total + o};
+            cls[srv][(size_t)c] = PrimCloud{sx + o, sy + o, sz + o, nx + o, ny + o, nz + o, cnt[(size_t)c],
+                                            inl + srv * total + o};
         }
-    };
-    clouds(0);
-    if ((rc = sphere_batch(ctx, &prm->sphere, cl.data(), nc, rs.data())) != PITT_OK) return rc;
-    clouds(1);
-    if ((rc = cylinder_batch(ctx, &prm->cylinder, cl.data(), nc, ry.data())) != PITT_OK) return rc;
-    clouds(2);
-    if ((rc = cone_batch(ctx, &prm->cone, cl.data(), nc, rk.data())) != PITT_OK) return rc;
+    }
+    {
+        // the sphere and cylinder runs on the two side streams, the cone on the context's: their small
+        // per-cluster launches overlap on the device (each phase's synchronisation waits for all three)
+        for (hipStream_t& sd : ctx->side)
+            if (!sd) PITT_HIP_TRY(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
+        hipEvent_t ready = nullptr;  // the staged clusters and their normals
+        PITT_HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ready, s);
+        for (hipStream_t sd : ctx->side)
+            if (e == hipSuccess) e = hipStreamWaitEvent(sd, ready, 0);
+        (void)hipEventDestroy(ready);
+        PITT_HIP_TRY(e);
+        std::unique_ptr<PrimRunBase> runs[3] = {sphere_run(ctx, &prm->sphere, cls[0].data(), nc, rs.data()),
+                                                cylinder_run(ctx, &prm->cylinder, cls[1].data(), nc, ry.data()),
+                                                cone_run(ctx, &prm->cone, cls[2].data(), nc, rk.data())};
+        rc = prim_ransac_lockstep(ctx, {runs[0].get(), runs[1].get(), runs[2].get()}, {ctx->side[0], ctx->side[1], s});
+        if (rc != PITT_OK) {
+            for (hipStream_t sd : ctx->side) (void)hipStreamSynchronize(sd);
+            return rc;
+        }
+    }
+
+    rc = pitt_wait(ctx->aux);  // the plane batch (results into pr)
+    if (rc < 0) return ctx->fail(rc, std::string("plane batch: ") + pitt_last_error(ctx->aux));
 
     // --- axis height of every cylinder / cone with inliers ---
     std::vector<int64_t> joff, jn;

@@ -246,21 +246,27 @@ struct ConeModelT {
                            ConeWriteIdx{c.inliers}, c.n, to);
     }
     // any inliers: the refinement (fewer than 7: the model unchanged, its direction normalised)
-    static int refine_kind(int64_t n_inliers) { return n_inliers > 0 ? 1 : 0; }
-    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const Coef7& bc, int64_t n_inl,
-                      Coef7* out) const {
-        if (n_inl >= 7) return launch_lm7(ctx, s, ConeResidual{}, c.x, c.y, c.z, c.inliers, n_inl, bc, out);
+    using LmP = Lm7Model<ConeResidual>;
+    static int refine_kind(int64_t n_inliers) { return n_inliers >= 7 ? 1 : n_inliers > 0 ? 2 : 0; }
+    static LmP lm_params(const Coef7& bc) { return LmP{bc}; }
+    void launch_normalize(hipStream_t s, const Coef7& bc, Coef7* out) const {
         hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
-        return PITT_OK;
     }
 };
 
-// A batch of cone services (pitt_classify_clusters): one host synchronisation per phase.
+static ConeModelT cone_model_t(const pitt_cone_params* p) {
+    return ConeModelT{p->max_iterations, p->probability, p->seed, p->optimize,
+                      ConeCfg{p->normal_distance_weight, p->threshold, p->min_angle, p->max_angle, p->eps_angle,
+                              p->axis[0], p->axis[1], p->axis[2], p->eigen33}};
+}
+// A batch of cone services: one host synchronisation per phase.
 int cone_batch(pitt_ctx* ctx, const pitt_cone_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
-    const ConeModelT m{p->max_iterations, p->probability, p->seed, p->optimize,
-                       ConeCfg{p->normal_distance_weight, p->threshold, p->min_angle, p->max_angle, p->eps_angle,
-                               p->axis[0], p->axis[1], p->axis[2], p->eigen33}};
-    return prim_ransac_batch(ctx, m, cl, nc, res);
+    return prim_ransac_batch(ctx, cone_model_t(p), cl, nc, res);
+}
+// The same as a run of prim_ransac_lockstep (pitt_classify_clusters).
+std::unique_ptr<PrimRunBase> cone_run(pitt_ctx* ctx, const pitt_cone_params* p, const PrimCloud* cl, int nc,
+                                      PrimResult* res) {
+    return std::make_unique<PrimRun<ConeModelT>>(ctx, cone_model_t(p), cl, nc, res);
 }
 
 }  // namespace pitt

@@ -63,6 +63,11 @@ struct pitt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    // a second context on its own stream for work that overlaps this one's (pitt_classify_clusters runs
+    // the plane service's batch there beside the other services); created on first use
+    pitt_ctx* aux = nullptr;
+    // two more streams for independent service runs (pitt_classify_clusters), created on first use
+    hipStream_t side[2] = {nullptr, nullptr};
     std::string err;
 
     // scratch arena: named growable buffers (contents undefined between calls)

@@ -212,20 +212,26 @@ struct CylModel {
     }
     // any inliers: the least-squares refinement (7 or more: Eigen's LM refuses m < n, the model then
     // stays and only the direction is normalised)
-    static int refine_kind(int64_t n_inliers) { return n_inliers > 0 ? 1 : 0; }
-    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const CylCoef& bc, int64_t n_inl,
-                      CylCoef* out) const {
-        if (n_inl >= 7) return launch_lm7(ctx, s, CylResidual{}, c.x, c.y, c.z, c.inliers, n_inl, bc, out);
+    using LmP = Lm7Model<CylResidual>;
+    static int refine_kind(int64_t n_inliers) { return n_inliers >= 7 ? 1 : n_inliers > 0 ? 2 : 0; }
+    static LmP lm_params(const Coef7& bc) { return LmP{bc}; }
+    void launch_normalize(hipStream_t s, const Coef7& bc, Coef7* out) const {
         hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
-        return PITT_OK;
     }
 };
 
-// A batch of cylinder services (pitt_classify_clusters): one host synchronisation per phase.
+static CylModel cyl_model(const pitt_cylinder_params* p) {
+    return CylModel{p->max_iterations, p->probability, p->seed, p->optimize, p->radius_min, p->radius_max,
+                    p->normal_distance_weight, p->threshold, (int)p->eigen33};
+}
+// A batch of cylinder services: one host synchronisation per phase.
 int cylinder_batch(pitt_ctx* ctx, const pitt_cylinder_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
-    const CylModel m{p->max_iterations, p->probability, p->seed, p->optimize, p->radius_min, p->radius_max,
-                     p->normal_distance_weight, p->threshold, (int)p->eigen33};
-    return prim_ransac_batch(ctx, m, cl, nc, res);
+    return prim_ransac_batch(ctx, cyl_model(p), cl, nc, res);
+}
+// The same as a run of prim_ransac_lockstep (pitt_classify_clusters).
+std::unique_ptr<PrimRunBase> cylinder_run(pitt_ctx* ctx, const pitt_cylinder_params* p, const PrimCloud* cl, int nc,
+                                          PrimResult* res) {
+    return std::make_unique<PrimRun<CylModel>>(ctx, cyl_model(p), cl, nc, res);
 }
 
 }  // namespace pitt

@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <string>
+#include <vector>
 
 #include "ctx.hpp"
 
@@ -58,7 +60,7 @@ __device__ __forceinline__ void lm_grid_sync(uint32_t* bar, uint32_t& target) {
 // points gid, gid + G * 256, ...; then the wave (xor shuffles), then the four waves in order.
 template <class P>
 __device__ void lm_partial(const P& prm, const float* X, const float* Y, const float* Z, const int32_t* inl,
-                           int64_t m, const double* v, double (*red)[kLmMaxSums], double* out) {
+                           int64_t m, const double* v, double (*red)[kLmMaxSums], double* out, int blk, int nblk) {
     constexpr int N = P::N, S = lm_sums<N>();
     double acc[S];
 #pragma unroll
@@ -67,7 +69,7 @@ __device__ void lm_partial(const P& prm, const float* X, const float* Y, const f
 #pragma unroll
     for (int q = 0; q < N; ++q) w[q] = v[q];
     w[N] = prm.aux(v);
-    for (int64_t k = (int64_t)blockIdx.x * kLmThreads + threadIdx.x; k < m; k += (int64_t)gridDim.x * kLmThreads) {
+    for (int64_t k = (int64_t)blk * kLmThreads + threadIdx.x; k < m; k += (int64_t)nblk * kLmThreads) {
         const int id = inl[k];
         double J[N], f;
         prm.residual(w, X[id], Y[id], Z[id], J, &f);
@@ -165,34 +167,41 @@ __device__ __forceinline__ bool lm_solve_dev(const double* sums, double lambda, 
     return true;
 }
 
-// The oracle's lm_solve<N> on a grid of G <= kLmMaxBlocks resident blocks.  Block 0's thread 0 runs the
-// scalar control (Marquardt damping x10 / x0.1, accept on a lower cost, stop when no damping lowers it, the
-// step (accepted or rejected) falls below 1e-10 relative or P::kMaxIt iterations pass); every block sums its share of the
-// residuals at each trial point.  Two grid barriers per evaluation: after the trial point is published, and
-// after the partial sums are written (block 0 then reduces them over the blocks in order: deterministic).
-template <class P>
-__global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restrict__ X, const float* __restrict__ Y,
-                                                   const float* __restrict__ Z, const int32_t* __restrict__ inl,
-                                                   int64_t m, LmGlobal* __restrict__ g, typename P::Out* __restrict__ out) {
+// Block-shared state of one Levenberg-Marquardt run (GRID: the partial-sum staging of a multi-block run).
+template <int N, bool GRID>
+struct LmShared {
+    static constexpr int S = lm_sums<N>();
+    double red[kLmThreads / 64][kLmMaxSums];
+    double stage[GRID ? kLmMaxBlocks * S : 1];
+    double cur[S], trial[S];
+    double xv[N], xn[N], dl[N];  // block 0's current point, the trial point it publishes, their step
+    int32_t st_s;
+};
+
+// The oracle's lm_solve<N> (oracle/pitt_oracle.cpp, sphere_refine / lm_solve) on nblk resident blocks
+// (blk = this block's index).  Block 0's thread 0 runs the scalar control (Marquardt damping x10 / x0.1,
+// accept on a lower cost, stop when no damping lowers it, the step dl (accepted or rejected) falls below
+// 1e-10 relative to the trial point -- the oracle's measure -- or P::kMaxIt iterations pass); every block
+// sums its share of the residuals at each trial point.  One block (`one`): partial sums straight into
+// LDS, __syncthreads for the barriers.  Several (GRID): two grid barriers per evaluation, after the trial
+// point is published and after the partial sums are written (block 0 reduces them in order).
+template <class P, bool GRID>
+__device__ void lm_run(const P& prm, const float* __restrict__ X, const float* __restrict__ Y,
+                       const float* __restrict__ Z, const int32_t* __restrict__ inl, int64_t m, LmGlobal* g,
+                       typename P::Out* out, bool one, int blk, int nblk, LmShared<P::N, GRID>& sh) {
     constexpr int N = P::N, S = lm_sums<N>();
-    __shared__ double red[kLmThreads / 64][kLmMaxSums];
-    __shared__ double stage[kLmMaxBlocks * S];
-    __shared__ double cur[S], trial[S];
-    __shared__ double xv[N], xn[N];  // block 0's copy of the trial point it publishes in g->xn
-    __shared__ int32_t st_s;
-    // one block (small inlier sets): partial sums straight into cur / trial, __syncthreads for the
-    // barriers, the trial point and the state in LDS -- no device-memory round trips per evaluation
-    const bool one = gridDim.x == 1;
     double v0[N];
     prm.init(v0);
     uint32_t target = 0;
-    lm_partial(prm, X, Y, Z, inl, m, v0, red, one ? cur : g->part[blockIdx.x]);
-    const bool ctl = blockIdx.x == 0;
-    if (!one) {
-        lm_grid_sync(&g->bar, target);
-        if (ctl) lm_reduce_grid<S>(g, stage, cur);
+    lm_partial(prm, X, Y, Z, inl, m, v0, sh.red, one ? sh.cur : g->part[blk], blk, nblk);
+    const bool ctl = blk == 0;
+    if constexpr (GRID) {
+        if (!one) {
+            lm_grid_sync(&g->bar, target);
+            if (ctl) lm_reduce_grid<S>(g, sh.stage, sh.cur);
+        }
     }
-    if (ctl && threadIdx.x < N) xv[threadIdx.x] = v0[threadIdx.x];
+    if (ctl && threadIdx.x < N) sh.xv[threadIdx.x] = v0[threadIdx.x];
     // control state (block 0, thread 0)
     double lambda = 1e-3;
     int it = 0;
@@ -202,72 +211,124 @@ __global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restric
         if (ctl && threadIdx.x == 0) {
             bool stop = false;
             if (have_trial) {
-                if (trial[S - 1] < cur[S - 1]) {  // accepted: the end of an outer iteration
-                    double step = 0, nx = 0;
-                    for (int r = 0; r < N; ++r) {
-                        const double d = xn[r] - xv[r];
-                        step += d * d;
-                        nx += xn[r] * xn[r];
-                        xv[r] = xn[r];
-                    }
-                    for (int q = 0; q < S; ++q) cur[q] = trial[q];
+                double rs = 0, rx = 0;  // the step and the trial point, as the oracle measures them
+                for (int r = 0; r < N; ++r) {
+                    rs += sh.dl[r] * sh.dl[r];
+                    rx += sh.xn[r] * sh.xn[r];
+                }
+                const bool small = sqrt(rs / (rx + 1e-300)) < 1e-10;
+                if (sh.trial[S - 1] < sh.cur[S - 1]) {  // accepted: the end of an outer iteration
+                    for (int r = 0; r < N; ++r) sh.xv[r] = sh.xn[r];
+                    for (int q = 0; q < S; ++q) sh.cur[q] = sh.trial[q];
                     lambda *= 0.1;
                     ++it;
-                    stop = sqrt(step / (nx + 1e-300)) < 1e-10 || it >= P::kMaxIt;
+                    stop = small || it >= P::kMaxIt;
                 } else {  // a rejected step below 1e-10 relative cannot change the float result: stop
-                    double rs = 0, rx = 0;
-                    for (int r = 0; r < N; ++r) {
-                        const double d = xn[r] - xv[r];
-                        rs += d * d;
-                        rx += xn[r] * xn[r];
-                    }
-                    stop = sqrt(rs / (rx + 1e-300)) < 1e-10;
+                    stop = small;
                     lambda *= 10;
                 }
             }
             if (!stop && !(lambda < 1e10)) stop = true;  // no damping lowered the cost
             double dl[N];
-            if (!stop && !lm_solve_dev<N>(cur, lambda, P::kDiagEps, dl)) stop = true;
+            if (!stop && !lm_solve_dev<N>(sh.cur, lambda, P::kDiagEps, dl)) stop = true;
             if (!stop)
                 for (int r = 0; r < N; ++r) {
-                    xn[r] = xv[r] + dl[r];
-                    if (!one) g->xn[r] = xn[r];
+                    sh.dl[r] = dl[r];
+                    sh.xn[r] = sh.xv[r] + dl[r];
+                    if constexpr (GRID)
+                        if (!one) g->xn[r] = sh.xn[r];
                 }
-            st_s = stop ? 3 : 0;
-            if (!one) g->state = st_s;
+            sh.st_s = stop ? 3 : 0;
+            if constexpr (GRID)
+                if (!one) g->state = sh.st_s;
         }
         double vn[N];
         if (one) {
             __syncthreads();
-            if (st_s == 3) break;
+            if (sh.st_s == 3) break;
 #pragma unroll
-            for (int k = 0; k < N; ++k) vn[k] = xn[k];
-            lm_partial(prm, X, Y, Z, inl, m, vn, red, trial);
-        } else {
+            for (int k = 0; k < N; ++k) vn[k] = sh.xn[k];
+            lm_partial(prm, X, Y, Z, inl, m, vn, sh.red, sh.trial, blk, nblk);
+        } else if constexpr (GRID) {
             lm_grid_sync(&g->bar, target);
             if (__hip_atomic_load(&g->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) break;
 #pragma unroll
             for (int k = 0; k < N; ++k) vn[k] = __hip_atomic_load(&g->xn[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            lm_partial(prm, X, Y, Z, inl, m, vn, red, g->part[blockIdx.x]);
+            lm_partial(prm, X, Y, Z, inl, m, vn, sh.red, g->part[blk], blk, nblk);
             lm_grid_sync(&g->bar, target);
-            if (ctl) lm_reduce_grid<S>(g, stage, trial);
+            if (ctl) lm_reduce_grid<S>(g, sh.stage, sh.trial);
         }
         have_trial = true;
     }
-    if (ctl && threadIdx.x == 0) prm.finish(xv, out);
+    if (ctl && threadIdx.x == 0) prm.finish(sh.xv, out);
 }
 
-// Host side: G = ceil(m / 1024) blocks (at most kLmMaxBlocks), the barrier counter zeroed on the stream.
+template <class P>
+__global__ __launch_bounds__(kLmThreads) void k_lm(P prm, const float* __restrict__ X, const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, const int32_t* __restrict__ inl,
+                                                   int64_t m, LmGlobal* __restrict__ g, typename P::Out* __restrict__ out) {
+    __shared__ LmShared<P::N, true> sh;
+    lm_run<P, true>(prm, X, Y, Z, inl, m, g, out, gridDim.x == 1, (int)blockIdx.x, (int)gridDim.x, sh);
+}
+
+// One refinement per block (pitt_classify_clusters: every cluster's model of one kind at once); each
+// block runs the one-block form of k_lm on its job, so a job's result is the single launch's bit for bit.
+template <class P>
+struct LmJob {
+    P prm;
+    const float *x, *y, *z;
+    const int32_t* inl;
+    int64_t m;
+    typename P::Out* out;
+};
+template <class P>
+__global__ __launch_bounds__(kLmThreads) void k_lm_batch(const LmJob<P>* __restrict__ jobs) {
+    __shared__ LmShared<P::N, false> sh;
+    const LmJob<P> j = jobs[blockIdx.x];
+    lm_run<P, false>(j.prm, j.x, j.y, j.z, j.inl, j.m, nullptr, j.out, true, 0, 1, sh);
+}
+
+// Host side: G = ceil(m / 1024) blocks (at most kLmMaxBlocks, and no more than can be resident at once:
+// the grid barrier needs every block running), the barrier counter zeroed on the stream.
 template <class P>
 inline int launch_lm(pitt_ctx* ctx, hipStream_t s, const P& prm, const float* x, const float* y, const float* z,
-                     const int32_t* inl, int64_t m, typename P::Out* out) {
-    LmGlobal* g = (LmGlobal*)ctx->buf("lm_global", sizeof(LmGlobal));
+                     const int32_t* inl, int64_t m, typename P::Out* out, const char* scratch = "lm_global") {
+    // scratch: one LmGlobal per stream that may run a grid refinement (its barrier and partial sums)
+    LmGlobal* g = (LmGlobal*)ctx->buf(scratch, sizeof(LmGlobal));
     if (!g) return ctx->fail(PITT_E_NOMEM, "lm scratch");
     // up to P::kSmall inliers one block (no grid barrier: two device-memory round trips per evaluation
     // cost more than the 256 threads' extra points), above that one block per 1024 inliers
-    const int G = m <= P::kSmall ? 1 : (int)std::min<int64_t>(kLmMaxBlocks, (m + 1023) / 1024);
+    int G = m <= P::kSmall ? 1 : (int)std::min<int64_t>(kLmMaxBlocks, (m + 1023) / 1024);
+    if (G > 1) {
+        static int resident = -1;  // blocks of k_lm<P> the device holds at once
+        if (resident < 0) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_lm<P>),
+                                                             kLmThreads, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+                return ctx->fail(PITT_E_HIP, "lm occupancy query");
+            resident = per_cu * cus;
+        }
+        if (resident < 1) return ctx->fail(PITT_E_HIP, "lm kernel cannot be resident");
+        G = std::min(G, resident);
+    }
     PITT_HIP_TRY(hipMemsetAsync(&g->bar, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_lm<P>, dim3(G), dim3(kLmThreads), 0, s, prm, x, y, z, inl, m, g, out);
+    PITT_HIP_TRY(hipGetLastError());
+    return PITT_OK;
+}
+
+// A batch of one-block refinements (every job's m <= P::kSmall) in one launch.
+template <class P>
+inline int launch_lm_batch(pitt_ctx* ctx, hipStream_t s, const std::vector<LmJob<P>>& jobs, const char* name) {
+    if (jobs.empty()) return PITT_OK;
+    const size_t bytes = jobs.size() * sizeof(LmJob<P>);
+    auto* h = (LmJob<P>*)ctx->pinned(std::string(name) + "_lmjobs_h", bytes);
+    auto* d = (LmJob<P>*)ctx->buf(std::string(name) + "_lmjobs", bytes);
+    if (!h || !d) return ctx->fail(PITT_E_NOMEM, "lm batch scratch");
+    std::copy(jobs.begin(), jobs.end(), h);
+    PITT_HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_lm_batch<P>, dim3((unsigned)jobs.size()), dim3(kLmThreads), 0, s, d);
     PITT_HIP_TRY(hipGetLastError());
     return PITT_OK;
 }

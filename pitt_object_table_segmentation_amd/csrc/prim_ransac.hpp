@@ -24,8 +24,9 @@
 //   launch_model / launch_count  the hypothesis and counting kernels of one cloud
 //   kDevicePrep, prep_host / launch_prep, prep_valid   isModelValid (+ constants) on host or device
 //   launch_select                k_pred_count / k_scan_tiles / k_pred_apply of one cloud
-//   refine_kind(n_inliers)       0: none, 1: refine and select again
-//   launch_refine                the refinement of one cloud into a device Coef
+//   refine_kind(n_inliers)       0: none, 1: refine (LmP, lm.hpp) and select again, 2: only normalise
+//                                the direction (Eigen's LM refuses m < n) and select again
+//   LmP, lm_params, launch_normalize   the refinement's lm.hpp model from a winning model
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -33,11 +34,13 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "compact.hpp"
 #include "ctx.hpp"
+#include "lm.hpp"
 
 namespace pitt {
 
@@ -54,92 +57,149 @@ struct PrimResult {
     float coef[7];
 };
 
+// The phase interface of one model's batch (PrimRun<M> below); pitt_classify_clusters drives runs of the
+// three models, built in their own translation units, through it.
+struct PrimRunBase {
+    int nc = 0;
+    bool any_model = false, launched = false;
+    std::vector<int> refined;
+    virtual ~PrimRunBase() = default;
+    virtual void set_stream(hipStream_t st) = 0;
+    virtual int setup() = 0;
+    virtual int issue_hyp() = 0;
+    virtual int issue_chunk(int chunk, bool* any) = 0;
+    virtual void consume_chunk(int chunk) = 0;
+    virtual int issue_best() = 0;
+    virtual void read_best() = 0;
+    virtual bool needs_prep_sync() const = 0;
+    virtual int issue_prep() = 0;
+    virtual int issue_select() = 0;
+    virtual void read_select() = 0;
+    virtual int issue_refine() = 0;
+    virtual void read_refine() = 0;
+    virtual void finish() = 0;
+};
+
+// One model's batch, phase by phase: every issue_* enqueues work on the stream without waiting, every
+// read_* / consume_* uses what the last synchronisation brought back.  prim_ransac_batch drives one run,
+// prim_ransac_lockstep several (pitt_classify_clusters: the sphere, cylinder and cone services share
+// each synchronisation).
 template <class M>
-int prim_ransac_batch(pitt_ctx* ctx, const M& m, const PrimCloud* cl, int nc, PrimResult* res) {
+struct PrimRun final : PrimRunBase {
     using Coef = typename M::Coef;
     using Prep = typename M::Prep;
-    hipStream_t s = ctx->stream;
-    const std::string nm = M::kName;
-    if (m.max_iterations < 0 || !(m.probability > 0 && m.probability < 1))
-        return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
-    const int64_t max_skip = (int64_t)m.max_iterations * 10;
-    const int64_t A = (int64_t)m.max_iterations + 1 + max_skip;
-    if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
-    for (int c = 0; c < nc; ++c) {
-        res[c].status = PITT_NO_MODEL;  // getSamples: "Can not select k unique points" below kSample
-        res[c].hypotheses = 0;
-        res[c].n_inliers = 0;
-        for (int k = 0; k < 7; ++k) res[c].coef[k] = 0.0f;
-        if (cl[c].n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
-    }
-    if (nc == 0) return PITT_OK;
-    // scratch: per cloud A attempts of tables, models, flags and counts; tile counts for the selection
-    std::vector<int64_t> toff((size_t)nc + 1, 0);
-    for (int c = 0; c < nc; ++c) toff[(size_t)c + 1] = toff[(size_t)c] + ctiles(std::max<int64_t>(cl[c].n, 1)) + 1;
-    int32_t* dtab = (int32_t*)ctx->buf(nm + "_table", (size_t)nc * A * M::kSample * 4);
-    Coef* dcoef = (Coef*)ctx->buf(nm + "_coef", (size_t)nc * A * sizeof(Coef));
-    int32_t* dflag = (int32_t*)ctx->buf(nm + "_flag", (size_t)nc * A * 4);
-    int32_t* dcnt = (int32_t*)ctx->buf(nm + "_cnt", (size_t)nc * A * 4);
-    int32_t* tc = (int32_t*)ctx->buf(nm + "_tc", (size_t)toff[(size_t)nc] * 4);
-    int32_t* to = (int32_t*)ctx->buf(nm + "_to", (size_t)toff[(size_t)nc] * 4);
-    Coef* dref = (Coef*)ctx->buf(nm + "_ref", (size_t)nc * sizeof(Coef));
-    Prep* dprep = (Prep*)ctx->buf(nm + "_prep", (size_t)nc * sizeof(Prep));
-    int32_t* htab = (int32_t*)ctx->pinned(nm + "_table_h", (size_t)nc * A * M::kSample * 4);
-    int32_t* hflag = (int32_t*)ctx->pinned(nm + "_flag_h", (size_t)nc * A * 4);
-    int32_t* hcnt = (int32_t*)ctx->pinned(nm + "_cnt_h", (size_t)nc * 256 * 4);
-    Coef* hcoef = (Coef*)ctx->pinned(nm + "_coef_h", (size_t)nc * sizeof(Coef));
-    Prep* hprep = (Prep*)ctx->pinned(nm + "_prep_h", (size_t)nc * sizeof(Prep));
-    int32_t* hto = (int32_t*)ctx->pinned(nm + "_to_h", (size_t)nc * 4);
-    if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref || !dprep || !htab || !hflag || !hcnt || !hcoef ||
-        !hprep || !hto)
-        return ctx->fail(PITT_E_NOMEM, nm + " scratch");
-    // per-cloud replay state (RandomSampleConsensus::computeModel)
-    struct St {
+    struct St {  // RandomSampleConsensus::computeModel's state per cloud
         bool run = false;
         int iterations = 0, n_best = -INT32_MAX, best = -1;
         double k = 1.0;
         int64_t skipped = 0, a = 0;
     };
-    std::vector<St> st((size_t)nc);
-    const double log_probability = std::log(1.0 - m.probability);
+    pitt_ctx* ctx;
+    M m;
+    const PrimCloud* cl;
+    PrimResult* res;
+    hipStream_t s = nullptr;
+    std::string nm;
+    int64_t A = 0, max_skip = 0;
+    double log_probability = 0;
+    std::vector<int64_t> toff;
+    int32_t *dtab = nullptr, *dflag = nullptr, *dcnt = nullptr, *tc = nullptr, *to = nullptr;  // dcnt: [nc][256]
+    Coef *dcoef = nullptr, *dref = nullptr, *hcoef = nullptr;
+    Prep *dprep = nullptr, *hprep = nullptr;
+    int32_t *htab = nullptr, *hflag = nullptr, *hcnt = nullptr, *hto = nullptr;
+    std::vector<St> st;
+    std::vector<Coef> cur;
+    std::vector<int> with_model, sel;
 
-    // 1. hypotheses
-    for (int c = 0; c < nc; ++c) {
-        if (cl[c].n < M::kSample) continue;
-        st[(size_t)c].run = true;
-        const std::vector<int32_t>& tab = sampler_table(ctx, cl[c].n, m.seed, A, M::kSample);
-        int32_t* ht = htab + (size_t)c * A * M::kSample;
-        std::copy(tab.begin(), tab.end(), ht);
-        int32_t* dt = dtab + (size_t)c * A * M::kSample;
-        PITT_HIP_TRY(hipMemcpyAsync(dt, ht, (size_t)A * M::kSample * 4, hipMemcpyHostToDevice, s));
-        const int rec = ctx->prof_begin((nm + "_model").c_str(), (double)A * M::kModelBytes);
-        m.launch_model(s, cl[c], dt, (int)A, dcoef + (size_t)c * A, dflag + (size_t)c * A);
-        ctx->prof_end(rec);
-        PITT_HIP_TRY(hipGetLastError());
-        PITT_HIP_TRY(hipMemcpyAsync(hflag + (size_t)c * A, dflag + (size_t)c * A, (size_t)A * 4,
-                                    hipMemcpyDeviceToHost, s));
+    PrimRun(pitt_ctx* c, const M& model, const PrimCloud* clouds, int n, PrimResult* r) : ctx(c), m(model), cl(clouds), res(r) {
+        nc = n;
     }
-    PITT_HIP_TRY(hipStreamSynchronize(s));
 
-    // 2. chunks of attempts, every running cloud per chunk, the serial loop replayed on the host
-    for (int chunk = 32;; chunk = std::min(chunk * 2, 256)) {
-        bool any = false;
+    void set_stream(hipStream_t st) override { s = st; }
+    int setup() override {
+        if (!s) s = ctx->stream;
+        nm = M::kName;
+        if (m.max_iterations < 0 || !(m.probability > 0 && m.probability < 1))
+            return ctx->fail(PITT_E_INVALID, "max_iterations / probability");
+        max_skip = (int64_t)m.max_iterations * 10;
+        A = (int64_t)m.max_iterations + 1 + max_skip;
+        if (A > (1 << 24)) return ctx->fail(PITT_E_INVALID, "max_iterations too large");
+        for (int c = 0; c < nc; ++c) {
+            res[c].status = PITT_NO_MODEL;  // getSamples: "Can not select k unique points" below kSample
+            res[c].hypotheses = 0;
+            res[c].n_inliers = 0;
+            for (int k = 0; k < 7; ++k) res[c].coef[k] = 0.0f;
+            if (cl[c].n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "more than 2^31 points");
+        }
+        if (nc == 0) return PITT_OK;
+        // per cloud A attempts of tables, models, flags and counts; tile counts for the selection
+        toff.assign((size_t)nc + 1, 0);
+        for (int c = 0; c < nc; ++c) toff[(size_t)c + 1] = toff[(size_t)c] + ctiles(std::max<int64_t>(cl[c].n, 1)) + 1;
+        dtab = (int32_t*)ctx->buf(nm + "_table", (size_t)nc * A * M::kSample * 4);
+        dcoef = (Coef*)ctx->buf(nm + "_coef", (size_t)nc * A * sizeof(Coef));
+        dflag = (int32_t*)ctx->buf(nm + "_flag", (size_t)nc * A * 4);
+        dcnt = (int32_t*)ctx->buf(nm + "_cnt", (size_t)nc * 256 * 4);  // the chunk's counts, all clouds
+        tc = (int32_t*)ctx->buf(nm + "_tc", (size_t)toff[(size_t)nc] * 4);
+        to = (int32_t*)ctx->buf(nm + "_to", (size_t)toff[(size_t)nc] * 4);
+        dref = (Coef*)ctx->buf(nm + "_ref", (size_t)nc * sizeof(Coef));
+        dprep = (Prep*)ctx->buf(nm + "_prep", (size_t)nc * sizeof(Prep));
+        htab = (int32_t*)ctx->pinned(nm + "_table_h", (size_t)nc * A * M::kSample * 4);
+        hflag = (int32_t*)ctx->pinned(nm + "_flag_h", (size_t)nc * A * 4);
+        hcnt = (int32_t*)ctx->pinned(nm + "_cnt_h", (size_t)nc * 256 * 4);
+        hcoef = (Coef*)ctx->pinned(nm + "_coef_h", (size_t)nc * sizeof(Coef));
+        hprep = (Prep*)ctx->pinned(nm + "_prep_h", (size_t)nc * sizeof(Prep));
+        hto = (int32_t*)ctx->pinned(nm + "_to_h", (size_t)nc * 4);
+        if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref || !dprep || !htab || !hflag || !hcnt ||
+            !hcoef || !hprep || !hto)
+            return ctx->fail(PITT_E_NOMEM, nm + " scratch");
+        st.assign((size_t)nc, St{});
+        cur.assign((size_t)nc, Coef{});
+        log_probability = std::log(1.0 - m.probability);
+        return PITT_OK;
+    }
+
+    // 1. every cloud's hypotheses and their validity flags
+    int issue_hyp() override {
+        for (int c = 0; c < nc; ++c) {
+            if (cl[c].n < M::kSample) continue;
+            st[(size_t)c].run = true;
+            const std::vector<int32_t>& tab = sampler_table(ctx, cl[c].n, m.seed, A, M::kSample);
+            int32_t* ht = htab + (size_t)c * A * M::kSample;
+            std::copy(tab.begin(), tab.end(), ht);
+            int32_t* dt = dtab + (size_t)c * A * M::kSample;
+            PITT_HIP_TRY(hipMemcpyAsync(dt, ht, (size_t)A * M::kSample * 4, hipMemcpyHostToDevice, s));
+            const int rec = ctx->prof_begin((nm + "_model").c_str(), (double)A * M::kModelBytes);
+            m.launch_model(s, cl[c], dt, (int)A, dcoef + (size_t)c * A, dflag + (size_t)c * A);
+            ctx->prof_end(rec);
+            PITT_HIP_TRY(hipGetLastError());
+            PITT_HIP_TRY(hipMemcpyAsync(hflag + (size_t)c * A, dflag + (size_t)c * A, (size_t)A * 4,
+                                        hipMemcpyDeviceToHost, s));
+        }
+        return PITT_OK;
+    }
+
+    // 2. the next chunk of attempts of every cloud still running (*any: something was enqueued)
+    int issue_chunk(int chunk, bool* any) override {
+        *any = false;
+        for (int c = 0; c < nc && !*any; ++c) *any = st[(size_t)c].run;
+        if (!*any) return PITT_OK;
+        // one zeroed [nc][256] count block per chunk, read back whole
+        PITT_HIP_TRY(hipMemsetAsync(dcnt, 0, (size_t)nc * 256 * 4, s));
         for (int c = 0; c < nc; ++c) {
             St& q = st[(size_t)c];
             if (!q.run) continue;
-            any = true;
             const int64_t a1 = std::min<int64_t>(A, q.a + chunk);
             const int nh = (int)(a1 - q.a);
-            int32_t* dc = dcnt + (size_t)c * A + q.a;
-            PITT_HIP_TRY(hipMemsetAsync(dc, 0, (size_t)nh * 4, s));
             const int rec = ctx->prof_begin((nm + "_count").c_str(), (double)nh * (double)cl[c].n * M::kCountBytes);
-            m.launch_count(s, cl[c], dcoef + (size_t)c * A, dflag + (size_t)c * A, (int)q.a, nh, dc);
+            m.launch_count(s, cl[c], dcoef + (size_t)c * A, dflag + (size_t)c * A, (int)q.a, nh, dcnt + (size_t)c * 256);
             ctx->prof_end(rec);
             PITT_HIP_TRY(hipGetLastError());
-            PITT_HIP_TRY(hipMemcpyAsync(hcnt + (size_t)c * 256, dc, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
         }
-        if (!any) break;
-        PITT_HIP_TRY(hipStreamSynchronize(s));
+        PITT_HIP_TRY(hipMemcpyAsync(hcnt, dcnt, (size_t)nc * 256 * 4, hipMemcpyDeviceToHost, s));
+        return PITT_OK;
+    }
+    // the serial loop replayed on the host over the chunk's counts
+    void consume_chunk(int chunk) override {
         for (int c = 0; c < nc; ++c) {
             St& q = st[(size_t)c];
             if (!q.run) continue;
@@ -178,32 +238,40 @@ int prim_ransac_batch(pitt_ctx* ctx, const M& m, const PrimCloud* cl, int nc, Pr
     }
 
     // 3. the winning models
-    bool any_model = false;
-    for (int c = 0; c < nc; ++c) {
-        res[c].hypotheses = st[(size_t)c].iterations;
-        if (st[(size_t)c].best < 0) continue;
-        any_model = true;
-        PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dcoef + (size_t)c * A + st[(size_t)c].best, sizeof(Coef),
-                                    hipMemcpyDeviceToHost, s));
+    int issue_best() override {
+        any_model = false;
+        with_model.clear();
+        for (int c = 0; c < nc; ++c) {
+            res[c].hypotheses = st[(size_t)c].iterations;
+            if (st[(size_t)c].best < 0) continue;
+            any_model = true;
+            with_model.push_back(c);
+            PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dcoef + (size_t)c * A + st[(size_t)c].best, sizeof(Coef),
+                                        hipMemcpyDeviceToHost, s));
+        }
+        return PITT_OK;
     }
-    if (!any_model) return PITT_OK;
-    PITT_HIP_TRY(hipStreamSynchronize(s));
-    std::vector<Coef> cur((size_t)nc);
-    for (int c = 0; c < nc; ++c) cur[(size_t)c] = hcoef[c];
+    void read_best() override {
+        for (int c : with_model) cur[(size_t)c] = hcoef[c];
+        sel = with_model;
+    }
 
-    // 4. selectWithinDistance of the clouds in `which`
-    auto select = [&](const std::vector<int>& which) -> int {
-        if (which.empty()) return PITT_OK;
+    // 4. selectWithinDistance of the clouds in `sel`: isModelValid (+ the predicate's constants) first,
+    //    on the device for the cone
+    bool needs_prep_sync() const override { return M::kDevicePrep && !sel.empty(); }
+    int issue_prep() override {
         if constexpr (M::kDevicePrep) {
-            for (int c : which) m.launch_prep(s, cur[(size_t)c], dprep + c);
+            for (int c : sel) m.launch_prep(s, cur[(size_t)c], dprep + c);
             PITT_HIP_TRY(hipGetLastError());
             PITT_HIP_TRY(hipMemcpyAsync(hprep, dprep, (size_t)nc * sizeof(Prep), hipMemcpyDeviceToHost, s));
-            PITT_HIP_TRY(hipStreamSynchronize(s));
-        } else {
-            for (int c : which) m.prep_host(cur[(size_t)c], hprep + c);
         }
-        bool launched = false;
-        for (int c : which) {
+        return PITT_OK;
+    }
+    int issue_select() override {
+        launched = false;
+        if constexpr (!M::kDevicePrep)
+            for (int c : sel) m.prep_host(cur[(size_t)c], hprep + c);
+        for (int c : sel) {
             res[c].n_inliers = 0;
             hto[c] = 0;
             if (!m.prep_valid(hprep[c])) continue;
@@ -215,41 +283,138 @@ int prim_ransac_batch(pitt_ctx* ctx, const M& m, const PrimCloud* cl, int nc, Pr
             PITT_HIP_TRY(hipMemcpyAsync(hto + c, cto + nt, 4, hipMemcpyDeviceToHost, s));
             launched = true;
         }
-        if (launched) PITT_HIP_TRY(hipStreamSynchronize(s));
-        for (int c : which) res[c].n_inliers = hto[c];
         return PITT_OK;
-    };
-    std::vector<int> with_model;
-    for (int c = 0; c < nc; ++c)
-        if (st[(size_t)c].best >= 0) with_model.push_back(c);
-    int rc = select(with_model);
-    if (rc != PITT_OK) return rc;
+    }
+    void read_select() override {
+        for (int c : sel) res[c].n_inliers = hto[c];
+    }
 
-    // 5. optimizeModelCoefficients, then the selection with the refined model
-    if (m.optimize) {
-        std::vector<int> refined;
+    // 5. optimizeModelCoefficients: the refinements of all clouds with at most LmP::kSmall inliers in one
+    //    launch (one block each, lm.hpp k_lm_batch), the larger ones on their own grid, the refined models
+    //    back; then the selection again with them
+    int issue_refine() override {
+        refined.clear();
+        if (!m.optimize) return PITT_OK;
+        using LmP = typename M::LmP;
+        std::vector<LmJob<LmP>> jobs;
         for (int c : with_model) {
-            if (!m.refine_kind(res[c].n_inliers)) continue;
+            const int kind = m.refine_kind(res[c].n_inliers);
+            if (!kind) continue;
             const int rec = ctx->prof_begin((nm + "_lm").c_str(), (double)res[c].n_inliers * 12.0);
-            rc = m.launch_refine(ctx, s, cl[c], cur[(size_t)c], res[c].n_inliers, dref + c);
-            if (rc != PITT_OK) return rc;
+            if (kind == 2) {
+                m.launch_normalize(s, cur[(size_t)c], dref + c);
+            } else if (res[c].n_inliers <= LmP::kSmall) {
+                jobs.push_back(LmJob<LmP>{m.lm_params(cur[(size_t)c]), cl[c].x, cl[c].y, cl[c].z, cl[c].inliers,
+                                          res[c].n_inliers, dref + c});
+            } else {
+                const int rc = launch_lm(ctx, s, m.lm_params(cur[(size_t)c]), cl[c].x, cl[c].y, cl[c].z,
+                                         cl[c].inliers, res[c].n_inliers, dref + c, (nm + "_lm_global").c_str());
+                if (rc != PITT_OK) return rc;
+            }
             ctx->prof_end(rec);
-            PITT_HIP_TRY(hipGetLastError());
-            PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dref + c, sizeof(Coef), hipMemcpyDeviceToHost, s));
             refined.push_back(c);
         }
-        if (!refined.empty()) {
-            PITT_HIP_TRY(hipStreamSynchronize(s));
-            for (int c : refined) cur[(size_t)c] = hcoef[c];
-            rc = select(refined);
-            if (rc != PITT_OK) return rc;
+        const int rc = launch_lm_batch(ctx, s, jobs, M::kName);
+        if (rc != PITT_OK) return rc;
+        PITT_HIP_TRY(hipGetLastError());
+        for (int c : refined) PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dref + c, sizeof(Coef), hipMemcpyDeviceToHost, s));
+        return PITT_OK;
+    }
+    void read_refine() override {
+        for (int c : refined) cur[(size_t)c] = hcoef[c];
+        sel = refined;
+    }
+
+    void finish() override {
+        for (int c : with_model) {
+            res[c].status = PITT_OK;
+            M::to_out(cur[(size_t)c], res[c].coef);
         }
     }
-    for (int c : with_model) {
-        res[c].status = PITT_OK;
-        M::to_out(cur[(size_t)c], res[c].coef);
+};
+
+// Several runs (different models, the same clouds or not) in lockstep on one stream: each phase is
+// enqueued for every run, then one synchronisation serves them all.  Every run's own launches keep their
+// order, so each result is that of its run alone.
+// streams: one per run (nullptr / absent: the context's), so that the runs' small launches overlap on
+// the device; a phase's synchronisation then waits for all of them.
+inline int prim_ransac_lockstep(pitt_ctx* ctx, const std::vector<PrimRunBase*>& runs,
+                                const std::vector<hipStream_t>& streams = {}) {
+    std::vector<hipStream_t> used;
+    for (size_t i = 0; i < runs.size(); ++i) {
+        hipStream_t st = i < streams.size() && streams[i] ? streams[i] : ctx->stream;
+        runs[i]->set_stream(st);
+        if (std::find(used.begin(), used.end(), st) == used.end()) used.push_back(st);
     }
-    return PITT_OK;
+    auto sync = [&]() -> int {
+        for (hipStream_t st : used) PITT_HIP_TRY(hipStreamSynchronize(st));
+        return PITT_OK;
+    };
+    int rc;
+    for (PrimRunBase* r : runs)
+        if ((rc = r->setup()) != PITT_OK) return rc;
+    bool work = false;
+    for (PrimRunBase* r : runs) work = work || r->nc > 0;
+    if (!work) return PITT_OK;
+    for (PrimRunBase* r : runs)
+        if ((rc = r->issue_hyp()) != PITT_OK) return rc;
+    if ((rc = sync()) != PITT_OK) return rc;
+    for (int chunk = 32;; chunk = std::min(chunk * 2, 256)) {
+        bool any = false;
+        for (PrimRunBase* r : runs) {
+            bool a = false;
+            if ((rc = r->issue_chunk(chunk, &a)) != PITT_OK) return rc;
+            any = any || a;
+        }
+        if (!any) break;
+        if ((rc = sync()) != PITT_OK) return rc;
+        for (PrimRunBase* r : runs) r->consume_chunk(chunk);
+    }
+    bool models = false;
+    for (PrimRunBase* r : runs) {
+        if ((rc = r->issue_best()) != PITT_OK) return rc;
+        models = models || r->any_model;
+    }
+    if (!models) return PITT_OK;
+    if ((rc = sync()) != PITT_OK) return rc;
+    for (PrimRunBase* r : runs) r->read_best();
+    auto select_phase = [&]() -> int {
+        bool prep = false;
+        for (PrimRunBase* r : runs) prep = prep || r->needs_prep_sync();
+        int e;
+        if (prep) {
+            for (PrimRunBase* r : runs)
+                if ((e = r->issue_prep()) != PITT_OK) return e;
+            if ((e = sync()) != PITT_OK) return e;
+        }
+        bool any = false;
+        for (PrimRunBase* r : runs) {
+            if ((e = r->issue_select()) != PITT_OK) return e;
+            any = any || r->launched;
+        }
+        if (any && (e = sync()) != PITT_OK) return e;
+        for (PrimRunBase* r : runs) r->read_select();
+        return PITT_OK;
+    };
+    if ((rc = select_phase()) != PITT_OK) return rc;
+    bool refine = false;
+    for (PrimRunBase* r : runs) {
+        if ((rc = r->issue_refine()) != PITT_OK) return rc;
+        refine = refine || !r->refined.empty();
+    }
+    if (refine) {
+        if ((rc = sync()) != PITT_OK) return rc;
+        for (PrimRunBase* r : runs) r->read_refine();
+        if ((rc = select_phase()) != PITT_OK) return rc;
+    }
+    for (PrimRunBase* r : runs) r->finish();
+    return sync();  // every stream idle: the inlier lists are complete for whoever reads them next
+}
+
+template <class M>
+int prim_ransac_batch(pitt_ctx* ctx, const M& m, const PrimCloud* cl, int nc, PrimResult* res) {
+    PrimRun<M> run(ctx, m, cl, nc, res);
+    return prim_ransac_lockstep(ctx, {&run});
 }
 
 }  // namespace pitt

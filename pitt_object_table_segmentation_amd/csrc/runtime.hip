@@ -192,6 +192,8 @@ int pitt_create(pitt_ctx** out, int hip_device) {
 
 void pitt_destroy(pitt_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->aux) pitt_destroy(ctx->aux);
+    ctx->aux = nullptr;
     (void)pitt::finish_batch(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -206,6 +208,12 @@ void pitt_destroy(pitt_ctx* ctx) {
         (void)hipEventDestroy(r.b);
     }
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (hipStream_t& sd : ctx->side)
+        if (sd) {
+            (void)hipStreamSynchronize(sd);
+            (void)hipStreamDestroy(sd);
+            sd = nullptr;
+        }
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }

@@ -198,11 +198,10 @@ struct SphModel {
     }
     // more than 4 inliers: Levenberg-Marquardt in double, the whole iteration in one launch (the
     // oracle's sphere_refine; fixed reduction order, so the same bits on every run)
+    using LmP = SphLmModel;
     static int refine_kind(int64_t n_inliers) { return n_inliers > 4 ? 1 : 0; }
-    int launch_refine(pitt_ctx* ctx, hipStream_t s, const PrimCloud& c, const float4& bc, int64_t n_inl,
-                      float4* out) const {
-        return launch_lm(ctx, s, SphLmModel{bc}, c.x, c.y, c.z, c.inliers, n_inl, out);
-    }
+    static SphLmModel lm_params(const float4& bc) { return SphLmModel{bc}; }
+    void launch_normalize(hipStream_t, const float4&, float4*) const {}
 };
 
 SphModel sph_model(const pitt_sphere_params* p) {
@@ -210,9 +209,14 @@ SphModel sph_model(const pitt_sphere_params* p) {
                     float_threshold(p->threshold)};
 }
 
-// A batch of sphere services (pitt_classify_clusters): one host synchronisation per phase.
+// A batch of sphere services: one host synchronisation per phase.
 int sphere_batch(pitt_ctx* ctx, const pitt_sphere_params* p, const PrimCloud* cl, int nc, PrimResult* res) {
     return prim_ransac_batch(ctx, sph_model(p), cl, nc, res);
+}
+// The same as a run of prim_ransac_lockstep (pitt_classify_clusters).
+std::unique_ptr<PrimRunBase> sphere_run(pitt_ctx* ctx, const pitt_sphere_params* p, const PrimCloud* cl, int nc,
+                                        PrimResult* res) {
+    return std::make_unique<PrimRun<SphModel>>(ctx, sph_model(p), cl, nc, res);
 }
 
 }  // namespace pitt

@@ -185,3 +185,23 @@ def test_primitive_arbitration():
         assert a(*map(int, c)) == ref(*map(int, c)), c
     with pytest.raises(pitt.PittError):
         a(-1, 0, 0, 0)
+
+
+def test_classify_params_defaults():
+    """pitt_classify_params_default holds the four handlers' defaults (sphere_segmentation_srv.cpp:20-23,
+    cylinder_segmentation_srv.cpp:23-27, cone_segmentation_srv.cpp:24-31), k = 50 (pc_manager.cpp:18) and
+    the cone-over-cylinder priority (ransac_segmentation.cpp:37); the ctypes mirrors match the C layout."""
+    import ctypes
+    import math
+    from pitt_object_table_segmentation_amd import _lib as L
+    assert ctypes.sizeof(L.ClassifyParams) == 264 and ctypes.sizeof(L.ClusterShape) == 240
+    p = pitt.classify_params()
+    assert p.k == 50 and abs(p.cone_over_cylinder - 0.9) < 1e-7
+    assert (p.sphere.threshold, p.sphere.radius_min, p.sphere.radius_max) == (0.007, 0.005, 0.5)
+    assert (p.cylinder.threshold, p.cylinder.normal_distance_weight) == (0.008, 0.001)
+    assert (p.cone.threshold, p.cone.normal_distance_weight, p.cone.eps_angle) == (0.0055, 0.0006, 0.4)
+    assert math.isclose(p.cone.min_angle, math.radians(10)) and math.isclose(p.cone.max_angle, math.radians(170))
+    for m in (p.sphere, p.cylinder, p.cone):
+        assert (m.max_iterations, m.optimize, m.probability) == (1000, 1, 0.99)
+    q = pitt.classify_params(k=20)
+    assert q.k == 20 and q.sphere.threshold == 0.007
