@@ -256,6 +256,7 @@ SIGNATURES = {
     "pitt_cluster_params_default": (None, [ctypes.POINTER(ClusterParams)]),
     "pitt_memcpy": (_i32, [_vp, _vp, _vp, _i64]),
     "pitt_graph_stats": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "pitt_refine_stats": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "pitt_segment_objects_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SupportParams),
                                         ctypes.POINTER(ClusterParams), ctypes.POINTER(Scene)]),
     "pitt_synth_frame": (_i32, [_i32, ctypes.c_uint64, _i32, _i32, _f32p, _f32p, _f32p]),

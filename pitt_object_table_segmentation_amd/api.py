@@ -480,6 +480,12 @@ class Context:
         self._check(lib.pitt_graph_stats(self.h, ctypes.byref(c), ctypes.byref(r)), "pitt_graph_stats")
         return c.value, r.value
 
+    def refine_stats(self):
+        """(batches refined by k_xrefine, frames it handed back to k_refine's serial chain)."""
+        b, f = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(lib.pitt_refine_stats(self.h, ctypes.byref(b), ctypes.byref(f)), "pitt_refine_stats")
+        return b.value, f.value
+
     # ---- device-resident support / cluster path (pitt_*_dev) ---------------------------------
     def _dev_copy(self, ptr, n: int, dtype, device):
         """A fresh device tensor holding n elements copied from a device address of the arena."""

@@ -85,6 +85,10 @@ struct pitt_ctx {
     int refine_producers = pitt_env_int("PITT_REFINE_PRODUCERS", PITT_REFINE_PRODUCERS_DEFAULT, 1, 4);
     // k_refine variant (bit 1: producers write inlier lanes only, as masked stores)
     int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 3);
+    // $PITT_XREFINE=1: optimizeModelCoefficients' sums by binade runs (k_xrefine, bit-exact, measured
+    // slower than k_refine's chain: DESIGN.md s6); 2: k_xrefine hands every frame back (tests)
+    int xrefine = pitt_env_int("PITT_XREFINE", 0, 0, 2);
+    int64_t xrefine_batches = 0, xrefine_fallbacks = 0;  // frames k_xrefine handed back to k_refine
     // $PITT_REFINE_DEBUG=1: k_refine records per-role cycles and spins, printed at completion
     bool refine_debug = pitt_env_flag("PITT_REFINE_DEBUG", false);
     void* refine_dbg_h = nullptr;
@@ -117,6 +121,7 @@ struct pitt_ctx {
     int inflight_frames = 0;
     void* inflight_hres = nullptr;
     void* inflight_hstat = nullptr;
+    void* inflight_xfb = nullptr;   // k_xrefine fallback count (pinned), when it ran
     std::vector<std::pair<int64_t, int64_t>> inflight_stat;
     std::vector<int> inflight_score_recs;
     std::vector<int> inflight_chunks;

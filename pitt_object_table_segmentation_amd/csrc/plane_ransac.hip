@@ -1297,12 +1297,13 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
     int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct,
-    unsigned long long* __restrict__ rdbg, int mode) {
+    unsigned long long* __restrict__ rdbg, int mode, const int32_t* __restrict__ only) {
     __shared__ RefineLds<P> L;
     const long long t_start = rdbg ? clock64() : 0;
     const int f = blockIdx.x;
     const FrameState s = st[f];
     if (!s.has_model || !s.need_refine) return;
+    if (only && !only[f]) return;  // after k_xrefine: only the frames it handed back
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -1363,6 +1364,339 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
             rdbg[(int64_t)f * 16 + 1] = spins;
             rdbg[(int64_t)f * 16 + 12] = (unsigned long long)n_in;
             rdbg[(int64_t)f * 16 + 13] = (unsigned long long)busy;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_xrefine: the same nine exact-order float sums (A6: accu[k] += v in ascending inlier order,
+// computeMeanAndCovarianceMatrix, called from optimizeModelCoefficients at
+// plane_segmentation_srv.cpp:55,67) without one dependent add per inlier ("binade runs").
+//
+// While a float sum s stays inside one binade [2^e, 2^(e+1)) (or its negative), every add rounds
+// to the same grid u = 2^(e-23), and s is a multiple of u.  So fl(s + v) = s + q u with
+// q = rint(v / u) whenever the exact sum is not a tie (|v/u - q| != 1/2) and the result stays
+// at least one u inside the binade: the rounding does not depend on s.  A run of elements then
+// advances s by R u with R = sum q, an integer computed in parallel, and it is valid for the actual
+// s exactly when every partial sum s + (q_1 + ... + q_m) u, m = 0..len, lies in
+// [2^e + u, 2^(e+1) - u] -- one integer range test on s / u against the run's prefix minimum and
+// maximum.  Only the elements where the sum crosses a binade (near zero, or at a power of two) or
+// hits a tie still need their own rounded add.
+//
+// One block per refined frame, kXW waves; per iteration each wave takes one listed tile (the tiles
+// where the winning hypothesis counted inliers, as k_refine) and lane l its 32 consecutive points.
+//   phase 1  per stream k (xx, xy, xz, yy, yz, zz, x, y, z): the lane's sum and absolute sum, a wave
+//            scan, the block's wave totals: an estimate P of the chain value at the lane's start
+//            (from the walk's exact value at the iteration start);
+//   phase 2  a lane whose estimated partial-sum range [P + neg, P + pos] (widened by a margin)
+//            stays inside one binade scores its elements on that grid: q, R, the prefix min / max
+//            and the tie test -> a RUN term (R u, the range limits); any other lane with inliers
+//            -> a SEQ term whose values are laid out in order for the walk;
+//   walk     wave 0, lane k = stream k: s += R u after the range test, or s = fl(s + v) per SEQ
+//            value, in lane-segment order (= ascending inlier order).
+// A RUN whose range test fails (an estimate off by more than the margin) marks the frame; such
+// frames are refined again by k_refine's serial chain (the fallback launch after this one), so
+// the result never depends on the estimate.  Bit-exact with k_refine by construction.
+constexpr int kXW = 4;              // waves per block = listed tiles per iteration
+constexpr int kXSeg = kTile / 64;   // points per lane segment (32)
+constexpr int kXLanes = 64 * kXW;   // lane segments (terms per stream) per iteration
+constexpr int kXCap = 1024;         // add-list entries per stream per window
+constexpr int kXVS = kXCap + 8;     // entry stride per stream (floats): streams on distinct banks
+
+struct XRefineLds {
+    int tl[kRMaxTiles];
+    float seqv[9][kXVS];  // a window of each stream's add list (then: the chain value before each entry)
+    float wsum[kXW][9];  // the waves' stream sums (estimates)
+    float wabs[kXW][9];  // and absolute sums
+    int wseq[kXW][9];    // add-list entries per wave and stream
+    float sx[9];         // the walk's exact chain value at the iteration start
+    int nact, n_in, fail;
+};
+
+// Stream k of computeMeanAndCovarianceMatrix's accumulator (PCL order): products rounded to float.
+__device__ __forceinline__ float xval(int k, float x, float y, float z) {
+    switch (k) {
+        case 0: return x * x;
+        case 1: return x * y;
+        case 2: return x * z;
+        case 3: return y * y;
+        case 4: return y * z;
+        case 5: return z * z;
+        case 6: return x;
+        case 7: return y;
+        default: return z;
+    }
+}
+
+__device__ __forceinline__ float wave_incl_f(float v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_incl_i(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// The points, opaque to the compiler: products are recomputed per phase instead of kept live.
+__device__ __forceinline__ void xopaque(float (&px)[kXSeg], float (&py)[kXSeg], float (&pz)[kXSeg]) {
+#pragma unroll
+    for (int j = 0; j < kXSeg; ++j) asm volatile("" : "+v"(px[j]), "+v"(py[j]), "+v"(pz[j]));
+}
+
+template <int ORDER, int DIV>
+__global__ __launch_bounds__(64 * kXW) void k_xrefine(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
+    float thf, const int32_t* __restrict__ tile_counts, int hstride, int tiles_max, float4* __restrict__ final_coef,
+    int32_t* __restrict__ fallback, int32_t* __restrict__ fallback_count, unsigned long long* __restrict__ acct,
+    int force_fallback, unsigned long long* __restrict__ rdbg) {
+    __shared__ XRefineLds L;
+    const long long t_start = rdbg ? clock64() : 0;
+    unsigned long long n_seq = 0, n_run = 0, n_wait = 0;
+    const int f = blockIdx.x;
+    const FrameState s = st[f];
+    if (!s.has_model || !s.need_refine) return;
+    const FrameMeta m = meta[f];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (wave == 0) {
+        const int nact = refine_tiles(L, m.tiles, lane, tile_counts + (int64_t)f * tiles_max * hstride + s.best_h,
+                                      hstride);
+        if (lane == 0) {
+            L.nact = nact;
+            L.n_in = 0;
+            L.fail = 0;
+            const int nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+            acct_add(acct, kAcRefine, (unsigned long long)nsteps * kRChunk * 12ull + (unsigned long long)m.tiles * 4ull + 32ull);
+        }
+        if (lane < 9) L.sx[lane] = 0.0f;
+    }
+    __syncthreads();
+    const int nact = L.nact;
+    const int npass = nact < 0 ? m.tiles : nact;
+    const float4 c = best_coef[f];
+    float tv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+    const int wk = lane < 9 ? lane : 0;  // the walk: wave 0, lane k = stream k
+    float ws = 0.0f;
+    for (int it = 0; it < npass; it += kXW) {
+        const int ti = it + wave;
+        const bool valid = ti < npass;
+        const int tile = valid ? (nact < 0 ? ti : L.tl[ti]) : 0;
+        const int64_t q0 = (int64_t)tile * kTile + lane * kXSeg;  // the segment's first point (in the frame)
+        float px[kXSeg], py[kXSeg], pz[kXSeg];
+        uint32_t msk = 0;
+        if (valid) {
+            const float4* gx = reinterpret_cast<const float4*>(X + m.off + q0);
+            const float4* gy = reinterpret_cast<const float4*>(Y + m.off + q0);
+            const float4* gz = reinterpret_cast<const float4*>(Z + m.off + q0);
+#pragma unroll
+            for (int i = 0; i < kXSeg / 4; ++i) {
+                const float4 a = gx[i], b = gy[i], d = gz[i];
+                px[4 * i] = a.x; px[4 * i + 1] = a.y; px[4 * i + 2] = a.z; px[4 * i + 3] = a.w;
+                py[4 * i] = b.x; py[4 * i + 1] = b.y; py[4 * i + 2] = b.z; py[4 * i + 3] = b.w;
+                pz[4 * i] = d.x; pz[4 * i + 1] = d.y; pz[4 * i + 2] = d.z; pz[4 * i + 3] = d.w;
+            }
+#pragma unroll
+            for (int j = 0; j < kXSeg; ++j) {
+                const bool in = (q0 + j < m.n) & (fabsf(plane_dot<ORDER>(c, px[j], py[j], pz[j])) < tv);
+                msk |= (in ? 1u : 0u) << j;  // NaN never counts
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kXSeg; ++j) px[j] = py[j] = pz[j] = 0.0f;
+        }
+        const int cnt = __builtin_popcount(msk);
+        // phase 1: sums per stream (estimates)
+        float sv[9], sa[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) sv[k] = sa[k] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kXSeg; ++j) {
+            const bool in = (msk >> j) & 1u;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const float v = in ? xval(k, px[j], py[j], pz[j]) : 0.0f;
+                sv[k] += v;
+                sa[k] += fabsf(v);
+            }
+        }
+        float pre[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const float inc = wave_incl_f(sv[k], lane);
+            pre[k] = inc - sv[k];
+            if (lane == 63) L.wsum[wave][k] = inc;
+            const float ab = wave_sum_f(sa[k]);
+            if (lane == 0) L.wabs[wave][k] = ab;
+        }
+        {
+            const int wc = __shfl(wave_incl_i(cnt, lane), 63, 64);
+            if (lane == 0) atomicAdd(&L.n_in, wc);
+        }
+        __syncthreads();
+        xopaque(px, py, pz);  // phase 2 recomputes the products (kept from phase 1: 288 live VGPRs)
+        // phase 2: RUN or SEQ per (lane segment, stream)
+        int ent[9], rlo[9], rhi[9], rex[9];
+        float ra[9];
+        uint32_t runbits = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            float P = L.sx[k], A = fabsf(L.sx[k]);
+#pragma unroll
+            for (int w = 0; w < kXW; ++w) {
+                if (w < wave) P += L.wsum[w][k];
+                A += L.wabs[w][k];
+            }
+            P += pre[k];
+            const float mg = A * 0x1p-14f;
+            const float pos = 0.5f * (sv[k] + sa[k]), neg = 0.5f * (sv[k] - sa[k]);
+            const float lo = (P + neg) - mg, hi = (P + pos) + mg;
+            const bool up = lo > 0.0f;
+            bool cand = cnt > 0 && (up || hi < 0.0f) && __builtin_isfinite(lo) && __builtin_isfinite(hi);
+            const float a0 = up ? lo : -hi, b0 = up ? hi : -lo;
+            int ex = 0;
+            (void)frexpf(a0, &ex);  // a0 in [2^(ex-1), 2^ex): binade e = ex - 1
+            const int e = ex - 1;
+            cand = cand && e >= -100 && e <= 125 && b0 < ldexpf(1.0f, e + 1);
+            float R = 0.0f, mn = 0.0f, mx = 0.0f, T = 0.0f;
+            if (cand) {
+                const float scale = ldexpf(1.0f, 23 - e);
+#pragma unroll
+                for (int j = 0; j < kXSeg; ++j) {
+                    const float v = ((msk >> j) & 1u) ? xval(k, px[j], py[j], pz[j]) : 0.0f;
+                    const float t = v * scale;
+                    const float q = rintf(t);
+                    T = fmaxf(T, fabsf(t - q));
+                    R += q;
+                    mn = fminf(mn, R);
+                    mx = fmaxf(mx, R);
+                }
+            }
+            const bool clean = cand && T < 0.5f && fabsf(mn) <= 0x1p25f && fabsf(mx) <= 0x1p25f;
+            // the lane's entries in the stream's add list: a RUN is one entry (R u), SEQ its values
+            ent[k] = cnt == 0 ? 0 : clean ? 1 : cnt;
+            runbits |= (cnt > 0 && clean ? 1u : 0u) << k;
+            ra[k] = clean ? ldexpf(R, e - 23) : 0.0f;  // exact: |R| <= 2^25, e >= -100
+            rlo[k] = (up ? (1 << 23) + 1 : -((1 << 24) - 1)) - (clean ? (int)mn : 0);
+            rhi[k] = (up ? (1 << 24) - 1 : -((1 << 23) + 1)) - (clean ? (int)mx : 0);
+            rex[k] = e;
+        }
+        int eoff[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int inc = wave_incl_i(ent[k], lane);
+            eoff[k] = inc - ent[k];
+            if (lane == 63) L.wseq[wave][k] = inc;
+        }
+        __syncthreads();
+        int ntot[9], nmax = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            ntot[k] = 0;
+#pragma unroll
+            for (int w = 0; w < kXW; ++w) {
+                if (w < wave) eoff[k] += L.wseq[w][k];
+                ntot[k] += L.wseq[w][k];
+            }
+            nmax = max(nmax, ntot[k]);
+        }
+        // windows of kXCap entries per stream: laid out, walked (each entry replaced by the chain
+        // value before it), then the window's RUN entries checked by the lanes that made them
+        for (int wb = 0; wb < nmax; wb += kXCap) {
+            xopaque(px, py, pz);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                if (ent[k] > 0 && eoff[k] < wb + kXCap && eoff[k] + ent[k] > wb) {
+                    if ((runbits >> k) & 1u) {
+                        L.seqv[k][eoff[k] - wb] = ra[k];
+                    } else {
+                        int r = eoff[k] - wb;
+#pragma unroll
+                        for (int j = 0; j < kXSeg; ++j) {
+                            if ((msk >> j) & 1u) {
+                                if (r >= 0 && r < kXCap) L.seqv[k][r] = xval(k, px[j], py[j], pz[j]);
+                                ++r;
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (wave == 0 && lane < 9) {
+                int nk = 0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) nk = wk == k ? ntot[k] : nk;
+                const int hi = min(nk - wb, kXCap);
+                float4* v = reinterpret_cast<float4*>(&L.seqv[wk][0]);
+                float4 cur = v[0], nxt = v[1];
+                for (int j = 0; j < hi; j += 4) {
+                    const float4 nn = v[(j >> 2) + 2];  // within the stride's padding at the end
+                    float4 pz4;
+                    const float a0 = j < hi ? cur.x : 0.0f, a1 = j + 1 < hi ? cur.y : 0.0f;
+                    const float a2 = j + 2 < hi ? cur.z : 0.0f, a3 = j + 3 < hi ? cur.w : 0.0f;
+                    pz4.x = ws;
+                    ws = ws + a0;
+                    pz4.y = ws;
+                    ws = ws + a1;
+                    pz4.z = ws;
+                    ws = ws + a2;
+                    pz4.w = ws;
+                    ws = ws + a3;
+                    v[j >> 2] = pz4;
+                    cur = nxt;
+                    nxt = nn;
+                }
+                n_seq += (unsigned long long)max(hi, 0);
+                if (wb + kXCap >= nk) L.sx[wk] = ws;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                if (((runbits >> k) & 1u) && eoff[k] >= wb && eoff[k] < wb + kXCap) {
+                    const float sb = L.seqv[k][eoff[k] - wb];  // the chain value before the run
+                    const float ts = sb * ldexpf(1.0f, 23 - rex[k]);  // s / u, exact when in range
+                    const bool ok = fabsf(ts) < 0x1p26f && (int)ts >= rlo[k] && (int)ts <= rhi[k];
+                    if (!ok) L.fail = 1;
+                    ++n_run;
+                }
+            }
+            __syncthreads();  // the window's checks read the values the next window replaces
+            ++n_wait;
+        }
+    }
+    if (wave == 0) {
+        float a9[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = __shfl(ws, k, 64);
+        const bool fail = force_fallback || L.fail != 0;
+        if (rdbg && lane < 9) {
+            rdbg[(int64_t)f * 16 + 3 + lane] = n_seq;  // 3..11: SEQ values per stream
+            if (lane == 0) rdbg[(int64_t)f * 16 + 13] = n_run;
+        }
+        if (lane == 0) {
+            if (rdbg) {  // PITT_REFINE_DEBUG: cycles, windows, RUN terms and SEQ values (stream 0, max)
+                rdbg[(int64_t)f * 16 + 0] = (unsigned long long)(clock64() - t_start);
+                rdbg[(int64_t)f * 16 + 1] = (unsigned long long)npass;
+                rdbg[(int64_t)f * 16 + 2] = n_wait;
+                rdbg[(int64_t)f * 16 + 12] = (unsigned long long)L.n_in;
+            }
+            if (!fail) final_coef[f] = refine_plane<ORDER, DIV>(a9, L.n_in);
+            else atomicAdd(fallback_count, 1);
+            fallback[f] = fail ? 1 : 0;
         }
     }
 }
@@ -1697,7 +2031,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     FrameState* st = as<FrameState>(ctx->buf("state", (size_t)nf * sizeof(FrameState)));
     int32_t* lists = as<int32_t>(ctx->buf("lists", (size_t)(nchunks + 1) * nf * 4));
     // counters + chunk stats in one zeroed block
-    const size_t cnt_bytes = (size_t)(nchunks + 1) * 4;
+    const size_t cnt_bytes = (size_t)(nchunks + 2) * 4;  // + k_xrefine's fallback count
     const size_t stat_off = (cnt_bytes + 15) & ~(size_t)15;
     const size_t acct_off = stat_off + (size_t)(nchunks + 1) * sizeof(ChunkStat);
     const size_t acct_bytes = (size_t)kAcKernels * kAcShards * sizeof(unsigned long long);
@@ -1724,6 +2058,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
     if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    int32_t* xfallback = ctx->xrefine ? as<int32_t>(ctx->buf("xfallback", (size_t)nf * 4)) : nullptr;
+    if (ctx->xrefine && !xfallback) return ctx->fail(PITT_E_NOMEM, "refinement flags");
     CovPart* part = nullptr;
     if (p->cov_mode == PITT_COV_FAST) {
         part = as<CovPart>(ctx->buf("cov_part", (size_t)nf * tiles_max * sizeof(CovPart)));
@@ -1731,6 +2067,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
     ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
+    int32_t* hxfb = as<int32_t>(ctx->pinned("xfb_h", 16));
+    if (!hxfb) return ctx->fail(PITT_E_NOMEM, "pinned results");
     void* hacct = acct ? ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4) : nullptr;
     if (!hres || !hstat || (acct && !hacct)) return ctx->fail(PITT_E_NOMEM, "pinned results");
     // $PITT_REFINE_DEBUG: k_refine's per-role cycles and spin counts, summarised on stderr by pitt_wait
@@ -1794,14 +2132,29 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         hipLaunchKernelGGL((k_cov_final<ORDER>), dim3(nf), dim3(64), 0, sm, meta, st, part, nf, tiles_max, final_coef);
         ctx->prof_end(rec);
     } else {
-        rec = ctx->prof_begin("k_refine", 0.0);
-        acct_recs[kAcRefine] = rec;
         const int P = ctx->refine_producers;
         auto kern = P == 1 ? k_refine<ORDER, DIV, 1> : P == 2 ? k_refine<ORDER, DIV, 2>
                   : P == 3 ? k_refine<ORDER, DIV, 3> : k_refine<ORDER, DIV, 4>;
-        hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
-                           thf, tile_counts, hstride, tiles_max, final_coef, acct, rdbg, ctx->refine_mode);
-        ctx->prof_end(rec);
+        if (ctx->xrefine) {  // binade runs; k_refine's chain only for frames it hands back
+            rec = ctx->prof_begin("k_xrefine", 0.0);
+            acct_recs[kAcRefine] = rec;
+            hipLaunchKernelGGL((k_xrefine<ORDER, DIV>), dim3(nf), dim3(64 * kXW), 0, sm, fr->x, fr->y, fr->z, meta, st,
+                               best_coef, thf, tile_counts, hstride, tiles_max, final_coef, xfallback,
+                               counters + nchunks + 1, acct, ctx->xrefine == 2 ? 1 : 0, rdbg);
+            ctx->prof_end(rec);
+            rec = ctx->prof_begin("k_refine:fallback", 0.0);
+            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+                               thf, tile_counts, hstride, tiles_max, final_coef, nullptr, rdbg, ctx->refine_mode,
+                               xfallback);
+            ctx->prof_end(rec);
+        } else {
+            rec = ctx->prof_begin("k_refine", 0.0);
+            acct_recs[kAcRefine] = rec;
+            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+                               thf, tile_counts, hstride, tiles_max, final_coef, acct, rdbg, ctx->refine_mode,
+                               nullptr);
+            ctx->prof_end(rec);
+        }
     }
     rec = ctx->prof_begin("k_sel_mark", 0.0);
     acct_recs[kAcSelMark] = rec;
@@ -1818,6 +2171,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     PITT_HIP_TRY(hipGetLastError());
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipMemcpyAsync(hxfb, counters + nchunks + 1, 4, hipMemcpyDeviceToHost, sm));
     if (rdbg) PITT_HIP_TRY(hipMemcpyAsync(ctx->refine_dbg_h, rdbg, (size_t)nf * 16 * 8, hipMemcpyDeviceToHost, sm));
     if (acct) {
         PITT_HIP_TRY(hipMemcpyAsync(hacct, acct, acct_bytes, hipMemcpyDeviceToHost, sm));
@@ -1839,7 +2193,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uintptr_t)inliers_dev, (uint64_t)A, (uint64_t)hcap,
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
                                      (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV),
-                                     (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode};
+                                     (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
+                                     (uint64_t)ctx->xrefine};  // 2: every frame handed back (tests)
         pitt_ctx::GraphEntry* hit = nullptr;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
@@ -1898,6 +2253,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ctx->inflight_score_recs = score_recs;
     ctx->inflight_chunks = chunks;
     ctx->inflight_hstat = hstat;
+    ctx->inflight_xfb = (ctx->xrefine && p->optimize && p->cov_mode != PITT_COV_FAST) ? hxfb : nullptr;
     ctx->inflight_acct = hacct;
     ctx->inflight_acct_tiles = (int64_t)tile_words;
     ctx->inflight_acct_recs = acct_recs;
@@ -1914,6 +2270,10 @@ int finish_batch(pitt_ctx* ctx) {
     ctx->inflight = false;
     PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     std::memcpy(ctx->inflight_results, ctx->inflight_hres, (size_t)ctx->inflight_frames * sizeof(pitt_plane_result));
+    if (ctx->inflight_xfb) {
+        ++ctx->xrefine_batches;
+        ctx->xrefine_fallbacks += *(const int32_t*)ctx->inflight_xfb;
+    }
     if (ctx->refine_debug && ctx->refine_dbg_h) {  // mean / max over the refined frames, cycles
         const unsigned long long* d = (const unsigned long long*)ctx->refine_dbg_h;
         double sum[16] = {0}, mx[16] = {0};
@@ -1930,9 +2290,13 @@ int finish_batch(pitt_ctx* ctx) {
             static const char* names[14] = {"chain_cyc", "chain_spin", "form_cyc", "form_spin(hi:data lo:slot)",
                                             "p0_cyc", "p0_ticket", "p0_ring", "steps", "p1_cyc", "p1_ticket",
                                             "p1_ring", "p1_steps", "inliers", "chain_busy"};
-            std::fprintf(stderr, "[refine_debug] frames %d producers %d\n", cnt, ctx->refine_producers);
+            static const char* xnames[14] = {"cyc", "tiles", "windows", "list_xx", "list_xy", "list_xz", "list_yy",
+                                             "list_yz", "list_zz", "list_x", "list_y", "list_z", "inliers", "-"};
+            const char* const* nm = ctx->xrefine ? xnames : names;
+            std::fprintf(stderr, "[refine_debug] frames %d producers %d xrefine %d\n", cnt, ctx->refine_producers,
+                         ctx->xrefine);
             for (int k = 0; k < 14; ++k)
-                std::fprintf(stderr, "[refine_debug] %-28s mean %14.1f max %14.1f\n", names[k], sum[k] / cnt, mx[k]);
+                std::fprintf(stderr, "[refine_debug] %-28s mean %14.1f max %14.1f\n", nm[k], sum[k] / cnt, mx[k]);
         }
     }
     const ChunkStat* hstat = (const ChunkStat*)ctx->inflight_hstat;

@@ -237,6 +237,13 @@ int pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays) {
     return PITT_OK;
 }
 
+int pitt_refine_stats(pitt_ctx* ctx, int64_t* batches, int64_t* fallback_frames) {
+    if (!ctx) return PITT_E_INVALID;
+    if (batches) *batches = ctx->xrefine_batches;
+    if (fallback_frames) *fallback_frames = ctx->xrefine_fallbacks;
+    return PITT_OK;
+}
+
 int pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     if (!ctx) return PITT_E_INVALID;
     if (bytes < 0 || (bytes > 0 && (!dst || !src))) return ctx->fail(PITT_E_INVALID, "null argument");

@@ -41,8 +41,9 @@ def _check(ctx, frames, res, inls, frame_ids=None, **kw):
         assert r["rejected_samples"] == o.rejected_samples, tag
         assert np.array_equal(ctx.hypothesis_counts(i, o.hypotheses), o.hyp_counts), tag
         assert np.array_equal(inl, o.inliers), tag
-        assert np.array_equal(r["coefficients"], o.coefficients), tag
-        assert np.max(np.abs(r["coefficients"] - o.coefficients)) <= 1e-5
+        assert np.array_equal(r["coefficients"], o.coefficients, equal_nan=True), tag  # NaN: degenerate covariance
+        if np.all(np.isfinite(o.coefficients)):
+            assert np.max(np.abs(r["coefficients"] - o.coefficients)) <= 1e-5
         assert r["flags"] == 0, tag
 
 

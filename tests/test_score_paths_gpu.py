@@ -4,7 +4,10 @@ lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only
 added into lane-private counters).  $PITT_LANE_SCORE picks one when a context is created; the other
 is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
 producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel and appending in
-step order): every count must give the same ascending inlier stream, hence the same floats."""
+step order): every count must give the same ascending inlier stream, hence the same floats.  The
+refinement itself has two paths: k_refine's serial chain (default) and k_xrefine's binade runs
+($PITT_XREFINE=1, with k_refine as the fallback for frames it hands back: $PITT_XREFINE=2 hands back
+every frame, so the fallback launch is covered too)."""
 import os
 
 import pytest
@@ -17,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 
 VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
-            {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}]
+            {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}, {"PITT_XREFINE": "1"},
+            {"PITT_XREFINE": "2"}]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=lambda v: "-".join(f"{k[5:].lower()}{x}" for k, x in v.items()))
