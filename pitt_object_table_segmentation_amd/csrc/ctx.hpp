@@ -83,8 +83,10 @@ struct pitt_ctx {
     bool lane_score = pitt_env_flag("PITT_LANE_SCORE", false);
     // producer waves of k_refine (1..4); $PITT_REFINE_PRODUCERS overrides
     int refine_producers = pitt_env_int("PITT_REFINE_PRODUCERS", PITT_REFINE_PRODUCERS_DEFAULT, 1, 4);
+    // frames per k_refine block (1: k_refine; 2, 3: k_refine_multi, one chain wave for all of them)
+    int refine_frames = pitt_env_int("PITT_REFINE_FRAMES", 1, 1, 3);
     // k_refine variant (bit 1: producers write inlier lanes only, as masked stores)
-    int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 3);
+    int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 7);  // bit 2: chain without adds (measurement)
     // $PITT_XREFINE=1: optimizeModelCoefficients' sums by binade runs (k_xrefine, bit-exact, measured
     // slower than k_refine's chain: DESIGN.md s6); 2: k_xrefine hands every frame back (tests)
     int xrefine = pitt_env_int("PITT_XREFINE", 0, 0, 2);

@@ -857,15 +857,25 @@ __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restr
 // k_sel_write.
 constexpr int kRChunk = 256;   // points per producer step (4 per lane)
 constexpr int kRSlot = 3 * kRChunk;          // floats per raw ring slot (x, y, z)
-constexpr int kRDepth = 4;     // raw steps in flight per producer
+#ifndef PITT_REFINE_DEPTH
+#define PITT_REFINE_DEPTH 4
+#endif
+constexpr int kRDepth = PITT_REFINE_DEPTH;  // raw steps in flight per producer
 #ifndef PITT_REFINE_RING
 #define PITT_REFINE_RING 1024
 #endif
 constexpr int kRRing = PITT_REFINE_RING;  // compacted-inlier ring (points, a power of two)
-constexpr int kRBlk = 256;     // chain block: products formed by all lanes, then the chains
+#ifndef PITT_REFINE_BLK
+#define PITT_REFINE_BLK 256
+#endif
+constexpr int kRBlk = PITT_REFINE_BLK;  // chain block (a multiple of 256): products formed by all lanes, then the chains
+static_assert(kRBlk % 256 == 0 && kRRing % kRBlk == 0, "chain blocks of 256-element parts that tile the ring");
 // producer waves: k_refine<.., P> is instantiated for P = 1..4, pitt_ctx::refine_producers picks
 
-constexpr int kRMaxTiles = (1 << 21) / kTile;  // tile list capacity (frames up to 2M points)
+#ifndef PITT_REFINE_MAX_TILES
+#define PITT_REFINE_MAX_TILES ((1 << 21) / kTile)
+#endif
+constexpr int kRMaxTiles = PITT_REFINE_MAX_TILES;  // tile list capacity (larger frames stream every tile)
 constexpr int kRStepsPerTile = kTile / kRChunk;
 
 // The nine chain lanes read nine different streams at the same offset in one ds_read_b128: the
@@ -1158,7 +1168,28 @@ __device__ __forceinline__ void chain32(float& s, const f4v (&v)[8]) {
                 make_float4(v[t + 3].x, v[t + 3].y, v[t + 3].z, v[t + 3].w));
 }
 
-// Former wave: the six product streams of each full 256-inlier block (formed by all 64 lanes,
+// The six product streams of the kRBlk ring entries from position r (a multiple of kRBlk: the block
+// does not wrap), 256 per pass, each lane four consecutive entries, separately rounded as PCL.
+__device__ __forceinline__ void form_block(const float* rx, int r, float* prod, int lane) {
+    const int q = r & (kRRing - 1);
+#pragma unroll
+    for (int h = 0; h < kRBlk / 256; ++h) {
+        const int e = q + 256 * h + 4 * lane;
+        const float4 x = *reinterpret_cast<const float4*>(rx + e);
+        const float4 y = *reinterpret_cast<const float4*>(rx + kRS + e);
+        const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRS + e);
+        float4* o = reinterpret_cast<float4*>(prod + 256 * h) + lane;
+        constexpr int S = kPS / 4;
+        o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
+        o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+        o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
+        o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
+        o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
+        o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
+    }
+}
+
+// Former wave: the six product streams of each full kRBlk-inlier block (formed by all 64 lanes,
 // separately rounded as PCL) into a product slot, up to kRProdSlots blocks ahead of the chain.
 template <int P>
 __device__ __forceinline__ void refine_form(RefineLds<P>& L, int lane, uint32_t& spins) {
@@ -1175,18 +1206,7 @@ __device__ __forceinline__ void refine_form(RefineLds<P>& L, int lane, uint32_t&
                     continue;
                 }
             }
-            const int q = rf & (kRRing - 1);  // multiple of kRBlk: the block does not wrap
-            const float4 x = *reinterpret_cast<const float4*>(rx + q + 4 * lane);
-            const float4 y = *reinterpret_cast<const float4*>(rx + kRS + q + 4 * lane);
-            const float4 z = *reinterpret_cast<const float4*>(rx + 2 * kRS + q + 4 * lane);
-            float4* o = reinterpret_cast<float4*>(&L.prod[(rf / kRBlk) % kRProdSlots][0]) + lane;
-            constexpr int S = kPS / 4;
-            o[0 * S] = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
-            o[1 * S] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
-            o[2 * S] = make_float4(x.x * z.x, x.y * z.y, x.z * z.z, x.w * z.w);
-            o[3 * S] = make_float4(y.x * y.x, y.y * y.y, y.z * y.z, y.w * y.w);
-            o[4 * S] = make_float4(y.x * z.x, y.y * z.y, y.z * z.z, y.w * z.w);
-            o[5 * S] = make_float4(z.x * z.x, z.y * z.y, z.z * z.z, z.w * z.w);
+            form_block(rx, rf, &L.prod[(rf / kRBlk) % kRProdSlots][0], lane);
             rf += kRBlk;
             if (lane == 0) lds_release(&L.F, rf);  // after the block's writes (in-order LDS)
             continue;
@@ -1202,7 +1222,8 @@ __device__ __forceinline__ void refine_form(RefineLds<P>& L, int lane, uint32_t&
 // the products from the former's slots, x, y, z from the inlier ring.  Lanes >= 9 repeat lane 0's
 // stream (uniform control flow: limiting the reads to 9 active lanes measured slower,
 // tools/microbench/chain_rate.hip).  The last partial block goes element by element.
-template <int P>
+// NOADD (PITT_REFINE_MODE bit 2, a measurement only, results wrong): the reads without the adds.
+template <int P, bool NOADD = false>
 __device__ __forceinline__ float refine_chain(RefineLds<P>& L, int lane, uint32_t& spins, long long& busy, bool timed) {
     const int k = lane < 9 ? lane : 0;
     float* rx = ring_x(L);
@@ -1224,14 +1245,14 @@ __device__ __forceinline__ float refine_chain(RefineLds<P>& L, int lane, uint32_
             for (int i = 0; i < kRBlk / 32; i += 2) {
                 lds_read32(B, pa + 128u * (i + 1));
                 asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-                chain32(s, A);
+                if constexpr (NOADD) s += A[0].x; else chain32(s, A);
                 if (i + 2 < kRBlk / 32) {
                     lds_read32(A, pa + 128u * (i + 2));
                     asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
                 } else {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
-                chain32(s, B);
+                if constexpr (NOADD) s += B[0].x; else chain32(s, B);
             }
             r += kRBlk;
             if (lane == 0) lds_release(&L.R, r);
@@ -1353,7 +1374,8 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
         __builtin_amdgcn_s_setprio(3);
         uint32_t spins = 0;
         long long busy = 0;
-        const float acc = refine_chain(L, lane, spins, busy, rdbg != nullptr);
+        const float acc = (mode & 4) ? refine_chain<P, true>(L, lane, spins, busy, rdbg != nullptr)
+                                     : refine_chain<P>(L, lane, spins, busy, rdbg != nullptr);
         float a9[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
@@ -1364,6 +1386,182 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
             rdbg[(int64_t)f * 16 + 1] = spins;
             rdbg[(int64_t)f * 16 + 12] = (unsigned long long)n_in;
             rdbg[(int64_t)f * 16 + 13] = (unsigned long long)busy;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_refine_multi: k_refine for F frames per block with one chain wave for all of them.  What the
+// serial chain costs the pipelined chip is its instruction count -- one wave64 v_add per inlier
+// with nine useful lanes (measured: the chain's reads without its adds, PITT_REFINE_MODE bit 2,
+// took 362k to 430k frames/s at four batches in flight, while k_refine itself only went from 670
+// to 554 us).  Here lanes 9 j + k (j < F) run stream k of frame j, so one v_add advances F frames.
+// Per frame: a producer wave (refine_stream, unchanged) and its own ring and product slots; one
+// former wave forms every frame's product blocks, round robin; the chain takes block b of every
+// frame that has one, in lockstep (a frame whose stream has ended sits out under the exec mask),
+// then each frame's tail element by element.  Per frame the same values are added in the same
+// order as k_refine: bit-exact with it.
+constexpr int kRL1Words = (int)(sizeof(RefineLds<1>) / 4);
+// frame j's LDS starts 36 j banks on (nine 4-bank streams per frame): the frames' reads of one
+// stream never land on one bank group
+constexpr int kRL1Pad = (36 - kRL1Words % 64 + 64) % 64 + 64;
+struct RefineLdsP {
+    RefineLds<1> L;
+    float pad[kRL1Pad];
+};
+
+template <int F>
+__device__ __forceinline__ void refine_form_multi(RefineLdsP (&LL)[F], int lane) {
+    int rf[F], rc[F];
+    bool fin[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+        rf[j] = rc[j] = 0;
+        fin[j] = false;
+    }
+    while (true) {
+        bool progress = false, all = true;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+            if (fin[j]) continue;
+            all = false;
+            RefineLds<1>& L = LL[j].L;
+            const int w = lds_acquire(reinterpret_cast<int*>(&L.WS));
+            if (w - rf[j] >= kRBlk) {
+                if (rf[j] - rc[j] >= kRProdSlots * kRBlk) {  // both slots still being summed
+                    rc[j] = lds_acquire(&L.R);
+                    if (rf[j] - rc[j] >= kRProdSlots * kRBlk) continue;
+                }
+                form_block(ring_x(L), rf[j], &L.prod[(rf[j] / kRBlk) % kRProdSlots][0], lane);
+                rf[j] += kRBlk;
+                if (lane == 0) lds_release(&L.F, rf[j]);  // after the block's writes (in-order LDS)
+                progress = true;
+            } else if (lds_acquire(&L.done) && lds_acquire(reinterpret_cast<int*>(&L.WS)) - rf[j] < kRBlk) {
+                fin[j] = true;  // the rest is the chain's tail
+            }
+        }
+        if (all) break;
+        if (!progress) __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int F, bool NOADD>
+__device__ __forceinline__ float refine_chain_multi(RefineLdsP (&LL)[F], int lane) {
+    const int j = lane < 9 * F ? lane / 9 : 0;
+    const int k = lane < 9 * F ? lane - 9 * j : 0;  // lanes >= 9 F repeat frame 0's stream 0
+    RefineLds<1>& L = LL[j].L;
+    float* rx = ring_x(L);
+    float s = 0.0f;
+    int r = 0;
+    bool fin = false;
+    while (true) {
+        bool has = false;
+        if (!fin) {
+            if (lds_acquire(&L.F) - r >= kRBlk) has = true;
+            else if (lds_acquire(&L.done) && lds_acquire(reinterpret_cast<int*>(&L.WS)) - r < kRBlk) fin = true;
+        }
+        if (__builtin_amdgcn_ballot_w64(!fin && !has) != 0) {  // lockstep: every open frame's block b
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (__builtin_amdgcn_ballot_w64(has) == 0) break;
+        if (has) {
+            const int q = r & (kRRing - 1);
+            const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
+            const uint32_t pa = (uint32_t)(uintptr_t)p;
+            f4v A[8], B[8];
+            lds_read32(A, pa);
+#pragma unroll
+            for (int i = 0; i < kRBlk / 32; i += 2) {
+                lds_read32(B, pa + 128u * (i + 1));
+                asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                if constexpr (NOADD) s += A[0].x; else chain32(s, A);
+                if (i + 2 < kRBlk / 32) {
+                    lds_read32(A, pa + 128u * (i + 2));
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                if constexpr (NOADD) s += B[0].x; else chain32(s, B);
+            }
+            r += kRBlk;
+            if (k == 0 && lane < 9 * F) lds_release(&L.R, r);
+        }
+    }
+    // every full block summed: each frame's tail element by element
+    const int wf = lds_acquire(reinterpret_cast<int*>(&L.WS));
+    const float* U = (k == 0 || k == 1 || k == 2 || k == 6) ? rx : (k == 3 || k == 4 || k == 7) ? rx + kRS : rx + 2 * kRS;
+    const float* V = k == 0 ? rx : (k == 1 || k == 3) ? rx + kRS : rx + 2 * kRS;
+    for (; r < wf; ++r) {
+        const int q = r & (kRRing - 1);
+        s += k >= 6 ? U[q] : U[q] * V[q];
+    }
+    return s;
+}
+
+template <int ORDER, int DIV, int F>
+__global__ __launch_bounds__(64 * (F + 2)) void k_refine_multi(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
+    const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
+    int tiles_max, int n_frames, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct, int mode) {
+    __shared__ RefineLdsP LL[F];
+    __shared__ int act[F];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int f0 = blockIdx.x * F;
+    int nact = 0, nsteps = 0;
+    if (wave < F) {  // wave j: frame f0 + j's tile list and ring state, then its producer
+        RefineLds<1>& L = LL[wave].L;
+        const int f = f0 + wave;
+        bool a = false;
+        FrameState s;
+        if (f < n_frames) {
+            s = st[f];
+            a = s.has_model && s.need_refine;
+        }
+        if (a) {
+            const FrameMeta m = meta[f];
+            nact = refine_tiles(L, m.tiles, lane, tile_counts + (int64_t)f * tiles_max * hstride + s.best_h, hstride);
+            nsteps = nact < 0 ? (int)((m.n + kRChunk - 1) / kRChunk) : nact * kRStepsPerTile;
+        }
+        if (lane == 0) {
+            L.WS = 0ull;
+            L.R = 0;
+            L.F = 0;
+            L.done = nsteps == 0 ? 1 : 0;  // nothing to stream (or no refinement): no producer publishes
+            L.total = 0;
+            L.nact = nact;
+            act[wave] = a ? 1 : 0;
+            if (a) {
+                L.coef = best_coef[f];
+                acct_add(acct, kAcRefine,
+                         (unsigned long long)nsteps * kRChunk * 12ull + (unsigned long long)meta[f].tiles * 4ull + 32ull);
+            }
+        }
+    }
+    __syncthreads();
+    if (wave < F) {
+        if (nsteps > 0) {
+            RefineLds<1>& L = LL[wave].L;
+            const FrameMeta m = meta[f0 + wave];
+            uint32_t spin_ticket = 0, spin_ring = 0;
+            refine_stream<ORDER, 1>(L, 0, X + m.off, Y + m.off, Z + m.off, m.n, L.coef, thf, lane, nact, 0, nsteps,
+                                    spin_ticket, spin_ring, (mode & 2) != 0);
+        }
+    } else if (wave == F) {
+        __builtin_amdgcn_s_setprio(2);
+        refine_form_multi<F>(LL, lane);
+    } else {
+        __builtin_amdgcn_s_setprio(3);
+        const float acc = (mode & 4) ? refine_chain_multi<F, true>(LL, lane) : refine_chain_multi<F, false>(LL, lane);
+        // lane j < F: frame j's nine sums (lanes 9 j .. 9 j + 8), its plane
+        float a9[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, (9 * lane + k) & 63, 64);
+        if (lane < F && act[lane]) {
+            const int n_in = lds_acquire(reinterpret_cast<int*>(&LL[lane].L.WS));
+            final_coef[f0 + lane] = refine_plane<ORDER, DIV>(a9, n_in);
         }
     }
 }
@@ -1949,6 +2147,15 @@ __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __r
 template <typename T>
 static T* as(void* p) { return static_cast<T*>(p); }
 
+// k_refine_multi's instantiations that fit the CU's LDS (160 KB)
+constexpr bool kRefineMulti3 = 3 * sizeof(RefineLdsP) + 64 <= 160 * 1024;
+template <int ORDER, int DIV>
+static auto refine_multi_kernel(int F) {
+    if constexpr (kRefineMulti3)
+        if (F == 3) return k_refine_multi<ORDER, DIV, 3>;
+    return k_refine_multi<ORDER, DIV, 2>;
+}
+
 template <int ORDER, int DIV>
 static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                            pitt_plane_result* results, int32_t* inliers_dev) {
@@ -2147,6 +2354,14 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                thf, tile_counts, hstride, tiles_max, final_coef, nullptr, rdbg, ctx->refine_mode,
                                xfallback);
             ctx->prof_end(rec);
+        } else if (ctx->refine_frames > 1 && P == 1 && !rdbg) {  // F frames per block, one chain wave
+            rec = ctx->prof_begin("k_refine", 0.0);
+            acct_recs[kAcRefine] = rec;
+            const int F = ctx->refine_frames == 3 && kRefineMulti3 ? 3 : 2;
+            auto mk = refine_multi_kernel<ORDER, DIV>(F);
+            hipLaunchKernelGGL(mk, dim3((nf + F - 1) / F), dim3(64 * (F + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st,
+                               best_coef, thf, tile_counts, hstride, tiles_max, nf, final_coef, acct, ctx->refine_mode);
+            ctx->prof_end(rec);
         } else {
             rec = ctx->prof_begin("k_refine", 0.0);
             acct_recs[kAcRefine] = rec;
@@ -2194,7 +2409,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
                                      (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV),
                                      (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
-                                     (uint64_t)ctx->xrefine};  // 2: every frame handed back (tests)
+                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames};
         pitt_ctx::GraphEntry* hit = nullptr;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;

@@ -7,7 +7,9 @@ producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel a
 step order): every count must give the same ascending inlier stream, hence the same floats.  The
 refinement itself has two paths: k_refine's serial chain (default) and k_xrefine's binade runs
 ($PITT_XREFINE=1, with k_refine as the fallback for frames it hands back: $PITT_XREFINE=2 hands back
-every frame, so the fallback launch is covered too)."""
+every frame, so the fallback launch is covered too).  k_refine_multi ($PITT_REFINE_FRAMES = 2, 3) runs
+2 or 3 frames per block with one chain wave for all of them: per frame the same sums in the same
+order, so the same bits."""
 import os
 
 import pytest
@@ -21,7 +23,8 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
             {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}, {"PITT_XREFINE": "1"},
-            {"PITT_XREFINE": "2"}]
+            {"PITT_XREFINE": "2"}, {"PITT_REFINE_FRAMES": "1"}, {"PITT_REFINE_FRAMES": "2"},
+            {"PITT_REFINE_FRAMES": "3"}]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=lambda v: "-".join(f"{k[5:].lower()}{x}" for k, x in v.items()))
