@@ -1397,9 +1397,9 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
 // took 362k to 430k frames/s at four batches in flight, while k_refine itself only went from 670
 // to 554 us).  Here lanes 9 j + k (j < F) run stream k of frame j, so one v_add advances F frames.
 // Per frame: a producer wave (refine_stream, unchanged) and its own ring and product slots; one
-// former wave forms every frame's product blocks, round robin; the chain takes block b of every
-// frame that has one, in lockstep (a frame whose stream has ended sits out under the exec mask),
-// then each frame's tail element by element.  Per frame the same values are added in the same
+// former wave forms every frame's product blocks, round robin; the chain takes the next block of
+// every frame that has one formed (the others sit out under the exec mask), then each frame's tail
+// element by element.  Per frame the same values are added in the same
 // order as k_refine: bit-exact with it.
 constexpr int kRL1Words = (int)(sizeof(RefineLds<1>) / 4);
 // frame j's LDS starts 36 j banks on (nine 4-bank streams per frame): the frames' reads of one
@@ -1460,11 +1460,13 @@ __device__ __forceinline__ float refine_chain_multi(RefineLdsP (&LL)[F], int lan
             if (lds_acquire(&L.F) - r >= kRBlk) has = true;
             else if (lds_acquire(&L.done) && lds_acquire(reinterpret_cast<int*>(&L.WS)) - r < kRBlk) fin = true;
         }
-        if (__builtin_amdgcn_ballot_w64(!fin && !has) != 0) {  // lockstep: every open frame's block b
+        // the frames whose next block is formed go on (the others sit out under the exec mask): no
+        // frame waits for another's producer
+        if (__builtin_amdgcn_ballot_w64(has) == 0) {
+            if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        if (__builtin_amdgcn_ballot_w64(has) == 0) break;
         if (has) {
             const int q = r & (kRRing - 1);
             const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
