@@ -86,7 +86,8 @@ struct pitt_ctx {
     // frames per k_refine block (1: k_refine; 2, 3: k_refine_multi, one chain wave for all of them)
     int refine_frames = pitt_env_int("PITT_REFINE_FRAMES", 1, 1, 3);
     // k_refine variant (bit 1: producers write inlier lanes only, as masked stores)
-    int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 7);  // bit 2: chain without adds (measurement)
+    // bit 2: chain without adds (a measurement); bit 3: the chain prefetches across block boundaries
+    int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 15);
     // $PITT_XREFINE=1: optimizeModelCoefficients' sums by binade runs (k_xrefine, bit-exact, measured
     // slower than k_refine's chain: DESIGN.md s6); 2: k_xrefine hands every frame back (tests)
     int xrefine = pitt_env_int("PITT_XREFINE", 0, 0, 2);

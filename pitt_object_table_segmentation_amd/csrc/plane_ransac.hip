@@ -1223,32 +1223,53 @@ __device__ __forceinline__ void refine_form(RefineLds<P>& L, int lane, uint32_t&
 // stream (uniform control flow: limiting the reads to 9 active lanes measured slower,
 // tools/microbench/chain_rate.hip).  The last partial block goes element by element.
 // NOADD (PITT_REFINE_MODE bit 2, a measurement only, results wrong): the reads without the adds.
-template <int P, bool NOADD = false>
+// PF (bit 3): the former's count is read during the block's second-to-last 64 elements; when the next
+// block is formed by then, its first 32 elements load under this block's last 32 adds, so the block
+// boundary costs neither the count's round trip nor the first reads' latency.
+template <int P>
+__device__ __forceinline__ uint32_t chain_addr(RefineLds<P>& L, int k, int r) {
+    const int q = r & (kRRing - 1);
+    const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : ring_x(L) + (k - 6) * kRS + q;
+    return (uint32_t)(uintptr_t)p;
+}
+
+template <int P, bool NOADD = false, bool PF = false>
 __device__ __forceinline__ float refine_chain(RefineLds<P>& L, int lane, uint32_t& spins, long long& busy, bool timed) {
     const int k = lane < 9 ? lane : 0;
     float* rx = ring_x(L);
     float s = 0.0f;
     int r = 0;
+    f4v A[8], B[8];
+    bool pre = false;  // PF: the block at r is formed and its first 32 elements are in flight in A
     while (true) {
-        const int formed = lds_acquire(&L.F);
+        const int formed = pre ? r + kRBlk : lds_acquire(&L.F);
         if (formed - r >= kRBlk) {
             const long long tb = timed ? clock64() : 0;
-            const int q = r & (kRRing - 1);
-            const float* p = k < 6 ? &L.prod[(r / kRBlk) % kRProdSlots][k * kPS] : rx + (k - 6) * kRS + q;
             // the next 32 elements' reads are in flight while these 32 are added (reads and waits
-            // in asm: the compiler would otherwise sink each read to just before its use).  A
-            // variant that also read the next block ahead of the boundary measured slower.
-            const uint32_t pa = (uint32_t)(uintptr_t)p;
-            f4v A[8], B[8];
-            lds_read32(A, pa);
+            // in asm: the compiler would otherwise sink each read to just before its use)
+            const uint32_t pa = chain_addr(L, k, r);
+            if (!pre) lds_read32(A, pa);
+            pre = false;
+            bool nxt = false;
 #pragma unroll
             for (int i = 0; i < kRBlk / 32; i += 2) {
                 lds_read32(B, pa + 128u * (i + 1));
                 asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
                 if constexpr (NOADD) s += A[0].x; else chain32(s, A);
                 if (i + 2 < kRBlk / 32) {
+                    int fn = 0;
+                    if (PF && i + 4 == kRBlk / 32)
+                        asm volatile("ds_read_b32 %0, %1" : "=v"(fn) : "v"((uint32_t)(uintptr_t)&L.F) : "memory");
                     lds_read32(A, pa + 128u * (i + 2));
-                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // B (and the count) landed
+                    if (PF && i + 4 == kRBlk / 32) {
+                        int fs;
+                        asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(fs) : "v"(fn));
+                        nxt = fs - (r + kRBlk) >= kRBlk;
+                    }
+                } else if (PF && nxt) {
+                    lds_read32(A, chain_addr(L, k, r + kRBlk));
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // B landed; the next A in flight
                 } else {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
@@ -1257,6 +1278,7 @@ __device__ __forceinline__ float refine_chain(RefineLds<P>& L, int lane, uint32_
             r += kRBlk;
             if (lane == 0) lds_release(&L.R, r);
             if (timed) busy += clock64() - tb;
+            pre = PF && nxt;
             continue;
         }
         if (lds_acquire(&L.done)) {
@@ -1375,6 +1397,7 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
         uint32_t spins = 0;
         long long busy = 0;
         const float acc = (mode & 4) ? refine_chain<P, true>(L, lane, spins, busy, rdbg != nullptr)
+                        : (mode & 8) ? refine_chain<P, false, true>(L, lane, spins, busy, rdbg != nullptr)
                                      : refine_chain<P>(L, lane, spins, busy, rdbg != nullptr);
         float a9[9];
 #pragma unroll

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
             {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}, {"PITT_XREFINE": "1"},
             {"PITT_XREFINE": "2"}, {"PITT_REFINE_FRAMES": "1"}, {"PITT_REFINE_FRAMES": "2"},
-            {"PITT_REFINE_FRAMES": "3"}]
+            {"PITT_REFINE_FRAMES": "3"}, {"PITT_REFINE_MODE": "10"}]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=lambda v: "-".join(f"{k[5:].lower()}{x}" for k, x in v.items()))
