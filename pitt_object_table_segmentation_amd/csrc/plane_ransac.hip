@@ -360,6 +360,19 @@ __device__ __forceinline__ bool box_clear(const RowGeo& G, float4 c, float tv) {
     return fabsf(dc) - rr > lim;
 }
 
+// True when every point p of the box certainly passes PCL's |c . (p, 1)| < t: |d(p)| <= |d(centre)| +
+// sum |c_k| h_k, with box_clear's margin on the other side (1e-5 S below t).  A point with a NaN
+// coordinate never widens the box and never counts (its distance is NaN), so such a pair counts the
+// group's all-non-NaN points exactly.  NaN or infinite boxes never compare true.
+__device__ __forceinline__ bool box_inside(const RowGeo& G, float4 c, float tv) {
+    const float n1 = fabsf(c.x) + fabsf(c.y) + fabsf(c.z);
+    const float s = __builtin_fmaf(n1, G.m, fabsf(c.w) + 1e-25f);
+    const float lim = __builtin_fmaf(-1e-5f, s, tv);
+    const float dc = __builtin_fmaf(c.x, G.c[0], __builtin_fmaf(c.y, G.c[1], __builtin_fmaf(c.z, G.c[2], c.w)));
+    const float rr = __builtin_fmaf(fabsf(c.x), G.h[0], __builtin_fmaf(fabsf(c.y), G.h[1], fabsf(c.z) * G.h[2]));
+    return fabsf(dc) + rr < lim;
+}
+
 // v_writelane_b32 (the compiler routes an SGPR lane select through m0: gfx9's constant bus takes
 // one SGPR operand)
 __device__ int writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
@@ -442,7 +455,9 @@ __device__ __forceinline__ void score_list(uint32_t lb, int c, float x, float y,
 }
 
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
-template <int ORDER, bool BOX>
+// INS: a pair whose box lies certainly inside the slab (box_inside) is not scored point by point;
+// it counts the group's points with no NaN coordinate (gcnt, one ballot per group and sub-step).
+template <int ORDER, bool BOX, bool INS>
 __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, SubPts& P, int rem, float tv, int lane,
                                           int32_t* __restrict__ wc, float& tb, float* __restrict__ gbox,
                                           uint32_t gsrc) {
@@ -450,6 +465,15 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
 #pragma unroll
         for (int g = 0; g < kGPS; ++g)
             if (g * kGrp + lane >= rem) P.x[g] = P.y[g] = P.z[g] = __builtin_nanf("");
+    }
+    int gcnt = 0;  // INS: this lane's group's points with three non-NaN coordinates
+    if constexpr (INS) {
+#pragma unroll
+        for (int g = 0; g < kGPS; ++g) {
+            const int cg = __builtin_popcountll(
+                __builtin_amdgcn_ballot_w64(P.x[g] == P.x[g] && P.y[g] == P.y[g] && P.z[g] == P.z[g]));
+            gcnt = (lane >> 4) == g ? cg : gcnt;
+        }
     }
     RowBox B;
     if constexpr (BOX) {
@@ -490,8 +514,16 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         const float4 cr = cl[min(hl, Hf - 1)];
         const int nb = min(kRnd, Hf - kRnd * r);  // valid hypotheses of this round
         const uint64_t valid = (((uint64_t)1 << nb) - 1) * 0x0001000100010001ull;
-        const uint64_t need = __builtin_amdgcn_ballot_w64(!box_clear(G, cr, tv)) & valid;
-        if (need == 0) continue;
+        const bool clr = box_clear(G, cr, tv);
+        bool ins = false;
+        if constexpr (INS) ins = !clr && ((valid >> lane) & 1u) && box_inside(G, cr, tv);
+        const int add_in = ins ? gcnt : 0;
+        const uint64_t need = __builtin_amdgcn_ballot_w64(!clr && !ins) & valid;
+        if (need == 0) {
+            if constexpr (INS)
+                if (ins) wc[64 * r + lane] += add_in;
+            continue;
+        }
         // compaction: the surviving hypotheses of group g, in ascending order, into list slots
         // 16 g + k (k = the bit's rank inside its 16-lane row)
         const bool mine = (need >> lane) & 1u;
@@ -507,7 +539,7 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         score_list<ORDER, 3>(lb, __builtin_popcount((uint32_t)(need >> 48)), P.x[3], P.y[3], P.z[3], tv, vc);
         // back to the hypothesis lanes: lane 16 g + h' reads lane 16 g + k
         const int got = __builtin_amdgcn_ds_bpermute(4 * ((lane & 48) + k), vc);
-        wc[64 * r + lane] += mine ? got : 0;
+        wc[64 * r + lane] += (mine ? got : 0) + add_in;
     }
 }
 
@@ -631,7 +663,7 @@ __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__
 
 // BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
 // -- for k_refine's tile skipping.
-template <int ORDER, int NST, bool BOX, bool LANE = false>
+template <int ORDER, int NST, bool BOX, bool LANE = false, bool INS = false>
 __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
@@ -684,10 +716,10 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
-        score_sub<ORDER, BOX>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
                               gsrc + 128u * s);
         if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
-        score_sub<ORDER, BOX>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
                               gsrc + 128u * (s + 1));
     }
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
@@ -2333,9 +2365,14 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         rec = ctx->prof_begin("k_score", 0.0);
         if (c == 0) ctx->prof_alias(rec, "k_score.first");  // the first chunk: every frame, H hypotheses
         score_recs.push_back(rec);
+        const bool ins = ctx->inside_cull;
         auto kern = c == 0 ? (H <= 32 && ctx->lane_score ? k_score<ORDER, 1, true, true>
-                              : H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
-                           : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
+                              : ins ? (H <= 64 ? k_score<ORDER, 1, true, false, true> : H <= 128 ? k_score<ORDER, 2, true, false, true>
+                                                : k_score<ORDER, 4, true, false, true>)
+                                    : (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>))
+                           : ins ? (H <= 64 ? k_score<ORDER, 1, false, false, true> : H <= 128 ? k_score<ORDER, 2, false, false, true>
+                                             : k_score<ORDER, 4, false, false, true>)
+                                 : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
         // the first chunk scores every frame (one item per wave); later ones stride over a capped grid
         const int64_t all_blocks = ((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves;
         const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
@@ -2432,7 +2469,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uintptr_t)fr->x, (uint64_t)(uintptr_t)fr->y, (uint64_t)(uintptr_t)fr->z,
                                      (uint64_t)(uintptr_t)inliers_dev, (uint64_t)A, (uint64_t)hcap,
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
-                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score, (uint64_t)(ORDER * 2 + DIV),
+                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score * 2 + (uint64_t)ctx->inside_cull, (uint64_t)(ORDER * 2 + DIV),
                                      (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
                                      (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames};
         pitt_ctx::GraphEntry* hit = nullptr;

@@ -1,7 +1,8 @@
 """The first scoring chunk has two implementations: the survivor-list scorer
 (compaction, v_cmp -> s_bcnt1 -> v_writelane per surviving (group, hypothesis) pair) and the
 lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only, |d| - t sign bits
-added into lane-private counters).  $PITT_LANE_SCORE picks one when a context is created; the other
+added into lane-private counters).  Either way a pair whose group box lies certainly inside the slab
+may count the group's non-NaN points without scoring them ($PITT_INSIDE_CULL, on by default).  $PITT_LANE_SCORE picks one when a context is created; the other
 is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
 producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel and appending in
 step order): every count must give the same ascending inlier stream, hence the same floats.  The
@@ -24,7 +25,8 @@ pytestmark = pytest.mark.gpu
 VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
             {"PITT_REFINE_PRODUCERS": "2"}, {"PITT_REFINE_PRODUCERS": "4"}, {"PITT_XREFINE": "1"},
             {"PITT_XREFINE": "2"}, {"PITT_REFINE_FRAMES": "1"}, {"PITT_REFINE_FRAMES": "2"},
-            {"PITT_REFINE_FRAMES": "3"}, {"PITT_REFINE_MODE": "10"}]
+            {"PITT_REFINE_FRAMES": "3"}, {"PITT_REFINE_MODE": "10"}, {"PITT_INSIDE_CULL": "0"},
+            {"PITT_INSIDE_CULL": "1"}]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=lambda v: "-".join(f"{k[5:].lower()}{x}" for k, x in v.items()))

@@ -83,6 +83,34 @@ def test_points_straddling_the_threshold(ctx):
         _check(ctx, frames, res, inls, threshold=th, max_iterations=100)
 
 
+def test_groups_inside_the_slab(ctx):
+    """k_score's inside shortcut ($PITT_INSIDE_CULL, default on): a (64-point group, hypothesis) pair
+    whose box lies certainly inside the slab counts the group's points with three non-NaN coordinates.
+    Thin planes (noise far below t) give many such pairs; their groups carry points with one NaN
+    coordinate (x, y or z alone: they never widen the box and never count), all-NaN groups, and
+    groups whose box reaches t - a few ulps (not certified: scored point by point)."""
+    rng = np.random.default_rng(15)
+    frames = []
+    for k in range(4):
+        x, y, z = _plane_scene(rng, 24, range(2, 22), noise=0.0002 if k < 2 else 0.0)
+        n = len(x)
+        idx = rng.choice(np.arange(2 * TILE, 22 * TILE), 3000, replace=False)
+        x[idx[:1000]] = np.nan
+        y[idx[1000:2000]] = np.nan
+        z[idx[2000:]] = np.nan
+        g = (5 + k) * TILE + 64 * 3  # one whole group of NaN points
+        x[g:g + 64] = y[g:g + 64] = z[g:g + 64] = np.nan
+        if k >= 2:  # exact z = 0 plane with groups whose extreme point sits at +-t - u ulps
+            t = pitt.float_threshold(0.007)
+            for j, u in enumerate(range(1, 9)):
+                q = (10 + j) * TILE + 64 * j + 5
+                z[q] = np.float32((-1) ** j) * _ulps(t, -u)
+        frames.append((x, y, z))
+    assert n == 24 * TILE
+    res, inls = _run_batch(ctx, frames, max_iterations=200)
+    _check(ctx, frames, res, inls, max_iterations=200)
+
+
 def test_later_chunks_and_hypothesis_limit(ctx):
     """Low-inlier-ratio frames run many chunks (the per-frame limit applies from chunk 1 on);
     mixed with easy frames so chunk work lists shrink unevenly."""
