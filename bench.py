@@ -628,6 +628,8 @@ def main():
                                "step later)" if world > 1 else None),
                 "gather_us_per_step": (round(gather.seconds / args.steps * 1e6, 1) if gather is not None else None),
                 "gathers": (gather.posted if gather is not None else None),
+                # runtime knobs of the exact kernel variants (read when a context is created)
+                "knobs": {k: os.environ[k] for k in sorted(os.environ) if k.startswith("PITT_")} or None,
             },
             "roofline": {
                 "kernel": "k_score",

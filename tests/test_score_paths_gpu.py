@@ -2,7 +2,7 @@
 (compaction, v_cmp -> s_bcnt1 -> v_writelane per surviving (group, hypothesis) pair) and the
 lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only, |d| - t sign bits
 added into lane-private counters).  Either way a pair whose group box lies certainly inside the slab
-may count the group's non-NaN points without scoring them ($PITT_INSIDE_CULL, on by default).  $PITT_LANE_SCORE picks one when a context is created; the other
+may count the group's non-NaN points without scoring them ($PITT_INSIDE_CULL, off by default).  $PITT_LANE_SCORE picks one when a context is created; the other
 is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
 producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel and appending in
 step order): every count must give the same ascending inlier stream, hence the same floats.  The

@@ -84,7 +84,7 @@ def test_points_straddling_the_threshold(ctx):
 
 
 def test_groups_inside_the_slab(ctx):
-    """k_score's inside shortcut ($PITT_INSIDE_CULL, default on): a (64-point group, hypothesis) pair
+    """k_score's inside shortcut ($PITT_INSIDE_CULL, off by default): a (64-point group, hypothesis) pair
     whose box lies certainly inside the slab counts the group's points with three non-NaN coordinates.
     Thin planes (noise far below t) give many such pairs; their groups carry points with one NaN
     coordinate (x, y or z alone: they never widen the box and never count), all-NaN groups, and
