@@ -466,15 +466,19 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         for (int g = 0; g < kGPS; ++g)
             if (g * kGrp + lane >= rem) P.x[g] = P.y[g] = P.z[g] = __builtin_nanf("");
     }
-    int gcnt = 0;  // INS: this lane's group's points with three non-NaN coordinates
-    if constexpr (INS) {
+    // INS: this lane's group's points with three non-NaN coordinates, counted in the first round that
+    // certifies a pair of the sub-step (x + y + z is NaN iff a coordinate is NaN, or when infinities of
+    // both signs meet, and an infinite coordinate never lets its group's box certify)
+    int gcnt = 0;
+    bool have_gcnt = false;
+    auto count_groups = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < kGPS; ++g) {
-            const int cg = __builtin_popcountll(
-                __builtin_amdgcn_ballot_w64(P.x[g] == P.x[g] && P.y[g] == P.y[g] && P.z[g] == P.z[g]));
+            const float sxyz = P.x[g] + P.y[g] + P.z[g];
+            const int cg = __builtin_popcountll(__builtin_amdgcn_ballot_w64(sxyz == sxyz));
             gcnt = (lane >> 4) == g ? cg : gcnt;
         }
-    }
+    };
     RowBox B;
     if constexpr (BOX) {
         coord_box(P.x[0], P.x[1], P.x[2], P.x[3], B.lo[0], B.hi[0]);
@@ -516,7 +520,13 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         const uint64_t valid = (((uint64_t)1 << nb) - 1) * 0x0001000100010001ull;
         const bool clr = box_clear(G, cr, tv);
         bool ins = false;
-        if constexpr (INS) ins = !clr && ((valid >> lane) & 1u) && box_inside(G, cr, tv);
+        if constexpr (INS) {
+            ins = !clr && ((valid >> lane) & 1u) && box_inside(G, cr, tv);
+            if (!have_gcnt && __builtin_amdgcn_ballot_w64(ins) != 0) {  // wave-uniform
+                count_groups();
+                have_gcnt = true;
+            }
+        }
         const int add_in = ins ? gcnt : 0;
         const uint64_t need = __builtin_amdgcn_ballot_w64(!clr && !ins) & valid;
         if (need == 0) {
