@@ -13,6 +13,8 @@ evaluates the bounds with FMAs; here they are evaluated in float64 and rounded t
 from the device by a few float32 ulps of S -- far inside the margin, which is what this test pins: no
 certified pair may contain a point whose PCL-order float32 distance decides the other way, in any of
 the three reduce orders (A3)."""
+import warnings
+
 import numpy as np
 import pytest
 
@@ -35,7 +37,8 @@ def _pcl_dist(c, x, y, z, order):
 
 def _certificates(G, c, t):
     """(clear, inside) for groups G (n, 64, 3) float32 against coefficients c (float32 x4)."""
-    with np.errstate(invalid="ignore", over="ignore"):
+    with np.errstate(invalid="ignore", over="ignore"), warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)  # all-NaN groups: an empty (NaN) box
         lo = np.nanmin(G, axis=1)
         hi = np.nanmax(G, axis=1)
         cen = (F(0.5) * (lo + hi)).astype(F)
@@ -73,7 +76,9 @@ def test_certificates_are_sound(order, scale, spread, t):
         G = _groups(rng, 256, scale, spread, nan_rate=0.02)
         # a hypothesis through a random group's centre, tilted, shifted by a few thresholds
         k = rng.integers(len(G))
-        p0 = np.nanmean(G[k].astype(np.float64), axis=0)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            p0 = np.nan_to_num(np.nanmean(G[k].astype(np.float64), axis=0))
         nrm = rng.normal(0, 1, 3)
         nrm /= np.linalg.norm(nrm)
         c = np.empty(4)
