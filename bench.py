@@ -444,6 +444,9 @@ def main():
     # frames/s against 355.2k at 3 in flight on the box's default 4 queues; 4 in flight sharing 4
     # queues measured 287.4k)
     ap.add_argument("--pipeline", type=int, default=4, help="contexts/streams with batches in flight")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="world 1: each step's batch split over this many contexts (the same frames and work per "
+                         "step, several steps in flight); the roofline and extra passes keep whole batches")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's); set before HIP starts")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -488,11 +491,16 @@ def main():
     t_gen = time.perf_counter()
     # one distinct batch per in-flight context: batch j holds frames start + j * total + [0, B)
     batches, frames0 = [], None
+    parts = args.parts if world == 1 else 1
+    pbatches = []  # parts > 1: slot j's frames as `parts` contiguous part batches (slot-major)
     for j in range(args.pipeline):
         fr = make_frames(range(start + j * total, end + j * total), threads)
         if j == 0:
             frames0 = fr
         batches.append(pitt.FrameBatch.from_host(fr, device=dev))
+        if parts > 1:
+            ps = (len(fr) + parts - 1) // parts
+            pbatches += [pitt.FrameBatch.from_host(fr[q * ps:(q + 1) * ps], device=dev) for q in range(parts)]
     log(f"[rank {rank}] {args.pipeline} x {len(frames0)} frames generated + uploaded in "
         f"{time.perf_counter() - t_gen:.1f} s")
 
@@ -541,6 +549,35 @@ def main():
         if gather is not None:
             collect(0)
         return records[(counter[0] - 1) % len(ctxs)]
+
+    if parts > 1:
+        # one context per part: a step enqueues its batch's parts on `parts` contexts at once
+        pctxs = [pitt.Context(gpu) for _ in pbatches]
+        pouts = [None if args.no_inliers else torch.empty(b.capacity, dtype=torch.int32, device=dev)
+                 for b in pbatches]
+        ppending, precords = [None] * len(pctxs), [None] * len(pctxs)
+        for k in range(len(pctxs)):
+            for _ in range(2):
+                pctxs[k].plane_segment_batch(pbatches[k], params, pouts[k])
+
+        def step():  # noqa: F811 (parts: replaces the whole-batch step)
+            i = counter[0] % args.pipeline
+            counter[0] += 1
+            for k in range(i * parts, (i + 1) * parts):
+                if ppending[k] is not None:
+                    pctxs[k].wait()
+                    precords[k] = ppending[k]
+                pctxs_k = pctxs[k]
+                ppending[k] = pctxs_k.plane_segment_batch_async(pbatches[k], params, pouts[k])
+
+        def drain():  # noqa: F811
+            for k in range(len(pctxs)):
+                if ppending[k] is not None:
+                    pctxs[k].wait()
+                    precords[k] = ppending[k]
+                    ppending[k] = None
+            i = (counter[0] - 1) % args.pipeline
+            return np.concatenate([precords[k] for k in range(i * parts, (i + 1) * parts)])
 
     ctx = ctxs[0]
     # setup, not steps: every context runs its batch twice, so that its scratch arena is allocated
@@ -621,7 +658,8 @@ def main():
                             " PCL plane RANSAC th 0.007 / 1000 iters / seed 12345 / optimize, final inlier lists",
                 "frames_per_gpu": B,
                 "points_per_frame": W * H,
-                "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU",
+                "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU"
+                               + (f", each split over {parts} contexts" if parts > 1 else ""),
                 "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
                 "world_size_seen": world,
                 "collective": (f"{backend} all_gather_into_tensor of per-frame records, async (collected one "
