@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG=${1:-parts}
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for cfg in "4 1 8" "2 4 16" "3 4 16" "1 4 8"; do
     set -- $cfg
     timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-extras --no-cpu-baseline \
