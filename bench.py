@@ -130,16 +130,31 @@ def cpu_baseline(frames, clutter_frame, cpus, budget_s):
                 host=cpus)
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of k_score from the committed rocprofv3 PMC summary, if present."""
+def library_sha16():
+    """sha256 (16 hex) of the libpitt_seg.so this process runs: the stamp that ties a PMC summary to
+    the build it measured."""
+    import hashlib
+    from pitt_object_table_segmentation_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def pmc_traffic(lib_sha):
+    """Per-launch HBM bytes of k_score from the committed rocprofv3 PMC summary, when that summary was
+    measured on this very library build (its `library_sha16` stamp); otherwise (None, reason)."""
     path = os.path.join(ROOT, "profiles", "pmc_k_score.json")
     if not os.path.exists(path):
-        return None
+        return None, "no PMC summary (profiles/pmc_k_score.json)"
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+            pmc = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"unreadable PMC summary: {e}"
+    stamp = pmc.get("library_sha16")
+    if stamp != lib_sha:
+        return None, (f"PMC summary {pmc.get('tag')} measured library {stamp}, this run's library is {lib_sha}: "
+                      "not this build's traffic")
+    return pmc.get("hbm_bytes_per_launch"), f"PMC summary {pmc.get('tag')}, same library build"
 
 
 def kernel_table(ctx, batches):
@@ -186,7 +201,9 @@ def cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, steps, frames_p
     against the exact mode.  Exact order stays the default and the parity path."""
     import torch
     fast = pitt.sac_params(cov_mode=pitt.COV_FAST)
-    for _ in range(3):
+    # every context sees the fast layout twice before timing (its graph is captured on the second
+    # sight), as the main pass primes its contexts
+    for _ in range(2 * len(batches)):
         step(fast)
     drain()
     torch.cuda.synchronize()
@@ -550,34 +567,39 @@ def main():
             collect(0)
         return records[(counter[0] - 1) % len(ctxs)]
 
+    timed_step, timed_drain = step, drain  # the timed pass; the extra passes always use whole batches
     if parts > 1:
         # one context per part: a step enqueues its batch's parts on `parts` contexts at once
         pctxs = [pitt.Context(gpu) for _ in pbatches]
         pouts = [None if args.no_inliers else torch.empty(b.capacity, dtype=torch.int32, device=dev)
                  for b in pbatches]
         ppending, precords = [None] * len(pctxs), [None] * len(pctxs)
+        pcounter = [0]
         for k in range(len(pctxs)):
             for _ in range(2):
                 pctxs[k].plane_segment_batch(pbatches[k], params, pouts[k])
 
-        def step():  # noqa: F811 (parts: replaces the whole-batch step)
-            i = counter[0] % args.pipeline
-            counter[0] += 1
+        def parts_step():
+            i = pcounter[0] % args.pipeline
+            pcounter[0] += 1
             for k in range(i * parts, (i + 1) * parts):
                 if ppending[k] is not None:
                     pctxs[k].wait()
                     precords[k] = ppending[k]
-                pctxs_k = pctxs[k]
-                ppending[k] = pctxs_k.plane_segment_batch_async(pbatches[k], params, pouts[k])
+                ppending[k] = pctxs[k].plane_segment_batch_async(pbatches[k], params, pouts[k])
 
-        def drain():  # noqa: F811
+        def parts_drain():
             for k in range(len(pctxs)):
                 if ppending[k] is not None:
                     pctxs[k].wait()
                     precords[k] = ppending[k]
                     ppending[k] = None
-            i = (counter[0] - 1) % args.pipeline
-            return np.concatenate([precords[k] for k in range(i * parts, (i + 1) * parts)])
+            for j in range(args.pipeline):  # slot j's records: its parts' records, in frame order
+                if all(precords[k] is not None for k in range(j * parts, (j + 1) * parts)):
+                    records[j] = np.concatenate([precords[k] for k in range(j * parts, (j + 1) * parts)])
+            return records[(pcounter[0] - 1) % args.pipeline]
+
+        timed_step, timed_drain = parts_step, parts_drain
 
     ctx = ctxs[0]
     # setup, not steps: every context runs its batch twice, so that its scratch arena is allocated
@@ -587,8 +609,8 @@ def main():
         for _ in range(2):
             ctxs[i].plane_segment_batch(batches[i], params, outs[i])
     for _ in range(args.warmup):
-        step()
-    drain()
+        timed_step()
+    timed_drain()
     # parity spot check outside the timed region (first frame of this rank vs the oracle)
     if rank == 0:
         res0 = ctx.plane_segment_batch(batches[0], params, outs[0])
@@ -606,8 +628,9 @@ def main():
         gather.seconds, gather.posted = 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    res = drain()
+        timed_step()
+    res = timed_drain()
+    rec_dump = None if records[0] is None else records[0].copy()  # before the extra passes reuse the slots
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -636,6 +659,8 @@ def main():
 
     line = None
     if rank == 0:
+        lib_sha = library_sha16()
+        traffic, traffic_note = pmc_traffic(lib_sha)
         avg_ms = ms / max(1, launches)
         achieved = (nbytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if launches else 0.0
         line = {
@@ -676,7 +701,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(),
+                "traffic": traffic,
+                "traffic_source": traffic_note,
                 "launches": launches,
                 "measured": f"HIP events on k_score's stream over a separate {roof_steps}-batch pass with one "
                             "batch in flight (the timed pass overlaps batches on several streams); launches "
@@ -688,6 +714,7 @@ def main():
             },
             "kernels": kernels,
             "hip_graphs": dict(zip(("captures", "replays"), ctxs[0].graph_stats())),
+            "library_sha16": lib_sha,
         }
     if rank == 0 and world == 1 and not args.no_extras:
         line["cov_fast"] = cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, args.steps, B)
@@ -710,7 +737,7 @@ def main():
         cl = clutter_frames[0] if clutter_frames else make_frames([0], 1, pitt.SCENE_CLUTTER)[0]
         line["cpu_baseline"] = cpu_baseline(frames0, cl, cpus, args.cpu_budget)
     if rank == 0 and args.dump_records:
-        np.save(args.dump_records, records[0])
+        np.save(args.dump_records, rec_dump)
     if rank == 0:
         print(json.dumps(line), flush=True)
     for c in ctxs:

@@ -47,7 +47,8 @@
 extern "C" {
 #endif
 
-#define PITT_ABI_VERSION 2
+/* 3: pitt_sac_params.cov_mode (A6), pitt_cylinder_params / pitt_cone_params.eigen33, pitt_build_flags */
+#define PITT_ABI_VERSION 3
 /* Points per scoring tile; frames are scored in tiles of this many points. */
 #define PITT_TILE_POINTS 2048
 
@@ -138,6 +139,11 @@ int  pitt_refine_stats(pitt_ctx* ctx, int64_t* batches, int64_t* fallback_frames
 void* pitt_get_stream(pitt_ctx* ctx);
 const char* pitt_last_error(pitt_ctx* ctx);
 int  pitt_abi_version(void);
+/* Build flags of the loaded library: PITT_BUILD_AB_VARIANTS when it is the A/B build
+ * (libpitt_seg_ab.so, `make ab`) that reads kernel-variant knobs ($PITT_LANE_SCORE, ...) from the
+ * environment.  The product library returns 0 and ignores those variables. */
+enum { PITT_BUILD_AB_VARIANTS = 1 };
+int  pitt_build_flags(void);
 
 /* --- plane segmentation ------------------------------------------------------------------ */
 /* Single cloud from host memory, PCL layout: stride 16 (PointXYZ: x, y, z, pad) or 12.

@@ -21,6 +21,7 @@ PITT_E_NOMEM = -3
 PITT_E_SAMPLER = -4
 PITT_E_NODEVICE = -5
 PITT_TILE_POINTS = 2048
+PITT_BUILD_AB_VARIANTS = 1
 PITT_FLAG_K_NEAR_INTEGER = 1
 PITT_VOXEL_OVERFLOW_COPY = 1
 PITT_VOXEL_ORDER_PCL, PITT_VOXEL_ORDER_STABLE = 0, 1
@@ -217,6 +218,7 @@ _i64p = ctypes.POINTER(ctypes.c_int64)
 # name -> (restype, argtypes); every symbol declared in include/pitt_seg.h
 SIGNATURES = {
     "pitt_abi_version": (_i32, []),
+    "pitt_build_flags": (_i32, []),
     "pitt_sac_params_default": (None, [ctypes.POINTER(SacParams)]),
     "pitt_create": (_i32, [ctypes.POINTER(_vp), _i32]),
     "pitt_destroy": (None, [_vp]),

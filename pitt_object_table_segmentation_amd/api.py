@@ -492,6 +492,9 @@ class Context:
         import torch
         t = torch.empty(max(n, 1), dtype=dtype, device=device)
         if n:
+            # the caching allocator may hand back a block that kernels still queued on torch's stream
+            # use; pitt_memcpy writes on the context's stream, so let torch's stream drain first
+            torch.cuda.current_stream(t.device).synchronize()
             self._check(lib.pitt_memcpy(self.h, ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
                                         n * t.element_size()), "pitt_memcpy")
         return t[:n]

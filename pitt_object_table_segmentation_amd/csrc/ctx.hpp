@@ -79,6 +79,13 @@ struct pitt_ctx {
     // device pool of the last batch's tables
     std::vector<std::tuple<int64_t, uint32_t, int64_t>> pool_keys;
 
+    // Kernel variants kept for A/B measurements.  Only a library built with
+    // -DPITT_AB_VARIANTS (`make ab`: libpitt_seg_ab.so, loaded by tools/ and the variant tests through
+    // $PITT_LIB_PATH) reads them from the environment and instantiates their kernels.  The product
+    // library fixes them at the defaults below and ignores the environment, so no setting can make
+    // it run a variant -- in particular not the chain-without-adds measurement (refine_mode bit 2).
+#ifdef PITT_AB_VARIANTS
+    static constexpr bool kVariants = true;
     // first scoring chunk with lane-private counters (k_score LANE); $PITT_LANE_SCORE overrides
     bool lane_score = pitt_env_flag("PITT_LANE_SCORE", false);
     // k_score: pairs whose group box lies certainly inside the slab count the group without scoring
@@ -89,14 +96,25 @@ struct pitt_ctx {
     // frames per k_refine block (1: k_refine; 2, 3: k_refine_multi, one chain wave for all of them)
     int refine_frames = pitt_env_int("PITT_REFINE_FRAMES", 1, 1, 3);
     // k_refine variant (bit 1: producers write inlier lanes only, as masked stores)
-    // bit 2: chain without adds (a measurement); bit 3: the chain prefetches across block boundaries
+    // bit 2: chain without adds (a measurement: WRONG planes); bit 3: the chain prefetches across
+    // block boundaries
     int refine_mode = pitt_env_int("PITT_REFINE_MODE", 2, 0, 15);
     // $PITT_XREFINE=1: optimizeModelCoefficients' sums by binade runs (k_xrefine, bit-exact, measured
     // slower than k_refine's chain: DESIGN.md s6); 2: k_xrefine hands every frame back (tests)
     int xrefine = pitt_env_int("PITT_XREFINE", 0, 0, 2);
-    int64_t xrefine_batches = 0, xrefine_fallbacks = 0;  // frames k_xrefine handed back to k_refine
     // $PITT_REFINE_DEBUG=1: k_refine records per-role cycles and spins, printed at completion
     bool refine_debug = pitt_env_flag("PITT_REFINE_DEBUG", false);
+#else
+    static constexpr bool kVariants = false;
+    static constexpr bool lane_score = false;
+    static constexpr bool inside_cull = false;
+    static constexpr int refine_producers = 1;
+    static constexpr int refine_frames = 1;
+    static constexpr int refine_mode = 2;
+    static constexpr int xrefine = 0;
+    static constexpr bool refine_debug = false;
+#endif
+    int64_t xrefine_batches = 0, xrefine_fallbacks = 0;  // frames k_xrefine handed back to k_refine
     void* refine_dbg_h = nullptr;
 
     // HIP graphs of the plane pipeline: a batch's ~20 launches are captured once per (layout,
@@ -155,9 +173,13 @@ struct pitt_ctx {
         err = msg;
         return code;
     }
-    // Device scratch buffer `name` of at least `bytes` (grows, never shrinks).
+    // Waits for the work queued on the context's stream and its side streams.
+    void drain();
+    // Device scratch buffer `name` of at least `bytes` (grows, never shrinks).  A block that moves
+    // is freed only after drain(), and bumps arena_gen so that no cached graph replays it.
     void* buf(const std::string& name, size_t bytes);
-    // Pinned host buffer.
+    // Pinned host buffer (the same rules: drain() before a free, arena_gen bumped on a move -- graph
+    // copy nodes hold these addresses too; DESIGN.md s3d, the round-3 graph fault).
     void* pinned(const std::string& name, size_t bytes);
 
     // Profiler hooks around a launch.

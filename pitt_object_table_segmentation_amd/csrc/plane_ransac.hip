@@ -1438,9 +1438,13 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
         __builtin_amdgcn_s_setprio(3);
         uint32_t spins = 0;
         long long busy = 0;
+#ifdef PITT_AB_VARIANTS
         const float acc = (mode & 4) ? refine_chain<P, true>(L, lane, spins, busy, rdbg != nullptr)
                         : (mode & 8) ? refine_chain<P, false, true>(L, lane, spins, busy, rdbg != nullptr)
                                      : refine_chain<P>(L, lane, spins, busy, rdbg != nullptr);
+#else
+        const float acc = refine_chain<P>(L, lane, spins, busy, false);  // the product: the exact chain only
+#endif
         float a9[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) a9[k] = __shfl(acc, k, 64);
@@ -2375,6 +2379,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         rec = ctx->prof_begin("k_score", 0.0);
         if (c == 0) ctx->prof_alias(rec, "k_score.first");  // the first chunk: every frame, H hypotheses
         score_recs.push_back(rec);
+#ifdef PITT_AB_VARIANTS
         const bool ins = ctx->inside_cull;
         auto kern = c == 0 ? (H <= 32 && ctx->lane_score ? k_score<ORDER, 1, true, true>
                               : ins ? (H <= 64 ? k_score<ORDER, 1, true, false, true> : H <= 128 ? k_score<ORDER, 2, true, false, true>
@@ -2383,6 +2388,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            : ins ? (H <= 64 ? k_score<ORDER, 1, false, false, true> : H <= 128 ? k_score<ORDER, 2, false, false, true>
                                              : k_score<ORDER, 4, false, false, true>)
                                  : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
+#else
+        auto kern = c == 0 ? (H <= 64 ? k_score<ORDER, 1, true> : H <= 128 ? k_score<ORDER, 2, true> : k_score<ORDER, 4, true>)
+                           : (H <= 64 ? k_score<ORDER, 1, false> : H <= 128 ? k_score<ORDER, 2, false> : k_score<ORDER, 4, false>);
+#endif
         // the first chunk scores every frame (one item per wave); later ones stride over a capped grid
         const int64_t all_blocks = ((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves;
         const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
@@ -2411,6 +2420,14 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         hipLaunchKernelGGL((k_cov_final<ORDER>), dim3(nf), dim3(64), 0, sm, meta, st, part, nf, tiles_max, final_coef);
         ctx->prof_end(rec);
     } else {
+#ifndef PITT_AB_VARIANTS
+        rec = ctx->prof_begin("k_refine", 0.0);
+        acct_recs[kAcRefine] = rec;
+        hipLaunchKernelGGL((k_refine<ORDER, DIV, 1>), dim3(nf), dim3(64 * 3), 0, sm, fr->x, fr->y, fr->z, meta, st,
+                           best_coef, thf, tile_counts, hstride, tiles_max, final_coef, acct,
+                           (unsigned long long*)nullptr, 2, (const int32_t*)nullptr);
+        ctx->prof_end(rec);
+#else
         const int P = ctx->refine_producers;
         auto kern = P == 1 ? k_refine<ORDER, DIV, 1> : P == 2 ? k_refine<ORDER, DIV, 2>
                   : P == 3 ? k_refine<ORDER, DIV, 3> : k_refine<ORDER, DIV, 4>;
@@ -2442,6 +2459,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                nullptr);
             ctx->prof_end(rec);
         }
+#endif
     }
     rec = ctx->prof_begin("k_sel_mark", 0.0);
     acct_recs[kAcSelMark] = rec;

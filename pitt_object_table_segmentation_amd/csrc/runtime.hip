@@ -57,12 +57,18 @@ float float_threshold(double th) {
 }
 }  // namespace pitt
 
+void pitt_ctx::drain() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (hipStream_t sd : side)
+        if (sd) (void)hipStreamSynchronize(sd);
+}
+
 void* pitt_ctx::buf(const std::string& name, size_t bytes) {
     pitt::DevBuf& b = bufs[name];
     if (b.bytes < bytes || !b.p) {
-        // work queued on the stream may still use the old block: let it drain before freeing
+        // work queued on the context's streams may still use the old block: let it drain first
         if (b.p) {
-            (void)hipStreamSynchronize(stream);
+            drain();
             (void)hipFree(b.p);
         }
         size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
@@ -86,7 +92,7 @@ void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
         // an async copy queued on the stream may still read or write the old block; cached graphs
         // hold its address in their copy nodes
         if (e.first) {
-            (void)hipStreamSynchronize(stream);
+            drain();
             (void)hipHostFree(e.first);
         }
         ++arena_gen;
@@ -154,6 +160,8 @@ int pitt_ctx::prof_collect() {
 extern "C" {
 
 int pitt_abi_version(void) { return PITT_ABI_VERSION; }
+
+int pitt_build_flags(void) { return pitt_ctx::kVariants ? PITT_BUILD_AB_VARIANTS : 0; }
 
 void pitt_sac_params_default(pitt_sac_params* p) {
     if (!p) return;
@@ -282,6 +290,10 @@ int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* fr, const p
         return ctx->fail(PITT_E_INVALID, "inliers_dev must be 4-byte aligned");
     if (p->reduce_order < 0 || p->reduce_order > 2 || p->div_mode < 0 || p->div_mode > 1)
         return ctx->fail(PITT_E_INVALID, "reduce_order / div_mode out of range");
+    // a caller built against ABI 2 passes the shorter struct: whatever lies past its end is
+    // rejected here unless it happens to read as a valid mode (ABI 3 added cov_mode)
+    if (p->cov_mode != PITT_COV_EXACT && p->cov_mode != PITT_COV_FAST)
+        return ctx->fail(PITT_E_INVALID, "cov_mode out of range");
     for (int f = 0; f < fr->n_frames; ++f) {
         const int64_t o = fr->offsets[f], n = fr->counts[f];
         if (o < 0 || n < 0 || (o & 3) != 0) return ctx->fail(PITT_E_INVALID, "frame offset must be >= 0 and a multiple of 4");

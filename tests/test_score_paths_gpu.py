@@ -2,8 +2,8 @@
 (compaction, v_cmp -> s_bcnt1 -> v_writelane per surviving (group, hypothesis) pair) and the
 lane-counter scorer (k_score LANE: every surviving pair with full-rate VALU only, |d| - t sign bits
 added into lane-private counters).  Either way a pair whose group box lies certainly inside the slab
-may count the group's non-NaN points without scoring them ($PITT_INSIDE_CULL, off by default).  $PITT_LANE_SCORE picks one when a context is created; the other
-is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
+may count the group's non-NaN points without scoring them ($PITT_INSIDE_CULL, off by default).  $PITT_LANE_SCORE picks one when a context is created (A/B
+build only); the other is run here on the bit-exact parity tests of the plane path, so both stay exact.  Likewise k_refine's
 producer count ($PITT_REFINE_PRODUCERS, 1..4 waves selecting steps in parallel and appending in
 step order): every count must give the same ascending inlier stream, hence the same floats.  The
 refinement itself has two paths: k_refine's serial chain (default) and k_xrefine's binade runs
@@ -16,10 +16,15 @@ import os
 import pytest
 
 import pitt_object_table_segmentation_amd as pitt
+from pitt_object_table_segmentation_amd import _lib
 import test_plane_gpu as P
 import test_shortcuts_gpu as S
 
-pytestmark = pytest.mark.gpu
+# The variants exist only in the A/B build (libpitt_seg_ab.so, `make ab`); the product library ignores
+# their environment knobs.  tests/test_variants_gpu.py runs this module under the A/B build.
+AB_BUILD = bool(_lib.lib.pitt_build_flags() & _lib.PITT_BUILD_AB_VARIANTS)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not AB_BUILD, reason="A/B variants: run under libpitt_seg_ab.so "
+                                                                          "(tests/test_variants_gpu.py)")]
 
 
 VARIANTS = [{"PITT_LANE_SCORE": "0"}, {"PITT_LANE_SCORE": "1"}, {"PITT_REFINE_PRODUCERS": "1"},
@@ -59,43 +64,3 @@ def test_both_scoring_paths_bit_exact(path_ctx, case):
 def test_both_paths_reduce_orders(path_ctx):
     for order in (pitt.REDUCE_SSE2, pitt.REDUCE_HADD, pitt.REDUCE_SEQ):
         P.test_reduce_orders_and_division_modes(path_ctx, order, pitt.DIV_EIGEN32)
-
-
-def test_hip_graph_replay_bit_exact():
-    """Repeated batch layouts are captured into a HIP graph (second sight) and replayed (third on):
-    the replays give the same records and inlier lists as direct launches ($PITT_GRAPHS=0) and the
-    oracle (pipelining)."""
-    import numpy as np
-    import torch
-    frames = [pitt.synth_frame(s, seed, 320, 240) for s, seed in ((0, 7000), (1, 7001), (2, 7002), (0, 7003))]
-    b = pitt.FrameBatch.from_host(frames, device="cuda:0")
-    old = {k: os.environ.get(k) for k in ("PITT_GRAPHS", "PITT_GRAPH_MIN_FRAMES")}
-    try:
-        os.environ["PITT_GRAPHS"] = "0"
-        direct = pitt.Context(0)
-        os.environ["PITT_GRAPHS"] = "1"
-        os.environ["PITT_GRAPH_MIN_FRAMES"] = "1"  # graphs for this 4-frame layout (default: 64 frames and up)
-        graphed = pitt.Context(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    try:
-        ref_inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
-        ref = direct.plane_segment_batch(b, pitt.sac_params(), ref_inl)
-        inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")  # one output buffer: one layout key
-        for k in range(4):
-            inl.fill_(-7)
-            res = graphed.plane_segment_batch(b, pitt.sac_params(), inl)
-            assert res.tobytes() == ref.tobytes(), k
-            for o, r in zip(b.offsets, ref):
-                assert torch.equal(inl[o:o + r["n_inliers"]], ref_inl[o:o + r["n_inliers"]]), k
-        captures, replays = graphed.graph_stats()
-        assert captures == 1 and replays == 3
-        assert direct.graph_stats() == (0, 0)
-        P._check(graphed, frames, ref, [ref_inl.cpu().numpy()[o:o + r["n_inliers"]] for o, r in zip(b.offsets, ref)])
-    finally:
-        direct.close()
-        graphed.close()

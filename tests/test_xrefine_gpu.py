@@ -12,9 +12,12 @@ import pytest
 import torch
 
 import pitt_object_table_segmentation_amd as pitt
+from pitt_object_table_segmentation_amd import _lib
 import test_plane_gpu as P
 
-pytestmark = pytest.mark.gpu
+# k_xrefine is an A/B variant: compiled only into libpitt_seg_ab.so (tests/test_variants_gpu.py)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not (_lib.lib.pitt_build_flags() & _lib.PITT_BUILD_AB_VARIANTS),
+                                                  reason="A/B variant: run under libpitt_seg_ab.so")]
 
 
 def _ctx(xrefine):

@@ -75,9 +75,11 @@ def main(tag):
                                   algorithmic_bytes_per_launch=bench["roofline"]["algorithmic_bytes_per_launch"],
                                   correction="FETCH_SIZE x 1024 x 2 (gfx950 half-count) + WRITE_SIZE x 1024")
         with open(os.path.join(ROOT, "profiles", "pmc_k_score.json"), "w") as f:
+            # stamped with the library the passes ran (bench.py prints its sha256): bench.py reports
+            # this traffic only for that same build
             json.dump(dict(tag=tag, hbm_bytes_per_launch=round(hbm, 1), launches=len(per),
-                           algorithmic_bytes_per_launch=bench["roofline"]["algorithmic_bytes_per_launch"]), f,
-                      indent=1)
+                           algorithmic_bytes_per_launch=bench["roofline"]["algorithmic_bytes_per_launch"],
+                           library_sha16=bench.get("library_sha16")), f, indent=1)
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench"}, indent=1))
