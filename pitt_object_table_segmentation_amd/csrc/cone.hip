@@ -13,11 +13,11 @@
 //                      distance - tan(angle) |apex - proj||, d_normal = min(a, pi - a) of the angle between
 //                      the normal and sinf(angle) * unit(apex - proj) + cosf(angle) * unit(p - proj);
 //   computeModel       the plane loop with w^3;
-//   optimize           the double Levenberg-Marquardt of lm.hpp on f = |v|^2 - (1 + tan^2 a) (u.v)^2 / |u|^2
-//                      (v = apex - p: the functor's residual by Lagrange's identity); PCL runs Eigen's float
-//                      LM: equal within its tolerance, not bit for bit.
-// A7: acosf / sinf / cosf are taken as correctly rounded -- (float) of the double function, here and in
-// the oracle -- so host libm and the device's agree except for values within 2^-29 of a rounding boundary.
+//   optimize           Eigen's float Levenberg-Marquardt with numerical differences on OptimizationFunctor's
+//                      residual (float)(sqrPointToLineDistance(p, apex, dir) - (tanf(a) |apex - proj(p)|)^2)
+//                      (elm.hpp, bit for bit the oracle's pcl_lm_cone), the direction normalised afterwards.
+// A7: acosf / sinf / cosf / tanf are taken as correctly rounded -- (float) of the double function, here and
+// in the oracle -- so host libm and the device's agree except for values within 2^-29 of a rounding boundary.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,7 +29,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
-#include "lm.hpp"
+#include "elm.hpp"
 #include "prim_ransac.hpp"
 #include "vec4.hpp"
 
@@ -187,26 +187,6 @@ __global__ void k_cone_prepare(Coef7 m, ConeCfg cfg, ConePrep* out) {
     *out = r;
 }
 
-struct ConeResidual {
-    static constexpr int64_t kSmall = 2048;  // one block measured slower than the grid at 4k inliers
-    __device__ static double aux(const double* q) { return tan(q[6]); }  // q[7] below
-    __device__ void operator()(const double* q, float px, float py, float pz, double J[7], double* f) const {
-        const double vx = q[0] - px, vy = q[1] - py, vz = q[2] - pz;
-        const double ux = q[3], uy = q[4], uz = q[5];
-        const double s = ux * ux + uy * uy + uz * uz, g = ux * vx + uy * vy + uz * vz;
-        const double t = q[7], K = 1.0 + t * t;
-        *f = (vx * vx + vy * vy + vz * vz) - K * g * g / s;
-        const double a = 2.0 * K * g / s;
-        J[0] = 2.0 * vx - a * ux;
-        J[1] = 2.0 * vy - a * uy;
-        J[2] = 2.0 * vz - a * uz;
-        J[3] = -a * (vx - g * ux / s);
-        J[4] = -a * (vy - g * uy / s);
-        J[5] = -a * (vz - g * uz / s);
-        J[6] = -(g * g / s) * 2.0 * t * K;
-    }
-};
-
 // prim_ransac.hpp traits of the cone service
 struct ConeModelT {
     using Coef = Coef7;
@@ -245,10 +225,10 @@ struct ConeModelT {
         hipLaunchKernelGGL((k_pred_apply<ConeIn, ConeWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,
                            ConeWriteIdx{c.inliers}, c.n, to);
     }
-    // any inliers: the refinement (fewer than 7: the model unchanged, its direction normalised)
-    using LmP = Lm7Model<ConeResidual>;
+    // any inliers: PCL's float Levenberg-Marquardt (fewer than 7: the model unchanged, its direction
+    // normalised)
+    using Elm = ElmCone;
     static int refine_kind(int64_t n_inliers) { return n_inliers >= 7 ? 1 : n_inliers > 0 ? 2 : 0; }
-    static LmP lm_params(const Coef7& bc) { return LmP{bc}; }
     void launch_normalize(hipStream_t s, const Coef7& bc, Coef7* out) const {
         hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
     }

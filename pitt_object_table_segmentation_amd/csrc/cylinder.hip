@@ -15,11 +15,9 @@
 //                      distance - r|, d_normal = min(angle, pi - angle) between the normal and the radial
 //                      direction (getAngle3D: acos of the clamped dot of the normalized vectors);
 //   computeModel       the plane loop with w^2;
-//   optimize           Levenberg-Marquardt on OptimizationFunctor's residual sqrPointToLineDistance - r^2 over
-//                      the inliers, the direction normalised as a Vector3f afterwards.  PCL runs Eigen's
-//                      float LM with numerical differences; this runs a double LM (one block, deterministic
-//                      sums) to the least-squares optimum: the axis and radius match PCL's within that
-//                      tolerance, not bit for bit (the point on the axis may slide along it).
+//   optimize           Eigen's float Levenberg-Marquardt with numerical differences on OptimizationFunctor's
+//                      residual (float)(sqrPointToLineDistance - r^2) over the inliers (elm.hpp, bit for bit
+//                      the oracle's pcl_lm_cylinder), the direction normalised as a Vector3f afterwards.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,7 +29,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
-#include "lm.hpp"
+#include "elm.hpp"
 #include "prim_ransac.hpp"
 #include "vec4.hpp"
 
@@ -144,29 +142,6 @@ struct CylWriteIdx {
     __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = (int32_t)i; }
 };
 
-// f = |u x (c - p)|^2 / |u|^2 - r^2 and its gradient in (c, u, r)
-__device__ __forceinline__ void cyl_residual(const double* v, float px, float py, float pz, double J[7], double* f) {
-    const double vx = v[0] - px, vy = v[1] - py, vz = v[2] - pz;
-    const double ux = v[3], uy = v[4], uz = v[5];
-    const double wx = uy * vz - uz * vy, wy = uz * vx - ux * vz, wz = ux * vy - uy * vx;
-    const double s = ux * ux + uy * uy + uz * uz, w2 = wx * wx + wy * wy + wz * wz;
-    *f = w2 / s - v[6] * v[6];
-    J[0] = 2.0 * (wy * uz - wz * uy) / s;
-    J[1] = 2.0 * (wz * ux - wx * uz) / s;
-    J[2] = 2.0 * (wx * uy - wy * ux) / s;
-    J[3] = 2.0 * (vy * wz - vz * wy) / s - 2.0 * w2 * ux / (s * s);
-    J[4] = 2.0 * (vz * wx - vx * wz) / s - 2.0 * w2 * uy / (s * s);
-    J[5] = 2.0 * (vx * wy - vy * wx) / s - 2.0 * w2 * uz / (s * s);
-    J[6] = -2.0 * v[6];
-}
-struct CylResidual {
-    static constexpr int64_t kSmall = 6144;
-    __device__ static double aux(const double*) { return 0.0; }
-    __device__ void operator()(const double* v, float px, float py, float pz, double J[7], double* f) const {
-        cyl_residual(v, px, py, pz, J, f);
-    }
-};
-
 // prim_ransac.hpp traits of the cylinder service
 struct CylPrep {
     int32_t valid;
@@ -210,11 +185,10 @@ struct CylModel {
         hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,
                            CylWriteIdx{c.inliers}, c.n, to);
     }
-    // any inliers: the least-squares refinement (7 or more: Eigen's LM refuses m < n, the model then
+    // any inliers: PCL's float Levenberg-Marquardt (7 or more: Eigen's LM refuses m < n, the model then
     // stays and only the direction is normalised)
-    using LmP = Lm7Model<CylResidual>;
+    using Elm = ElmCylinder;
     static int refine_kind(int64_t n_inliers) { return n_inliers >= 7 ? 1 : n_inliers > 0 ? 2 : 0; }
-    static LmP lm_params(const Coef7& bc) { return LmP{bc}; }
     void launch_normalize(hipStream_t s, const Coef7& bc, Coef7* out) const {
         hipLaunchKernelGGL(k_lm7_normalize_dir<>, dim3(1), dim3(1), 0, s, bc, out);
     }

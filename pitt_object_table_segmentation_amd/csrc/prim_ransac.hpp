@@ -11,7 +11,7 @@
 //      counts back, and PCL's serial computeModel loop replayed per cloud on the host  1 sync / chunk
 //   3. the winning models back                                                    1 sync
 //   4. selectWithinDistance (isModelValid first; the cone's needs device math)     1-2 syncs
-//   5. optimizeModelCoefficients (lm.hpp), the refined models back, select again   2-3 syncs
+//   5. optimizeModelCoefficients (elm.hpp), the refined models back, select again   2-3 syncs
 // Per cloud the launches, their order and every value are those of the single-cloud service, so a
 // batch of one is the service (the single-cloud entry points call this with nc = 1).
 //
@@ -24,9 +24,10 @@
 //   launch_model / launch_count  the hypothesis and counting kernels of one cloud
 //   kDevicePrep, prep_host / launch_prep, prep_valid   isModelValid (+ constants) on host or device
 //   launch_select                k_pred_count / k_scan_tiles / k_pred_apply of one cloud
-//   refine_kind(n_inliers)       0: none, 1: refine (LmP, lm.hpp) and select again, 2: only normalise
-//                                the direction (Eigen's LM refuses m < n) and select again
-//   LmP, lm_params, launch_normalize   the refinement's lm.hpp model from a winning model
+//   refine_kind(n_inliers)       0: none, 1: refine (Elm: the model's OptimizationFunctor for elm.hpp's
+//                                float Levenberg-Marquardt) and select again, 2: only normalise the
+//                                direction (Eigen's LM refuses m < n) and select again
+//   Elm, launch_normalize        the refinement's functor; the direction normalisation of kind 2
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -40,7 +41,7 @@
 
 #include "compact.hpp"
 #include "ctx.hpp"
-#include "lm.hpp"
+#include "elm.hpp"
 
 namespace pitt {
 
@@ -110,6 +111,7 @@ struct PrimRun final : PrimRunBase {
     std::vector<St> st;
     std::vector<Coef> cur;
     std::vector<int> with_model, sel;
+    int32_t* elm_info = nullptr;  // optional device [nc][2]: the refinements' LM status and evaluations
 
     PrimRun(pitt_ctx* c, const M& model, const PrimCloud* clouds, int n, PrimResult* r) : ctx(c), m(model), cl(clouds), res(r) {
         nc = n;
@@ -289,32 +291,35 @@ struct PrimRun final : PrimRunBase {
         for (int c : sel) res[c].n_inliers = hto[c];
     }
 
-    // 5. optimizeModelCoefficients: the refinements of all clouds with at most LmP::kSmall inliers in one
-    //    launch (one block each, lm.hpp k_lm_batch), the larger ones on their own grid, the refined models
-    //    back; then the selection again with them
+    // 5. optimizeModelCoefficients: PCL's float Levenberg-Marquardt (elm.hpp) for every cloud at once, one
+    //    block each in one launch; the refined models back; then the selection again with them
     int issue_refine() override {
         refined.clear();
         if (!m.optimize) return PITT_OK;
-        using LmP = typename M::LmP;
-        std::vector<LmJob<LmP>> jobs;
+        using E = typename M::Elm;
+        std::vector<ElmJob> jobs;
         for (int c : with_model) {
             const int kind = m.refine_kind(res[c].n_inliers);
             if (!kind) continue;
-            const int rec = ctx->prof_begin((nm + "_lm").c_str(), (double)res[c].n_inliers * 12.0);
             if (kind == 2) {
                 m.launch_normalize(s, cur[(size_t)c], dref + c);
-            } else if (res[c].n_inliers <= LmP::kSmall) {
-                jobs.push_back(LmJob<LmP>{m.lm_params(cur[(size_t)c]), cl[c].x, cl[c].y, cl[c].z, cl[c].inliers,
-                                          res[c].n_inliers, dref + c});
             } else {
-                const int rc = launch_lm(ctx, s, m.lm_params(cur[(size_t)c]), cl[c].x, cl[c].y, cl[c].z,
-                                         cl[c].inliers, res[c].n_inliers, dref + c, (nm + "_lm_global").c_str());
-                if (rc != PITT_OK) return rc;
+                ElmJob jb = {};
+                jb.x = cl[c].x;
+                jb.y = cl[c].y;
+                jb.z = cl[c].z;
+                jb.inl = cl[c].inliers;
+                jb.m = res[c].n_inliers;
+                M::to_out(cur[(size_t)c], jb.start);
+                jb.out = reinterpret_cast<float*>(dref + c);
+                jb.info = elm_info ? elm_info + 2 * c : nullptr;
+                jobs.push_back(jb);
             }
-            ctx->prof_end(rec);
             refined.push_back(c);
         }
-        const int rc = launch_lm_batch(ctx, s, jobs, M::kName);
+        const int rec = jobs.empty() ? -1 : ctx->prof_begin((nm + "_lm").c_str(), 0.0);
+        const int rc = launch_elm_batch<E>(ctx, s, jobs, M::kName);
+        ctx->prof_end(rec);
         if (rc != PITT_OK) return rc;
         PITT_HIP_TRY(hipGetLastError());
         for (int c : refined) PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dref + c, sizeof(Coef), hipMemcpyDeviceToHost, s));

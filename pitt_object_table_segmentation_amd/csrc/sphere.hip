@@ -10,16 +10,14 @@
 //   countWithinDistance 0 for a model outside the radius limits, else
 //                      |sqrtf((x - a)^2 + (y - b)^2 + (z - c)^2) - r| < threshold (A4 float threshold);
 //   computeModel       the plane path's loop with w^4 (strict > first-best, k, max_skip = 10 x max_it);
-//   optimize...        more than 4 inliers: a least-squares refinement of ||p - c|| - r.  PCL runs
-//                      Eigen's float Levenberg-Marquardt with numerical differences (stopping at its
-//                      sqrt(eps) tolerances); this runs a double Levenberg-Marquardt on device sums to
-//                      the optimum -- the coefficients match PCL's within that tolerance, not bit for bit.
+//   optimize...        more than 4 inliers: Eigen's float Levenberg-Marquardt with numerical
+//                      differences on fvec = sqrtf(|p - c|^2) - r (elm.hpp, bit for bit the oracle's
+//                      pcl_lm_sphere).
 //
 // Device pipeline: k_sph_model (one thread per attempt: the 4 x 4 determinants), k_sph_count per
 // chunk of attempts (one 2048-point tile x one hypothesis per block, ballot counts), the RANSAC replay
 // on the host over the chunk's counts (scalar control), compaction of the inliers, and for the
-// refinement k_lm<SphLmModel> (lm.hpp): the whole Levenberg-Marquardt iteration in one resident grid
-// (deterministic sums).
+// refinement k_elm<ElmSphere> (elm.hpp): the whole float Levenberg-Marquardt in one block per cloud.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,7 +29,7 @@
 #include "compact.hpp"
 #include "ctx.hpp"
 #include "device_common.hpp"
-#include "lm.hpp"
+#include "elm.hpp"
 #include "prim_ransac.hpp"
 
 #pragma clang fp contract(off)
@@ -126,33 +124,6 @@ struct WriteIdx {
     __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = (int32_t)i; }
 };
 
-// Levenberg-Marquardt over the inliers' residuals ||p - c|| - r in double (lm.hpp's resident grid, 100
-// iterations, no diagonal floor), the coefficients written back as floats.
-struct SphLmModel {
-    static constexpr int N = 4;
-    static constexpr int kMaxIt = 100;
-    static constexpr double kDiagEps = 0.0;
-    static constexpr int64_t kSmall = 2048;
-    using Out = float4;
-    __device__ double aux(const double*) const { return 0.0; }
-    float4 start;
-    __device__ void init(double* v) const {
-        v[0] = start.x, v[1] = start.y, v[2] = start.z, v[3] = start.w;
-    }
-    __device__ void residual(const double* v, float px, float py, float pz, double* J, double* f) const {
-        const double dx = (double)px - v[0], dy = (double)py - v[1], dz = (double)pz - v[2];
-        const double d = sqrt(dx * dx + dy * dy + dz * dz);
-        *f = d - v[3];
-        J[0] = d > 0 ? -dx / d : 0.0;
-        J[1] = d > 0 ? -dy / d : 0.0;
-        J[2] = d > 0 ? -dz / d : 0.0;
-        J[3] = -1.0;
-    }
-    __device__ void finish(const double* xv, float4* out) const {
-        *out = make_float4((float)xv[0], (float)xv[1], (float)xv[2], (float)xv[3]);
-    }
-};
-
 // prim_ransac.hpp traits of the sphere service
 struct SphPrep {
     int32_t valid;
@@ -196,11 +167,10 @@ struct SphModel {
         hipLaunchKernelGGL((k_pred_apply<SphIn, WriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, WriteIdx{c.inliers}, c.n,
                            to);
     }
-    // more than 4 inliers: Levenberg-Marquardt in double, the whole iteration in one launch (the
-    // oracle's sphere_refine; fixed reduction order, so the same bits on every run)
-    using LmP = SphLmModel;
+    // more than 4 inliers (sac_model_sphere.hpp: "Not enough inliers" below): PCL's float
+    // Levenberg-Marquardt on the sphere's OptimizationFunctor (elm.hpp), bit-exact with the oracle
+    using Elm = ElmSphere;
     static int refine_kind(int64_t n_inliers) { return n_inliers > 4 ? 1 : 0; }
-    static SphLmModel lm_params(const float4& bc) { return SphLmModel{bc}; }
     void launch_normalize(hipStream_t, const float4&, float4*) const {}
 };
 

@@ -9,11 +9,11 @@ Pins (CPU):
     an independent implementation of the same algorithm): on the sphere the same function-evaluation
     count and the same solution to ~1e-12; on the rank-deficient cylinder / cone parameterisations
     (a point sliding along the axis, a free direction scale) the same geometry;
-  * PCL's float LM against the least-squares optimum the device computes: the envelope below holds
-    on every test cluster, the final inlier sets are identical, and the arbitration of
-    ransac_segmentation.cpp:265-302 decides the same.
-The GPU tests (test_sphere / test_cylinder / test_cone / test_services_gpu) hold the device to both:
-the optimum tightly, PCL's float LM within this envelope."""
+  * PCL's float LM against the least-squares optimum (a double LM): the envelope below holds on every
+    test cluster, and the arbitration of ransac_segmentation.cpp:265-302 decides the same.
+The device runs the same float LM (csrc/elm.hpp, round 4): the GPU tests (test_sphere / test_cylinder /
+test_cone / test_services_gpu / test_classify_gpu) hold its coefficients and final inlier sets to this
+restatement bit for bit, and to the optimum within the envelope."""
 import numpy as np
 import pytest
 
@@ -171,8 +171,8 @@ def _box(n, seed):
 
 def test_arbitration_unchanged_by_the_lm_stopping_point():
     """ransac_segmentation.cpp:265-302 picks the primitive from the four services' inlier counts: on
-    clusters of each kind the counts after PCL's float LM and after the optimum (the device's
-    refinement) decide the same primitive."""
+    clusters of each kind the counts after PCL's float LM and after the optimum decide the same
+    primitive."""
     import pitt_object_table_segmentation_amd as pitt
     clusters = [sphere_scene(1500, 200, 31), cylinder_scene(1500, 200, 32)[0],
                 cone_scene(1500, 200, 33, half_deg=25.0)[0], _box(1500, 34)]
