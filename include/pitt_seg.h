@@ -133,6 +133,10 @@ int  pitt_set_stream(pitt_ctx* ctx, void* hip_stream);
 int  pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes);
 /* Plane batches captured into HIP graphs / replayed from them on this context ($PITT_GRAPHS=0 off). */
 int  pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays);
+/* The adaptive chunk schedule on this context: batches that ran past the scoring chunks the hint
+ * scheduled (a continuation finished them), and the chunks the last batch launched up front
+ * ($PITT_ADAPTIVE_CHUNKS=0 always launches every chunk). */
+int  pitt_schedule_stats(pitt_ctx* ctx, int64_t* continuations, int32_t* last_chunks);
 /* Refined plane batches completed with the binade-run refinement (k_xrefine) on this context, and
  * the frames it handed back to the serial chain ($PITT_XREFINE=0 selects the chain for every frame). */
 int  pitt_refine_stats(pitt_ctx* ctx, int64_t* batches, int64_t* fallback_frames);

@@ -219,6 +219,7 @@ _i64p = ctypes.POINTER(ctypes.c_int64)
 SIGNATURES = {
     "pitt_abi_version": (_i32, []),
     "pitt_build_flags": (_i32, []),
+    "pitt_schedule_stats": (_i32, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
     "pitt_sac_params_default": (None, [ctypes.POINTER(SacParams)]),
     "pitt_create": (_i32, [ctypes.POINTER(_vp), _i32]),
     "pitt_destroy": (None, [_vp]),

@@ -480,6 +480,13 @@ class Context:
         self._check(lib.pitt_graph_stats(self.h, ctypes.byref(c), ctypes.byref(r)), "pitt_graph_stats")
         return c.value, r.value
 
+    def schedule_stats(self):
+        """(batches finished by a continuation past their scheduled chunks, chunks the last batch launched
+        up front) of the adaptive chunk schedule on this context."""
+        c, k = ctypes.c_int64(0), ctypes.c_int32(0)
+        self._check(lib.pitt_schedule_stats(self.h, ctypes.byref(c), ctypes.byref(k)), "pitt_schedule_stats")
+        return c.value, k.value
+
     def refine_stats(self):
         """(batches refined by k_xrefine, frames it handed back to k_refine's serial chain)."""
         b, f = ctypes.c_int64(0), ctypes.c_int64(0)

@@ -3,7 +3,9 @@
 #include <cstdlib>
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <tuple>
 #include <string>
@@ -121,7 +123,51 @@ struct pitt_ctx {
     // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the
     // GPU, otherwise bounds the pipelined throughput.  $PITT_GRAPHS=0 disables.
     bool use_graphs = pitt_env_flag("PITT_GRAPHS", true);
-    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 64, 1, 1 << 30);  // smaller batches launch directly
+    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 1, 1, 1 << 30);  // smaller batches launch directly
+    // Adaptive chunk schedule (plane_ransac.hip): a batch launches the scoring chunks that the last
+    // batches of its layout needed; a frame still running after them is finished by a continuation.
+    // Exact either way; $PITT_ADAPTIVE_CHUNKS=0 always launches the whole schedule.
+    bool adaptive_chunks = pitt_env_flag("PITT_ADAPTIVE_CHUNKS", true);
+    // batches of up to this many frames refine through the chip-wide exact walk (xsum.hpp) instead of
+    // k_refine's per-frame chain (same sums, lower latency); $PITT_XS_MAX_FRAMES=0 keeps the chain always
+    int xs_max_frames = pitt_env_int("PITT_XS_MAX_FRAMES", 8, 0, 1 << 30);
+    struct ChunkHint {
+        std::array<uint64_t, 4> key;  // frame planes, frames, hypothesis cap, tiles
+        int need[4];                  // chunks with active frames in the last batches (0: none yet)
+        int pos;
+        uint64_t last_use;
+    };
+    std::vector<ChunkHint> chunk_hints;
+    uint64_t hint_clock = 0;
+    int64_t continuations = 0;        // batches that ran past their scheduled chunks
+    // chunks to launch for a layout: the most the last four batches needed (all of them when unknown)
+    int chunk_hint(const std::array<uint64_t, 4>& key, int all) {
+        for (ChunkHint& h : chunk_hints)
+            if (h.key == key) {
+                h.last_use = ++hint_clock;
+                int k = 0;
+                for (int v : h.need) k = v > k ? v : k;
+                return k > 0 ? k : all;
+            }
+        return all;
+    }
+    void chunk_hint_update(const std::array<uint64_t, 4>& key, int need) {
+        ChunkHint* h = nullptr;
+        for (ChunkHint& e : chunk_hints)
+            if (e.key == key) h = &e;
+        if (!h) {
+            if (chunk_hints.size() >= 16) {
+                size_t lru = 0;
+                for (size_t i = 1; i < chunk_hints.size(); ++i)
+                    if (chunk_hints[i].last_use < chunk_hints[lru].last_use) lru = i;
+                chunk_hints.erase(chunk_hints.begin() + (long)lru);
+            }
+            chunk_hints.push_back(ChunkHint{key, {0, 0, 0, 0}, 0, ++hint_clock});
+            h = &chunk_hints.back();
+        }
+        h->need[h->pos] = need;
+        h->pos = (h->pos + 1) & 3;
+    }
     uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
     struct GraphEntry {
         std::vector<uint64_t> key;
@@ -152,6 +198,9 @@ struct pitt_ctx {
     void* inflight_acct = nullptr;        // pinned copy of the device byte counters (profiling)
     std::vector<int> inflight_acct_recs;  // profiler record per counted kernel (-1: none)
     int64_t inflight_acct_tiles = 0;      // per-tile byte words following the counters
+    int inflight_k = 0;                   // scoring chunks the batch launched
+    std::array<uint64_t, 4> inflight_hint_key = {0, 0, 0, 0};
+    std::function<int(std::vector<int>&, std::vector<int>&)> inflight_cont;  // the rest of the chunks, if any
 
     // support loop: z sums that could not be certified and ran the sequential loop (diagnostic)
     int64_t zsum_sequential = 0;

@@ -24,6 +24,7 @@
 #include "ctx.hpp"
 #include "device_common.hpp"
 #include "score_list_asm.inc"
+#include "xsum.hpp"
 
 #pragma clang fp contract(off)
 
@@ -858,13 +859,18 @@ extend:
 }
 
 // ------------------------------------------------------------------------------------------
-// After the last chunk: decide model / refinement per frame (one thread per frame).
+// After the chunks: decide model / refinement per frame (one thread per frame).  A batch may run its
+// chunks in two phases (run_plane_batch: the chunks recent batches needed, then -- only when a frame is
+// still running -- the rest): phase p decides the frames that have finished and are not decided yet
+// (FrameState.pad1 = the phase that decided the frame), and k_refine refines only those.
 __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
                          const float4* __restrict__ hyp_coef, int hcap, int n_frames, int optimize,
-                         float4* __restrict__ best_coef, float4* __restrict__ final_coef) {
+                         float4* __restrict__ best_coef, float4* __restrict__ final_coef, int phase) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_frames) return;
     FrameState s = st[f];
+    if (!s.done || s.pad1 != 0) return;  // still running (a later phase decides it), or decided already
+    s.pad1 = phase;
     s.has_model = (s.best_h >= 0 && s.status == PITT_OK) ? 1 : 0;
     if (!s.has_model && s.status == PITT_OK) s.status = PITT_NO_MODEL;
     s.need_refine = (s.has_model && optimize && s.best_count >= 4) ? 1 : 0;
@@ -1382,12 +1388,12 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
     int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct,
-    unsigned long long* __restrict__ rdbg, int mode, const int32_t* __restrict__ only) {
+    unsigned long long* __restrict__ rdbg, int mode, const int32_t* __restrict__ only, int phase) {
     __shared__ RefineLds<P> L;
     const long long t_start = rdbg ? clock64() : 0;
     const int f = blockIdx.x;
     const FrameState s = st[f];
-    if (!s.has_model || !s.need_refine) return;
+    if (!s.has_model || !s.need_refine || s.pad1 != phase) return;
     if (only && !only[f]) return;  // after k_xrefine: only the frames it handed back
     const FrameMeta m = meta[f];
     const int lane = threadIdx.x & 63;
@@ -2213,6 +2219,141 @@ __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __r
 }
 
 // ------------------------------------------------------------------------------------------
+// Small batches (a service call, a support-loop iteration, one camera frame): optimizeModelCoefficients'
+// nine exact-order sums by the block-parallel exact walk (xsum.hpp) over the whole chip instead of one
+// frame's serial chain in k_refine -- the same float sums, so the same refined plane, at a fraction of
+// the latency (a 600k-inlier support plane: ~2.5 ms of chain).  The winning model's inliers, ascending,
+// become nine product streams (PCL's separately rounded xx, xy, xz, yy, yz, zz, then x, y, z) in one
+// 256-aligned segment per frame.
+__device__ __forceinline__ bool xr_eligible(const FrameState& s, int phase) {
+    return s.has_model && s.need_refine && s.pad1 == phase;
+}
+
+// per (frame, tile) wave: the tile's inliers of the winning model
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X, const float* __restrict__ Y,
+                                                     const float* __restrict__ Z, const FrameMeta* __restrict__ meta,
+                                                     const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
+                                                     float thf, int n_frames, int tiles_max, int32_t* __restrict__ tcnt,
+                                                     int phase) {
+    const int lane = threadIdx.x & 63;
+    const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    const int f = it / tiles_max, t = it - f * tiles_max;
+    if (f >= n_frames) return;
+    const FrameMeta m = meta[f];
+    int cnt = 0;
+    if (t < m.tiles && xr_eligible(st[f], phase)) {
+        const float4 c = best_coef[f];
+        float tv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+        for (int g = 0; g < kTile / 64; ++g) {
+            const int64_t i = (int64_t)t * kTile + 64 * g + lane;
+            const bool in = i < m.n && fabsf(plane_dot<ORDER>(c, X[m.off + i], Y[m.off + i], Z[m.off + i])) < tv;
+            cnt += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in));
+        }
+    }
+    if (lane == 0) tcnt[(int64_t)f * tiles_max + t] = cnt;
+}
+
+// one block per frame: the tiles' inlier offsets, the frame's segment (first block: the previous frames'
+// point spans, 256-aligned) and its length, and the block -> segment map of its span
+__global__ __launch_bounds__(256) void k_xr_scan(const FrameMeta* __restrict__ meta, int tiles_max,
+                                                 int32_t* __restrict__ tcnt, XsSeg* __restrict__ seg,
+                                                 int32_t* __restrict__ blk_seg) {
+    const int f = blockIdx.x;
+    __shared__ int64_t base;
+    __shared__ int32_t part[256];
+    const FrameMeta m = meta[f];
+    if (threadIdx.x == 0) {
+        int64_t b = 0;
+        for (int g = 0; g < f; ++g) b += (meta[g].n + kXsBlk - 1) / kXsBlk;
+        base = b;
+    }
+    int32_t* c = tcnt + (int64_t)f * tiles_max;
+    const int per = (m.tiles + 255) / 256;
+    const int a = (int)threadIdx.x * per, e = min(a + per, m.tiles);
+    int acc = 0;
+    for (int i = a; i < e; ++i) acc += c[i];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int i = 0; i < 256; ++i) {
+            const int t = part[i];
+            part[i] = run;
+            run += t;
+        }
+        seg[f] = XsSeg{base, (int64_t)run};
+    }
+    __syncthreads();
+    acc = part[threadIdx.x];
+    for (int i = a; i < e; ++i) {  // in place: count -> exclusive offset
+        const int t = c[i];
+        c[i] = acc;
+        acc += t;
+    }
+    const int64_t nb = (m.n + kXsBlk - 1) / kXsBlk;
+    for (int64_t b = threadIdx.x; b < nb; b += 256) blk_seg[base + b] = f;
+}
+
+// per (frame, tile) wave: the tile's inliers' nine products at their ascending positions
+template <int ORDER>
+__global__ __launch_bounds__(kBlock) void k_xr_write(const float* __restrict__ X, const float* __restrict__ Y,
+                                                     const float* __restrict__ Z, const FrameMeta* __restrict__ meta,
+                                                     const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
+                                                     float thf, int n_frames, int tiles_max, const int32_t* __restrict__ toff,
+                                                     const XsSeg* __restrict__ seg, float* __restrict__ V, int64_t T,
+                                                     int phase) {
+    const int lane = threadIdx.x & 63;
+    const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    const int f = it / tiles_max, t = it - f * tiles_max;
+    if (f >= n_frames) return;
+    const FrameMeta m = meta[f];
+    if (t >= m.tiles || !xr_eligible(st[f], phase)) return;
+    const float4 c = best_coef[f];
+    float tv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+    int64_t pos = seg[f].blk0 * kXsBlk + toff[(int64_t)f * tiles_max + t];
+    for (int g = 0; g < kTile / 64; ++g) {
+        const int64_t i = (int64_t)t * kTile + 64 * g + lane;
+        float x = 0.0f, y = 0.0f, z = 0.0f;
+        bool in = false;
+        if (i < m.n) {
+            x = X[m.off + i];
+            y = Y[m.off + i];
+            z = Z[m.off + i];
+            in = fabsf(plane_dot<ORDER>(c, x, y, z)) < tv;
+        }
+        const uint64_t b = __builtin_amdgcn_ballot_w64(in);
+        if (in) {
+            const int64_t p = pos + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            V[p] = x * x;
+            V[T + p] = x * y;
+            V[2 * T + p] = x * z;
+            V[3 * T + p] = y * y;
+            V[4 * T + p] = y * z;
+            V[5 * T + p] = z * z;
+            V[6 * T + p] = x;
+            V[7 * T + p] = y;
+            V[8 * T + p] = z;
+        }
+        pos += __builtin_popcountll(b);
+    }
+}
+
+// one thread per frame: the refined plane from the nine sums (k_refine's refine_plane)
+template <int ORDER, int DIV>
+__global__ void k_xr_plane(const FrameState* __restrict__ st, const XsSeg* __restrict__ seg,
+                           const float* __restrict__ sums, int n_frames, float4* __restrict__ final_coef, int phase) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames || !xr_eligible(st[f], phase)) return;
+    float a9[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a9[k] = sums[f * 9 + k];
+    final_coef[f] = refine_plane<ORDER, DIV>(a9, (int)seg[f].len);
+}
+
+// ------------------------------------------------------------------------------------------
 // Host orchestration.
 
 template <typename T>
@@ -2357,6 +2498,29 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         if (!rdbg || !ctx->refine_dbg_h) return ctx->fail(PITT_E_NOMEM, "refine debug");
     }
 
+    // small batches refine through the chip-wide exact walk (k_xr_*, xsum.hpp) instead of k_refine's chain
+    bool xs = p->optimize && p->cov_mode != PITT_COV_FAST && nf <= ctx->xs_max_frames;
+    if constexpr (pitt_ctx::kVariants)  // the A/B build keeps k_refine whenever one of its variants is asked for
+        xs = xs && ctx->refine_producers == 1 && ctx->refine_frames == 1 && ctx->xrefine == 0 &&
+             ctx->refine_mode == 2 && !ctx->refine_debug;
+    int64_t xs_blocks = 0;
+    for (int f = 0; f < nf; ++f) xs_blocks += (fr->counts[f] + kXsBlk - 1) / kXsBlk;
+    const int64_t xs_T = std::max<int64_t>(1, xs_blocks) * kXsBlk;
+    float* xr_v = nullptr;
+    int32_t *xr_tcnt = nullptr, *xr_bseg = nullptr;
+    XsSeg* xr_seg = nullptr;
+    float* xr_sums = nullptr;
+    XsScratch xr_scr;
+    if (xs) {
+        xr_v = as<float>(ctx->buf("xr_v", (size_t)9 * xs_T * 4));
+        xr_tcnt = as<int32_t>(ctx->buf("xr_tcnt", (size_t)nf * tiles_max * 4));
+        xr_bseg = as<int32_t>(ctx->buf("xr_bseg", (size_t)(xs_T / kXsBlk) * 4));
+        xr_seg = as<XsSeg>(ctx->buf("xr_seg", (size_t)nf * sizeof(XsSeg)));
+        xr_sums = as<float>(ctx->buf("xr_sums", (size_t)nf * 9 * 4));
+        if (!xr_v || !xr_tcnt || !xr_bseg || !xr_seg || !xr_sums) return ctx->fail(PITT_E_NOMEM, "refinement streams");
+        if (int rc = xs_scratch(ctx, xs_T / kXsBlk, 9, "xr", &xr_scr)) return rc;
+    }
+
     // Everything below is stream-ordered device work with device-built work lists.  Its launches
     // depend only on the key below, so a repeated batch layout is captured into a HIP graph and
     // replayed with one launch (profiling runs launch directly: their events time each kernel).
@@ -2364,17 +2528,33 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     const double log_prob = std::log(1.0 - p->probability);
     std::vector<int> acct_recs((size_t)kAcKernels, -1);
     std::vector<int> score_recs;
-    auto enqueue = [&]() -> int {
-    PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
-
+    // Adaptive chunk schedule: launch only the scoring chunks that recent batches of this layout needed
+    // (table scenes finish after 2 of 7; every launch past that would find no active frame).  A frame
+    // still running after them is finished by a continuation in finish_batch (the remaining chunks, then
+    // the decision, refinement and selection of the frames it finished): exact either way.
+    const std::array<uint64_t, 4> hint_key = {(uint64_t)(uintptr_t)fr->x, (uint64_t)nf, (uint64_t)hcap,
+                                              (uint64_t)tiles_max};
+    const int K = ctx->adaptive_chunks ? std::min(nchunks, ctx->chunk_hint(hint_key, nchunks)) : nchunks;
+    // everything the launches use, by value: a continuation runs after this call has returned
+    const float *fx = fr->x, *fy = fr->y, *fz = fr->z;
+    const int optimize = p->optimize ? 1 : 0, cov_mode = p->cov_mode;
+    // chunks [c0, c1) with their replays (front: the state reset and first hypotheses before them), then
+    // phase `phase`'s decisions, refinements, the final selection and the result copies
+    auto enqueue = [=](int c0, int c1, int phase, bool front, std::vector<int>& acct_recs,
+                       std::vector<int>& score_recs) -> int {
     int rec;
+    if (front) {
+    PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
     rec = ctx->prof_begin("k_hypothesize", 0.0);
     acct_recs[kAcHyp] = rec;
-    hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta,
+    hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fx, fy, fz, meta,
                        tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
                        counters, cstat, acct);
     ctx->prof_end(rec);
-    for (int c = 0, h0 = 0; c < nchunks; h0 += chunks[(size_t)c], ++c) {
+    }
+    int h0 = 0;
+    for (int c = 0; c < c0; ++c) h0 += chunks[(size_t)c];
+    for (int c = c0; c < c1; h0 += chunks[(size_t)c], ++c) {
         const int H = chunks[(size_t)c];
         rec = ctx->prof_begin("k_score", 0.0);
         if (c == 0) ctx->prof_alias(rec, "k_score.first");  // the first chunk: every frame, H hypotheses
@@ -2395,7 +2575,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         // the first chunk scores every frame (one item per wave); later ones stride over a capped grid
         const int64_t all_blocks = ((int64_t)nf * tiles_max + kScoreWaves - 1) / kScoreWaves;
         const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
-        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fr->x, fr->y, fr->z, meta, st, hyp_coef,
+        hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fx, fy, fz, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
                            tile_box, group_box);
         ctx->prof_end(rec);
@@ -2404,28 +2584,39 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int target_next = c + 1 < nchunks ? std::min(h0 + H + chunks[(size_t)c + 1], hcap) : 0;
         hipLaunchKernelGGL((k_replay<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride,
                            tiles_max, h0, H, max_iter, log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf,
-                           counters + c + 1, cstat + c + 1, fr->x, fr->y, fr->z, tables, A, target_next, hyp_coef,
+                           counters + c + 1, cstat + c + 1, fx, fy, fz, tables, A, target_next, hyp_coef,
                            hyp_attempt, acct);
         ctx->prof_end(rec);
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
-                       p->optimize ? 1 : 0, best_coef, final_coef);
+                       optimize, best_coef, final_coef, phase);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
-    if (p->cov_mode == PITT_COV_FAST) {  // A6 fast mode: double sums over the chip, fixed tree
+    if (cov_mode == PITT_COV_FAST) {  // A6 fast mode: double sums over the chip, fixed tree
         rec = ctx->prof_begin("k_cov_tiles", 0.0);
-        hipLaunchKernelGGL((k_cov_tiles<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
+        hipLaunchKernelGGL((k_cov_tiles<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st,
                            best_coef, thf, tile_counts, hstride, nf, tiles_max, part);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_cov_final", 0.0);
         hipLaunchKernelGGL((k_cov_final<ORDER>), dim3(nf), dim3(64), 0, sm, meta, st, part, nf, tiles_max, final_coef);
         ctx->prof_end(rec);
+    } else if (xs) {  // small batch: the nine sums by the exact walk over the chip
+        rec = ctx->prof_begin("k_refine:xsum", 0.0);
+        hipLaunchKernelGGL((k_xr_count<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
+                           thf, nf, tiles_max, xr_tcnt, phase);
+        hipLaunchKernelGGL(k_xr_scan, dim3(nf), dim3(256), 0, sm, meta, tiles_max, xr_tcnt, xr_seg, xr_bseg);
+        hipLaunchKernelGGL((k_xr_write<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
+                           thf, nf, tiles_max, xr_tcnt, xr_seg, xr_v, xs_T, phase);
+        xs_enqueue(sm, xr_v, xs_T, 9, nf, xr_seg, xr_bseg, xr_sums, xr_scr);
+        hipLaunchKernelGGL((k_xr_plane<ORDER, DIV>), dim3((nf + 63) / 64), dim3(64), 0, sm, st, xr_seg, xr_sums, nf,
+                           final_coef, phase);
+        ctx->prof_end(rec);
     } else {
 #ifndef PITT_AB_VARIANTS
         rec = ctx->prof_begin("k_refine", 0.0);
         acct_recs[kAcRefine] = rec;
-        hipLaunchKernelGGL((k_refine<ORDER, DIV, 1>), dim3(nf), dim3(64 * 3), 0, sm, fr->x, fr->y, fr->z, meta, st,
+        hipLaunchKernelGGL((k_refine<ORDER, DIV, 1>), dim3(nf), dim3(64 * 3), 0, sm, fx, fy, fz, meta, st,
                            best_coef, thf, tile_counts, hstride, tiles_max, final_coef, acct,
-                           (unsigned long long*)nullptr, 2, (const int32_t*)nullptr);
+                           (unsigned long long*)nullptr, 2, (const int32_t*)nullptr, phase);
         ctx->prof_end(rec);
 #else
         const int P = ctx->refine_producers;
@@ -2434,36 +2625,36 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         if (ctx->xrefine) {  // binade runs; k_refine's chain only for frames it hands back
             rec = ctx->prof_begin("k_xrefine", 0.0);
             acct_recs[kAcRefine] = rec;
-            hipLaunchKernelGGL((k_xrefine<ORDER, DIV>), dim3(nf), dim3(64 * kXW), 0, sm, fr->x, fr->y, fr->z, meta, st,
+            hipLaunchKernelGGL((k_xrefine<ORDER, DIV>), dim3(nf), dim3(64 * kXW), 0, sm, fx, fy, fz, meta, st,
                                best_coef, thf, tile_counts, hstride, tiles_max, final_coef, xfallback,
                                counters + nchunks + 1, acct, ctx->xrefine == 2 ? 1 : 0, rdbg);
             ctx->prof_end(rec);
             rec = ctx->prof_begin("k_refine:fallback", 0.0);
-            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fx, fy, fz, meta, st, best_coef,
                                thf, tile_counts, hstride, tiles_max, final_coef, nullptr, rdbg, ctx->refine_mode,
-                               xfallback);
+                               xfallback, phase);
             ctx->prof_end(rec);
         } else if (ctx->refine_frames > 1 && P == 1 && !rdbg) {  // F frames per block, one chain wave
             rec = ctx->prof_begin("k_refine", 0.0);
             acct_recs[kAcRefine] = rec;
             const int F = ctx->refine_frames == 3 && kRefineMulti3 ? 3 : 2;
             auto mk = refine_multi_kernel<ORDER, DIV>(F);
-            hipLaunchKernelGGL(mk, dim3((nf + F - 1) / F), dim3(64 * (F + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st,
+            hipLaunchKernelGGL(mk, dim3((nf + F - 1) / F), dim3(64 * (F + 2)), 0, sm, fx, fy, fz, meta, st,
                                best_coef, thf, tile_counts, hstride, tiles_max, nf, final_coef, acct, ctx->refine_mode);
             ctx->prof_end(rec);
         } else {
             rec = ctx->prof_begin("k_refine", 0.0);
             acct_recs[kAcRefine] = rec;
-            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fr->x, fr->y, fr->z, meta, st, best_coef,
+            hipLaunchKernelGGL(kern, dim3(nf), dim3(64 * (P + 2)), 0, sm, fx, fy, fz, meta, st, best_coef,
                                thf, tile_counts, hstride, tiles_max, final_coef, acct, rdbg, ctx->refine_mode,
-                               nullptr);
+                               nullptr, phase);
             ctx->prof_end(rec);
         }
 #endif
     }
     rec = ctx->prof_begin("k_sel_mark", 0.0);
     acct_recs[kAcSelMark] = rec;
-    hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fr->x, fr->y, fr->z, meta, st,
+    hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st,
                        final_coef, thf, nf, tiles_max, tile_box, group_box, sel_bits, sel_cnt, acct_tiles);
     ctx->prof_end(rec);
     rec = ctx->prof_begin("k_sel_write", 0.0);
@@ -2484,10 +2675,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     return PITT_OK;
     };
-    // Graphs only for the pipelined batch layouts (enough frames that the enqueue cost matters).  A
-    // replayed one-frame graph interleaved with the primitive services' direct launches on the same
-    // stream faulted (tests/test_classify_gpu.py under pytest, not reproduced in isolation; DESIGN.md
-    // s6), so service-sized batches always launch directly.
+    auto enqueue_front = [&]() -> int { return enqueue(0, K, 1, true, acct_recs, score_recs); };
+    // Graphs from ctx->graph_min_frames frames up (1 by default; DESIGN.md s3d: the round-3 fault was a
+    // stale pinned address, fixed by the arena generation in the key).
     if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
         const double log_prob_k = std::log(1.0 - p->probability);
         uint64_t thb = 0, lpb = 0;
@@ -2499,7 +2689,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
                                      (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score * 2 + (uint64_t)ctx->inside_cull, (uint64_t)(ORDER * 2 + DIV),
                                      (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
-                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames};
+                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K};
         pitt_ctx::GraphEntry* hit = nullptr;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
@@ -2513,7 +2703,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
             } else {
                 hipGraph_t graph = nullptr;
                 PITT_HIP_TRY(hipStreamBeginCapture(sm, hipStreamCaptureModeRelaxed));
-                const int erc = enqueue();
+                const int erc = enqueue_front();
                 const hipError_t ce = hipStreamEndCapture(sm, &graph);
                 if (erc) {
                     if (graph) (void)hipGraphDestroy(graph);
@@ -2542,13 +2732,21 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
             PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
             ++ctx->graph_replays;
         } else {
-            const int erc = enqueue();
+            const int erc = enqueue_front();
             if (erc) return erc;
         }
     } else {
-        const int erc = enqueue();
+        const int erc = enqueue_front();
         if (erc) return erc;
     }
+    // the continuation, should a frame still be running after the K chunks (finish_batch)
+    ctx->inflight_k = K;
+    ctx->inflight_hint_key = hint_key;
+    ctx->inflight_cont = nullptr;
+    if (K < nchunks)
+        ctx->inflight_cont = [enqueue, K, nchunks](std::vector<int>& ar, std::vector<int>& sr) -> int {
+            return enqueue(K, nchunks, 2, false, ar, sr);
+        };
     // completion (pitt_wait): copy results out, price the score launches
     ctx->inflight = true;
     ctx->inflight_results = results;
@@ -2574,6 +2772,25 @@ int finish_batch(pitt_ctx* ctx) {
     if (!ctx->inflight) return PITT_OK;
     ctx->inflight = false;
     PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const ChunkStat* cs = (const ChunkStat*)ctx->inflight_hstat;
+    const int nchunks = (int)ctx->inflight_chunks.size();
+    if (ctx->inflight_cont && cs[ctx->inflight_k].tiles > 0) {
+        // frames still running after the scheduled chunks: the rest of the chunks, then their frames'
+        // decisions, refinements and the selection (direct launches; rare once the hint has learnt)
+        std::function<int(std::vector<int>&, std::vector<int>&)> cont = std::move(ctx->inflight_cont);
+        ctx->inflight_cont = nullptr;
+        const int rc = cont(ctx->inflight_acct_recs, ctx->inflight_score_recs);
+        if (rc) return rc;
+        PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ++ctx->continuations;
+    }
+    ctx->inflight_cont = nullptr;
+    {  // chunks with active frames: the schedule the next batches of this layout launch
+        int need = 1;
+        for (int c = 1; c < nchunks; ++c)
+            if (cs[c].tiles > 0) need = c + 1;  // (a listed frame adds its tiles)
+        ctx->chunk_hint_update(ctx->inflight_hint_key, need);
+    }
     std::memcpy(ctx->inflight_results, ctx->inflight_hres, (size_t)ctx->inflight_frames * sizeof(pitt_plane_result));
     if (ctx->inflight_xfb) {
         ++ctx->xrefine_batches;

@@ -245,6 +245,13 @@ int pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays) {
     return PITT_OK;
 }
 
+int pitt_schedule_stats(pitt_ctx* ctx, int64_t* continuations, int32_t* last_chunks) {
+    if (!ctx) return PITT_E_INVALID;
+    if (continuations) *continuations = ctx->continuations;
+    if (last_chunks) *last_chunks = ctx->inflight_k;
+    return PITT_OK;
+}
+
 int pitt_refine_stats(pitt_ctx* ctx, int64_t* batches, int64_t* fallback_frames) {
     if (!ctx) return PITT_E_INVALID;
     if (batches) *batches = ctx->xrefine_batches;

@@ -1,0 +1,97 @@
+"""The adaptive chunk schedule ("Chunk schedule").
+
+A batch launches the scoring chunks its layout's last batches needed -- two of seven for table scenes,
+whose frames finish at T = 15..54 -- instead of the whole 32/64/128/256... schedule.  A frame still
+running after them (a clutter scene in the same buffers, T = 1001) is finished by a continuation: the
+rest of the chunks, then the decisions, refinements and selection of the frames it finished.  Results
+are the oracle's either way; these tests force the continuation and compare bit for bit with a context
+that always launches every chunk ($PITT_ADAPTIVE_CHUNKS=0)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import pitt_object_table_segmentation_amd as pitt
+import test_plane_gpu as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return pitt.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _lists(b, res, inl):
+    h = inl.cpu().numpy()
+    return [h[o:o + r["n_inliers"]].copy() for o, r in zip(b.offsets, res)]
+
+
+@pytest.mark.parametrize("graphs", [1, 0])
+def test_continuation_after_a_learnt_short_schedule(graphs):
+    w, h = 320, 240
+    table = [pitt.synth_frame(pitt.SCENE_TABLE, 8000 + i, w, h) for i in range(6)]
+    mixed = [pitt.synth_frame(pitt.SCENE_CLUTTER if i % 2 else pitt.SCENE_TABLE_NAN, 8100 + i, w, h) for i in range(6)]
+    b = pitt.FrameBatch.from_host(table, device="cuda:0")
+    bm = pitt.FrameBatch.from_host(mixed, device="cuda:0")
+    assert b.capacity == bm.capacity and list(b.offsets) == list(bm.offsets)
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+    ctx = _ctx(PITT_GRAPHS=graphs)
+    full = _ctx(PITT_ADAPTIVE_CHUNKS=0)
+    try:
+        for _ in range(3):  # the table layout: the hint learns the short schedule
+            res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+        cont0, k_table = ctx.schedule_stats()
+        assert k_table < 7, k_table
+        P._check(ctx, table, res, _lists(b, res, inl))
+        # the same buffers now hold clutter frames (T = 1001): the short schedule cannot finish them
+        for a, c in zip((b.x, b.y, b.z), (bm.x, bm.y, bm.z)):
+            a.copy_(c)
+        torch.cuda.synchronize()
+        res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+        got = _lists(b, res, inl)
+        cont1, _ = ctx.schedule_stats()
+        assert cont1 == cont0 + 1, (cont0, cont1)
+        inl_f = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+        ref = full.plane_segment_batch(b, pitt.sac_params(), inl_f)
+        assert full.schedule_stats() == (0, 7)
+        assert res.tobytes() == ref.tobytes()
+        assert all(np.array_equal(x, y) for x, y in zip(got, _lists(b, ref, inl_f)))
+        P._check(ctx, mixed, res, got)
+        # learnt: the next batch of the layout schedules every chunk, no continuation
+        res2 = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+        assert ctx.schedule_stats() == (cont1, 7) and res2.tobytes() == ref.tobytes()
+    finally:
+        ctx.close()
+        full.close()
+
+
+def test_profiled_short_schedule_has_no_empty_launches():
+    """With the schedule learnt, a table batch launches only scoring chunks that have active frames:
+    the profiler sees no empty k_score launch (they were 5 of 7 per batch)."""
+    frames = [pitt.synth_frame(pitt.SCENE_TABLE, 8200 + i, 640, 480) for i in range(8)]
+    b = pitt.FrameBatch.from_host(frames, device="cuda:0")
+    inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+    ctx = _ctx()
+    try:
+        for _ in range(2):
+            ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+        ctx.profile(True)
+        ctx.profile_reset()
+        res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
+        n_empty, _, _ = ctx.profile_get("k_score:empty")
+        n, _, _ = ctx.profile_get("k_score")
+        ctx.profile(False)
+        assert n_empty == 0 and 1 <= n < 7, (n, n_empty)
+        P._check(ctx, frames, res, _lists(b, res, inl))
+    finally:
+        ctx.close()

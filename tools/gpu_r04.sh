@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU pass: the whole -m gpu suite, the classification + graph tests with the graph floor at one
-# frame, then the default bench line.  Every step under its own time limit; the chain stops at the first
+# Round-4 GPU pass: the whole -m gpu suite (graphs from one frame up, the default since round 4), then the
+# default bench line.  Every step under its own time limit; the chain stops at the first
 # failure.
 #   bash tools/gpu_r04.sh <tag>
 set -o pipefail
@@ -10,9 +10,5 @@ mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
     > $OUT/${TAG}_pytest_gpu.log 2>&1 || { tail -30 $OUT/${TAG}_pytest_gpu.log; exit 1; }
 tail -3 $OUT/${TAG}_pytest_gpu.log
-PITT_GRAPH_MIN_FRAMES=1 timeout -k 10 400 python -u -m pytest tests/test_classify_gpu.py tests/test_graphs_gpu.py \
-    tests/test_services_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-    > $OUT/${TAG}_pytest_floor1.log 2>&1 || { tail -30 $OUT/${TAG}_pytest_floor1.log; exit 1; }
-tail -3 $OUT/${TAG}_pytest_floor1.log
 timeout -k 10 400 python -u bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.log || { tail -30 $OUT/${TAG}_bench.log; exit 1; }
 cat $OUT/${TAG}_bench.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'])"
