@@ -24,6 +24,7 @@
 
 #include "compact.hpp"
 #include "ctx.hpp"
+#include "xsum.hpp"
 
 #pragma clang fp contract(off)
 
@@ -456,6 +457,22 @@ __global__ __launch_bounds__(256) void k_sums(const int64_t* __restrict__ coff, 
 
 static inline int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
 
+// Large member sets: the same float sums by the block-parallel exact walk (xsum.hpp).  The members'
+// x, y, z are laid out as three streams with one 256-aligned segment per cluster (zeros past a
+// cluster's end, which the walk never adds).
+__global__ __launch_bounds__(256) void k_pad_members(const float* __restrict__ mxyz, int64_t M,
+                                                     const int64_t* __restrict__ coff, const XsSeg* __restrict__ seg,
+                                                     const int32_t* __restrict__ bseg, float* __restrict__ V, int64_t T) {
+    const int64_t b = blockIdx.x;
+    const int k = bseg[b];
+    const XsSeg g = seg[k];
+    const int64_t i = (b - g.blk0) * kXsBlk + threadIdx.x;
+    const bool in = i < g.len;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) V[s * T + b * kXsBlk + threadIdx.x] = in ? mxyz[s * M + coff[k] + i] : 0.0f;
+}
+constexpr int64_t kXsMinMembers = 16384;  // below: k_sums' three chains are short enough
+
 template <class Pred, class Act>
 static int compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total) {
     const int64_t nt = ctiles(n);
@@ -622,7 +639,32 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
         hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(Mp / kSortTile)), dim3(1024), 0, s, SK, Mp, kSortTile, k);
     }
     hipLaunchKernelGGL(k_members, dim3(ew(M)), dim3(256), 0, s, SK, M, X, Y, Z, MIDX, MXYZ, MXYZ + M, MXYZ + 2 * M);
-    hipLaunchKernelGGL(k_sums, dim3((unsigned)K), dim3(256), 0, s, COFF, (int32_t)K, MXYZ, MXYZ + M, MXYZ + 2 * M, SUMS);
+    if (M >= kXsMinMembers && K > 0) {  // the exact walk over the chip
+        std::vector<XsSeg> hseg((size_t)K);
+        int64_t nb = 0;
+        for (int64_t t = 0; t < K; ++t) {
+            hseg[(size_t)t] = XsSeg{nb, coff[(size_t)t + 1] - coff[(size_t)t]};
+            nb += (hseg[(size_t)t].len + kXsBlk - 1) / kXsBlk;
+        }
+        const int64_t T = std::max<int64_t>(nb, 1) * kXsBlk;
+        float* XV = (float*)ctx->buf("cl_xs_v", (size_t)3 * T * 4);
+        XsSeg* XSEG = (XsSeg*)ctx->buf("cl_xs_seg", (size_t)K * sizeof(XsSeg));
+        int32_t* XB = (int32_t*)ctx->buf("cl_xs_bseg", (size_t)std::max<int64_t>(nb, 1) * 4);
+        char* hp = (char*)ctx->pinned("cl_xs_h", (size_t)K * sizeof(XsSeg) + (size_t)nb * 4);
+        XsScratch scr;
+        if (!XV || !XSEG || !XB || !hp) return ctx->fail(PITT_E_NOMEM, "cluster sums scratch");
+        if (int e = xs_scratch(ctx, T / kXsBlk, 3, "cl", &scr)) return e;
+        std::memcpy(hp, hseg.data(), (size_t)K * sizeof(XsSeg));
+        int32_t* hb = (int32_t*)(hp + (size_t)K * sizeof(XsSeg));
+        for (int64_t t = 0; t < K; ++t)
+            for (int64_t j = 0; j < (hseg[(size_t)t].len + kXsBlk - 1) / kXsBlk; ++j) hb[hseg[(size_t)t].blk0 + j] = (int32_t)t;
+        PITT_HIP_TRY(hipMemcpyAsync(XSEG, hp, (size_t)K * sizeof(XsSeg), hipMemcpyHostToDevice, s));
+        if (nb) PITT_HIP_TRY(hipMemcpyAsync(XB, hb, (size_t)nb * 4, hipMemcpyHostToDevice, s));
+        if (nb) hipLaunchKernelGGL(k_pad_members, dim3((unsigned)nb), dim3(kXsBlk), 0, s, MXYZ, M, COFF, XSEG, XB, XV, T);
+        xs_enqueue(s, XV, T, 3, (int)K, XSEG, XB, SUMS, scr);
+    } else {
+        hipLaunchKernelGGL(k_sums, dim3((unsigned)K), dim3(256), 0, s, COFF, (int32_t)K, MXYZ, MXYZ + M, MXYZ + 2 * M, SUMS);
+    }
     PITT_HIP_TRY(hipGetLastError());
     float* sums = (float*)ctx->pinned("cl_sums_h", (size_t)K * 12);
     PITT_HIP_TRY(hipMemcpyAsync(sums, SUMS, (size_t)K * 12, hipMemcpyDeviceToHost, s));
