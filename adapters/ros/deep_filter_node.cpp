@@ -13,21 +13,7 @@
 namespace {
 double g_leaf = 0.0;
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    void* get(size_t b) {
-        if (b > bytes) {
-            if (p) (void)hipFree(p);
-            p = nullptr;
-            bytes = 0;
-            if (hipMalloc(&p, b) != hipSuccess) return nullptr;
-            bytes = b;
-        }
-        return p;
-    }
-};
-DevBuf g_payload, g_planes, g_out;
+pitt_ros::DevBuf g_payload, g_planes, g_out;
 
 bool copy_ok(hipError_t e) {
     if (e != hipSuccess) ROS_ERROR_STREAM("deep filter: HIP copy failed: " << hipGetErrorString(e));

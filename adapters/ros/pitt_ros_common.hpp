@@ -13,6 +13,7 @@
 //   * forwarding of the node's /pitt/srv/... ROS parameters to the service object with their XmlRpc
 //     type, so the mirror applies roscpp's typed-read rules exactly as NodeHandle::param would.
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <ros/ros.h>
 #include <sensor_msgs/PointCloud2.h>
 #include <sensor_msgs/PointField.h>
@@ -37,6 +38,22 @@ inline Node& node() {
     static Node n;
     return n;
 }
+
+// A grow-only device buffer (the nodes' per-message staging: payload, SoA planes).
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void* get(size_t b) {
+        if (b > bytes) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+            if (hipMalloc(&p, b) != hipSuccess) return nullptr;
+            bytes = b;
+        }
+        return p;
+    }
+};
 
 // pitt_create on device 0 (or $PITT_DEVICE) and the service object; throws when no gfx950 device.
 inline void init_node() {

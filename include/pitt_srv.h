@@ -8,6 +8,7 @@
  *   pitt_srv_find_supports    <-> findSupports          supports_segmentation_srv.cpp:241
  *   pitt_srv_clusterize       <-> clusterize            cluster_segmentation_srv.cpp:38
  *   pitt_srv_segment_objects  <-> depthAcquisition's support->cluster portion, obj_segmentation.cpp:261-312
+ *   pitt_srv_segment_objects_dev <-> the same with the world cloud in HBM (adapters/ros/obj_segmentation_node.cpp)
  *   pitt_srv_ransac_sphere    <-> ransacSphereDetection sphere_segmentation_srv.cpp:29
  *   pitt_srv_ransac_cylinder  <-> ransacCylinderDetaction cylinder_segmentation_srv.cpp:82
  *   pitt_srv_ransac_cone      <-> ransacConeDetaction     cone_segmentation_srv.cpp:83
@@ -117,6 +118,19 @@ int pitt_srv_segment_objects(pitt_srv* srv, const float* xyz16, int64_t n, int64
 int pitt_srv_output_size(pitt_srv* srv, int32_t o, int32_t* n_clusters);
 int pitt_srv_output_cluster(pitt_srv* srv, int32_t o, int32_t c, int32_t* inliers, int64_t* size,
                             float centroid[3]);
+
+/* depthAcquisition's support -> cluster portion (obj_segmentation.cpp:261-312) with the world cloud in HBM:
+ * x/y/z device SoA (the output of pitt_transform_cloud).  The support request is built from the
+ * parameter server as callSupportFilter builds it (:164-177, -1 when a parameter is unset) and resolved
+ * as findSupports resolves it (supports_segmentation_srv.cpp:70-86); the cluster parameters are read
+ * as clusterize reads them (cluster_segmentation_srv.cpp:44-50, Q6); then pitt_segment_objects_dev.
+ * The normals callSupportFilter sends are not needed: the support service's SACMODEL_PLANE never reads
+ * them, and the node's normals always match the cloud's size (A1).  Returns the pitt status; *out is
+ * valid until the next call on the context. */
+int pitt_srv_segment_objects_dev(pitt_srv* srv, const float* x, const float* y, const float* z, int64_t n,
+                                 pitt_scene* out);
+/* The two parameter sets pitt_srv_segment_objects_dev would use now (either pointer may be NULL). */
+int pitt_srv_resolved_params(pitt_srv* srv, pitt_support_params* sp, pitt_cluster_params* cp);
 
 #ifdef __cplusplus
 }

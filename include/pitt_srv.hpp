@@ -255,8 +255,20 @@ public:
     // then clusters per support; one ClustersOutput per support with at least one cluster.
     std::vector<pitt_msgs::ClustersOutput> segmentObjects(const pitt_msgs::PointCloud& world_cloud,
                                                           const pitt_msgs::NormalCloud& normals);
+    // callSupportFilter's request (obj_segmentation.cpp:147-177: each field from its parameter, -1 when
+    // unset) as findSupports resolves it (initializeInputParameters, supports_segmentation_srv.cpp:70-86)
+    pitt_support_params supportParams();
+    // the parameters clusterize reads per call (cluster_segmentation_srv.cpp:44-50, Q6)
+    pitt_cluster_params clusterParams();
+    // segmentObjects with the world cloud in HBM (device SoA x/y/z): pitt_segment_objects_dev with the
+    // two parameter sets above; the scene stays valid until the next call on the context.  Returns the
+    // pitt status.
+    int segmentObjectsDev(const float* x, const float* y, const float* z, int64_t n, pitt_scene* out);
 
 private:
+    static pitt_support_params resolveSupport(const pitt_msgs::SupportSegmentation::Request& req);
+    pitt_msgs::SupportSegmentation::Request supportRequest();
+
     pitt_ctx* ctx_;
     ParamServer params_;
     int status_ = PITT_OK;

@@ -319,6 +319,8 @@ SIGNATURES.update({
     "pitt_srv_output_size": (_i32, [_vp, _i32, _i32p]),
     "pitt_srv_output_cluster": (_i32, [_vp, _i32, _i32, _i32p, _i64p, _f32p]),
     "pitt_srv_classify_clusters": (_i32, [_vp, _vp, _vp, _vp, _i64p, _i64p, _i32, ctypes.POINTER(ClusterShape)]),
+    "pitt_srv_segment_objects_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(Scene)]),
+    "pitt_srv_resolved_params": (_i32, [_vp, ctypes.POINTER(SupportParams), ctypes.POINTER(ClusterParams)]),
 })
 
 

@@ -807,6 +807,38 @@ class Services:
             out.append(dict(inliers=idx[:size.value].copy(), centroid=ce, cloud=cl[:size.value, :3].copy()))
         return ok, out
 
+    def resolved_params(self):
+        """(SupportParams, ClusterParams) that segment_objects_dev would use with the current parameters."""
+        sp, cp = L.SupportParams(), L.ClusterParams()
+        self._rc(lib.pitt_srv_resolved_params(self.h, ctypes.byref(sp), ctypes.byref(cp)), "resolved_params")
+        return sp, cp
+
+    def segment_objects_dev(self, x, y, z):
+        """pitt_srv_segment_objects_dev: segment_objects with the world cloud in HBM (device tensors), the
+        parameters from the parameter server.  Returns one list per support with at least one cluster, of
+        dicts (inliers = on-support indices, centroid = sum / (size + 1)), as segment_objects."""
+        out = L.Scene()
+        rc = lib.pitt_srv_segment_objects_dev(self.h, x.data_ptr(), y.data_ptr(), z.data_ptr(), x.numel(),
+                                              ctypes.byref(out))
+        self._rc(rc, "segment_objects_dev")
+        total = max([out.objects[i].offset + out.objects[i].size for i in range(out.n_objects)], default=0)
+        idx = np.empty(max(total, 1), np.int32)
+        if total:
+            self.ctx._check(lib.pitt_memcpy(self.ctx.h, _ip(idx), ctypes.c_void_p(out.indices), total * 4),
+                            "pitt_memcpy")
+        outs = []
+        for s in range(out.supports.n_supports):
+            objs = []
+            for i in range(out.n_objects):
+                o = out.objects[i]
+                if o.support == s:
+                    sums = np.array(list(o.sum_xyz), np.float32)
+                    objs.append(dict(inliers=idx[o.offset:o.offset + o.size].copy(),
+                                     centroid=sums / np.float32(o.size + 1)))
+            if objs:
+                outs.append(objs)
+        return outs
+
     def segment_objects(self, cloud: np.ndarray, n_normals: Optional[int] = None):
         c = _cloud16(cloud)
         n = c.shape[0]

@@ -306,37 +306,38 @@ bool SegmentationServices::ransacSphereDetection(pitt_msgs::PrimitiveSegmentatio
     return true;
 }
 
+// initializeInputParameters, supports_segmentation_srv.cpp:70-86: a request field < 0 (or a vector
+// that is not 3 long) selects the service default.
+pitt_support_params SegmentationServices::resolveSupport(const pitt_msgs::SupportSegmentation::Request& req) {
+    static const float kAxis[3] = {0.0f, 0.0f, -1.0f};
+    static const float kOffset[3] = {0.02f, 0.02f, 0.005f};
+    pitt_support_params sp;
+    pitt_support_params_default(&sp);
+    sp.min_iterative_cloud_percentage = srvm::getServiceFloatParameter(req.min_iterative_cloud_percentual_size, 0.030f);
+    sp.min_iterative_plane_percentage = srvm::getServiceFloatParameter(req.min_iterative_plane_percentual_size, 0.030f);
+    sp.horizontal_variance_threshold = srvm::getServiceFloatParameter(req.variance_threshold_for_horizontal, 0.09f);
+    sp.ransac_distance_threshold = srvm::getServiceFloatParameter(req.ransac_distance_point_in_shape_threshold, 0.02f);
+    sp.ransac_max_iterations = srvm::getServiceIntParameter(req.ransac_max_iteration_threshold, 10);
+    const std::vector<float> axis = srvm::getService3DArrayParameter(req.horizontal_axis, kAxis);
+    const std::vector<float> off = srvm::getService3DArrayParameter(req.support_edge_remove_offset, kOffset);
+    for (int i = 0; i < 3; ++i) {
+        sp.horizontal_axis[i] = axis[(size_t)i];
+        sp.edge_remove_offset[i] = off[(size_t)i];
+    }
+    return sp;
+}
+
 // supports_segmentation_srv.cpp:241-361 (+ initializeInputParameters :70-86)
 bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request& req,
                                         pitt_msgs::SupportSegmentation::Response& res) {
-    static const float kAxis[3] = {0.0f, 0.0f, -1.0f};
-    static const float kOffset[3] = {0.02f, 0.02f, 0.005f};
-    const float minCloud = srvm::getServiceFloatParameter(req.min_iterative_cloud_percentual_size, 0.030f);
-    const float minPlane = srvm::getServiceFloatParameter(req.min_iterative_plane_percentual_size, 0.030f);
-    const float maxVar = srvm::getServiceFloatParameter(req.variance_threshold_for_horizontal, 0.09f);
-    const float minVar = -1 * maxVar;
-    const float th = srvm::getServiceFloatParameter(req.ransac_distance_point_in_shape_threshold, 0.02f);
+    const pitt_support_params sp = resolveSupport(req);
     const float ndw = srvm::getServiceFloatParameter(req.ransac_model_normal_distance_weigth, 0.9f);
-    const int maxIt = srvm::getServiceIntParameter(req.ransac_max_iteration_threshold, 10);
-    const std::vector<float> axis = srvm::getService3DArrayParameter(req.horizontal_axis, kAxis);
-    const std::vector<float> off = srvm::getService3DArrayParameter(req.support_edge_remove_offset, kOffset);
 
     res.supports_description.clear();
     status_ = PITT_OK;
     // The first RANSAC call runs with the request's normals: a size mismatch fails it (A1) and the
     // loop exits before any support is found.  Later rounds re-estimate normals of matching size.
     if (req.input_norm.size() == req.input_cloud.size()) {
-        pitt_support_params sp;
-        pitt_support_params_default(&sp);
-        sp.min_iterative_cloud_percentage = minCloud;
-        sp.min_iterative_plane_percentage = minPlane;
-        sp.horizontal_variance_threshold = maxVar;
-        sp.ransac_distance_threshold = th;
-        sp.ransac_max_iterations = maxIt;
-        for (int i = 0; i < 3; ++i) {
-            sp.horizontal_axis[i] = axis[(size_t)i];
-            sp.edge_remove_offset[i] = off[(size_t)i];
-        }
         std::vector<float> x, y, z;
         to_soa(req.input_cloud, x, y, z);
         pitt_support_list L;
@@ -360,37 +361,32 @@ bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request&
             }
         }
     }
-    res.used_min_iterative_cloud_percentual_size = minCloud;
-    res.used_min_iterative_plane_percentual_size = minPlane;
-    res.used_max_variance_threshold_for_horizontal = maxVar;
-    res.used_min_variance_threshold_for_horizontal = minVar;
-    res.used_ransac_max_iteration_threshold = maxIt;
-    res.used_ransac_distance_point_in_shape_threshold = th;
+    res.used_min_iterative_cloud_percentual_size = sp.min_iterative_cloud_percentage;
+    res.used_min_iterative_plane_percentual_size = sp.min_iterative_plane_percentage;
+    res.used_max_variance_threshold_for_horizontal = sp.horizontal_variance_threshold;
+    res.used_min_variance_threshold_for_horizontal = -1 * sp.horizontal_variance_threshold;
+    res.used_ransac_max_iteration_threshold = sp.ransac_max_iterations;
+    res.used_ransac_distance_point_in_shape_threshold = sp.ransac_distance_threshold;
     res.used_ransac_model_normal_distance_weigth = ndw;
-    res.used_horizontal_axis = axis;
-    res.used_support_edge_remove_offset = off;
+    res.used_horizontal_axis.assign(sp.horizontal_axis, sp.horizontal_axis + 3);
+    res.used_support_edge_remove_offset.assign(sp.edge_remove_offset, sp.edge_remove_offset + 3);
     return true;
 }
 
 // cluster_segmentation_srv.cpp:38-108
 bool SegmentationServices::clusterize(pitt_msgs::ClusterSegmentation::Request& req,
                                       pitt_msgs::ClusterSegmentation::Response& res) {
-    double tolerance, minClusterSizeRate, maxClusterSizeRate;
-    int minInputSize;
-    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, tolerance, 0.03);
-    params_.param(srvm::PARAM_NAME_CLUSTER_MIN_RATE, minClusterSizeRate, 0.01);
-    params_.param(srvm::PARAM_NAME_CLUSTER_MAX_RATE, maxClusterSizeRate, 0.99);
-    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, minInputSize, 30);  // Q6: the tolerance name
+    const pitt_cluster_params cp = clusterParams();
     res.cluster_objs.clear();
     status_ = PITT_OK;
     const size_t n = req.cloud.size();
-    if (n >= (size_t)(int64_t)minInputSize) {
-        const int mn = (int)std::round((double)n * minClusterSizeRate);
-        const int mx = (int)std::round((double)n * maxClusterSizeRate);
+    if (n >= (size_t)(int64_t)cp.min_input_size) {
+        const int mn = (int)std::round((double)n * cp.min_rate);
+        const int mx = (int)std::round((double)n * cp.max_rate);
         std::vector<float> x, y, z;
         to_soa(req.cloud, x, y, z);
         pitt_cluster_list L;
-        status_ = pitt_euclidean_clusters(ctx_, x.data(), y.data(), z.data(), (int64_t)n, tolerance, mn, mx, &L);
+        status_ = pitt_euclidean_clusters(ctx_, x.data(), y.data(), z.data(), (int64_t)n, cp.tolerance, mn, mx, &L);
         if (status_ == PITT_OK) {
             for (int c = 0; c < L.n_clusters; ++c) {
                 const pitt_cluster& cl = L.clusters[c];
@@ -456,12 +452,9 @@ int SegmentationServices::arbitratePrimitive(size_t sphereInl, size_t cylinderIn
     return TXT_UNKNOWN_SHAPE_TAG;
 }
 
-// obj_segmentation.cpp:143-207 (callSupportFilter) and :261-312 (support -> cluster glue)
-std::vector<pitt_msgs::ClustersOutput> SegmentationServices::segmentObjects(const pitt_msgs::PointCloud& world_cloud,
-                                                                            const pitt_msgs::NormalCloud& normals) {
+// callSupportFilter's request fields, obj_segmentation.cpp:164-177 (-1 / {-1} when a parameter is unset)
+pitt_msgs::SupportSegmentation::Request SegmentationServices::supportRequest() {
     pitt_msgs::SupportSegmentation srv;
-    srv.request.input_cloud = world_cloud;
-    srv.request.input_norm = normals;
     params_.param(srvm::PARAM_NAME_MIN_ITERATIVE_CLOUD_PERCENTAGE, srv.request.min_iterative_cloud_percentual_size,
                   srvm::DEFAULT_SERVICE_PARAMETER_REQUEST_F);
     params_.param(srvm::PARAM_NAME_MIN_ITERATIVE_SUPPORT_PERCENTAGE, srv.request.min_iterative_plane_percentual_size,
@@ -477,6 +470,38 @@ std::vector<pitt_msgs::ClustersOutput> SegmentationServices::segmentObjects(cons
     params_.param(srvm::PARAM_NAME_HORIZONTAL_AXIS, srv.request.horizontal_axis, std::vector<float>(1, -1.0f));
     params_.param(srvm::PARAM_NAME_SUPPORT_EDGE_REMOVE_OFFSET, srv.request.support_edge_remove_offset,
                   std::vector<float>(1, -1.0f));
+    return srv.request;
+}
+
+pitt_support_params SegmentationServices::supportParams() { return resolveSupport(supportRequest()); }
+
+pitt_cluster_params SegmentationServices::clusterParams() {
+    pitt_cluster_params cp;
+    pitt_cluster_params_default(&cp);
+    int minInputSize = 30;
+    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, cp.tolerance, 0.03);
+    params_.param(srvm::PARAM_NAME_CLUSTER_MIN_RATE, cp.min_rate, 0.01);
+    params_.param(srvm::PARAM_NAME_CLUSTER_MAX_RATE, cp.max_rate, 0.99);
+    params_.param(srvm::PARAM_NAME_CLUSTER_TOLERANCE, minInputSize, 30);  // Q6: the tolerance name
+    cp.min_input_size = minInputSize;
+    return cp;
+}
+
+int SegmentationServices::segmentObjectsDev(const float* x, const float* y, const float* z, int64_t n,
+                                            pitt_scene* out) {
+    const pitt_support_params sp = supportParams();
+    const pitt_cluster_params cp = clusterParams();
+    status_ = pitt_segment_objects_dev(ctx_, x, y, z, n, &sp, &cp, out);
+    return status_;
+}
+
+// obj_segmentation.cpp:143-207 (callSupportFilter) and :261-312 (support -> cluster glue)
+std::vector<pitt_msgs::ClustersOutput> SegmentationServices::segmentObjects(const pitt_msgs::PointCloud& world_cloud,
+                                                                            const pitt_msgs::NormalCloud& normals) {
+    pitt_msgs::SupportSegmentation srv;
+    srv.request = supportRequest();
+    srv.request.input_cloud = world_cloud;
+    srv.request.input_norm = normals;
     std::vector<pitt_msgs::ClustersOutput> outs;
     if (!findSupports(srv.request, srv.response)) return outs;
     for (pitt_msgs::Support& s : srv.response.supports_description) {
@@ -773,6 +798,19 @@ int pitt_srv_output_cluster(pitt_srv* s, int32_t o, int32_t c, int32_t* inliers,
         centroid[1] = m.y_centroid;
         centroid[2] = m.z_centroid;
     }
+    return PITT_OK;
+}
+
+int pitt_srv_segment_objects_dev(pitt_srv* s, const float* x, const float* y, const float* z, int64_t n,
+                                 pitt_scene* out) {
+    if (!s || !out || n < 0 || (n > 0 && (!x || !y || !z))) return PITT_E_INVALID;
+    return s->svc.segmentObjectsDev(x, y, z, n, out);
+}
+
+int pitt_srv_resolved_params(pitt_srv* s, pitt_support_params* sp, pitt_cluster_params* cp) {
+    if (!s) return PITT_E_INVALID;
+    if (sp) *sp = s->svc.supportParams();
+    if (cp) *cp = s->svc.clusterParams();
     return PITT_OK;
 }
 

@@ -1,6 +1,7 @@
-// Stand-in for <sensor_msgs/PointCloud2.h> (compile checks only).
+// Stand-in for <sensor_msgs/PointCloud2.h> (compile checks and the orchestrator harness).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <vector>
 #include "sensor_msgs/PointField.h"
 namespace sensor_msgs {
@@ -12,4 +13,5 @@ struct PointCloud2 {
     std::vector<uint8_t> data;
     bool is_dense = false;
 };
+typedef std::shared_ptr<const PointCloud2> PointCloud2ConstPtr;
 }  // namespace sensor_msgs

@@ -131,7 +131,8 @@ def test_preprocessing_entry_points_reject_null_context():
 
 def test_ros_adapters_use_only_declared_abi():
     """adapters/ros/ (compiled only where ROS and pitt_msgs exist) calls nothing but the C ABI that
-    include/*.h declares, and advertises the reference's service names (srv_manager.h:25-32)."""
+    include/*.h declares, advertises the reference's service names (srv_manager.h:25-32), and the two
+    orchestrators use the reference's topics (obj_segmentation.cpp:381,385; ransac_segmentation.cpp:352-354)."""
     import glob
     import os
     import re
@@ -141,7 +142,7 @@ def test_ros_adapters_use_only_declared_abi():
         declared |= set(re.findall(r"\b(pitt_\w+)\s*\(", open(h).read()))
     srcs = glob.glob(os.path.join(root, "adapters", "ros", "*.cpp")) + \
         glob.glob(os.path.join(root, "adapters", "ros", "*.hpp"))
-    assert len(srcs) == 8
+    assert len(srcs) == 10
     used = set()
     for s in srcs:
         used |= set(re.findall(r"\b(pitt_(?!ros\b)\w+)\s*\(", open(s).read()))
@@ -154,6 +155,12 @@ def test_ros_adapters_use_only_declared_abi():
              "cone_segmentation_node.cpp": "cone_segmentation_srv"}
     for f, name in names.items():
         assert f'advertiseService("{name}"' in open(os.path.join(root, "adapters", "ros", f)).read(), f
+    obj = open(os.path.join(root, "adapters", "ros", "obj_segmentation_node.cpp")).read()
+    assert '"obj_segmentation/ClusterOutput"' in obj and '"/camera/depth/points"' in obj
+    assert "pitt_srv_segment_objects_dev(" in obj and '"arm_filter_srv"' in obj
+    ran = open(os.path.join(root, "adapters", "ros", "ransac_segmentation_node.cpp")).read()
+    assert '"geometric_tracker/trackedCluster"' in ran and '"ransac_segmentation/trackedShapes"' in ran
+    assert "pitt_srv_classify_clusters(" in ran
 
 
 def test_primitive_arbitration():

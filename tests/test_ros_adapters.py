@@ -15,8 +15,9 @@ INC = ["-I" + STUB, "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(RO
 NODES = sorted(glob.glob(os.path.join(ROOT, "adapters", "ros", "*.cpp")))
 
 
-def test_seven_nodes_present():
-    assert len(NODES) == 7
+def test_nine_nodes_present():
+    """Seven service nodes and the two orchestrators (obj_segmentation, ransac_segmentation)."""
+    assert len(NODES) == 9
 
 
 @pytest.mark.parametrize("src", NODES, ids=[os.path.basename(n) for n in NODES])
@@ -43,3 +44,15 @@ def test_pointcloud2_layout_checks(tmp_path):
     assert got["normals_short"] == [0]
     assert got["normals_missing"] == [6, 0, 0, 0, 0, 0, 0]
     assert "rejected" in r.stderr
+
+
+def test_orchestrator_harness_links(tmp_path):
+    """The two orchestrator nodes link against libpitt_seg.so in their harness (every C-ABI symbol they
+    call is exported); running them needs the GPU (tests/test_ros_orchestrators_gpu.py)."""
+    lib = os.path.join(ROOT, "pitt_object_table_segmentation_amd", "libpitt_seg.so")
+    if not os.path.exists(lib):
+        pytest.skip("libpitt_seg.so not built")
+    p = subprocess.run(["make", "-C", STUB, "OUT=" + str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    for n in ("obj_segmentation_harness", "ransac_segmentation_harness"):
+        assert os.access(str(tmp_path / n), os.X_OK)
