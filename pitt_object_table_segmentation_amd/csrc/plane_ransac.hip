@@ -2368,6 +2368,25 @@ static auto refine_multi_kernel(int F) {
     return k_refine_multi<ORDER, DIV, 2>;
 }
 
+// Debug builds only (tools/build_variant.sh <name> -DPITT_SYNC_CHECK, with PITT_GRAPHS=0): synchronise
+// after every launch of a batch so that a faulting kernel is named on stderr.
+#ifdef PITT_SYNC_CHECK
+#define PITT_CHECK_LAUNCH(what, c, phase)                                                                    \
+    do {                                                                                                   \
+        hipStreamCaptureStatus cs_ = hipStreamCaptureStatusNone;                                           \
+        (void)hipStreamIsCapturing(sm, &cs_);                                                              \
+        if (cs_ != hipStreamCaptureStatusNone) break;                                                      \
+        const hipError_t e_ = hipStreamSynchronize(sm);                                                    \
+        std::fprintf(stderr, "PITT_SYNC_CHECK %s chunk %d phase %d: %s\n", what, c, phase,                \
+                     hipGetErrorString(e_));                                                               \
+        if (e_ != hipSuccess) return ctx->fail(PITT_E_HIP, what);                                          \
+    } while (0)
+#else
+#define PITT_CHECK_LAUNCH(what, c, phase) \
+    do {                                  \
+    } while (0)
+#endif
+
 template <int ORDER, int DIV>
 static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                            pitt_plane_result* results, int32_t* inliers_dev) {
@@ -2550,6 +2569,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fx, fy, fz, meta,
                        tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
                        counters, cstat, acct);
+    PITT_CHECK_LAUNCH("k_hypothesize", -1, phase);
     ctx->prof_end(rec);
     }
     int h0 = 0;
@@ -2578,6 +2598,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fx, fy, fz, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
                            tile_box, group_box);
+    PITT_CHECK_LAUNCH("k_score", c, phase);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
         if (c == 0) acct_recs[kAcReplay] = rec;  // every replay launch's bytes are counted in this one
@@ -2586,10 +2607,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            tiles_max, h0, H, max_iter, log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf,
                            counters + c + 1, cstat + c + 1, fx, fy, fz, tables, A, target_next, hyp_coef,
                            hyp_attempt, acct);
+    PITT_CHECK_LAUNCH("k_replay", c, phase);
         ctx->prof_end(rec);
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        optimize, best_coef, final_coef, phase);
+    PITT_CHECK_LAUNCH("k_decide", -1, phase);
     // refinement (pass 1 over refined frames), then the final selection over every frame's tiles
     if (cov_mode == PITT_COV_FAST) {  // A6 fast mode: double sums over the chip, fixed tree
         rec = ctx->prof_begin("k_cov_tiles", 0.0);
@@ -2603,12 +2626,17 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         rec = ctx->prof_begin("k_refine:xsum", 0.0);
         hipLaunchKernelGGL((k_xr_count<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
                            thf, nf, tiles_max, xr_tcnt, phase);
+    PITT_CHECK_LAUNCH("k_xr_count", -1, phase);
         hipLaunchKernelGGL(k_xr_scan, dim3(nf), dim3(256), 0, sm, meta, tiles_max, xr_tcnt, xr_seg, xr_bseg);
+    PITT_CHECK_LAUNCH("k_xr_scan", -1, phase);
         hipLaunchKernelGGL((k_xr_write<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
                            thf, nf, tiles_max, xr_tcnt, xr_seg, xr_v, xs_T, phase);
+    PITT_CHECK_LAUNCH("k_xr_write", -1, phase);
         xs_enqueue(sm, xr_v, xs_T, 9, nf, xr_seg, xr_bseg, xr_sums, xr_scr);
+    PITT_CHECK_LAUNCH("xs_enqueue", -1, phase);
         hipLaunchKernelGGL((k_xr_plane<ORDER, DIV>), dim3((nf + 63) / 64), dim3(64), 0, sm, st, xr_seg, xr_sums, nf,
                            final_coef, phase);
+    PITT_CHECK_LAUNCH("k_xr_plane", -1, phase);
         ctx->prof_end(rec);
     } else {
 #ifndef PITT_AB_VARIANTS
@@ -2617,6 +2645,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         hipLaunchKernelGGL((k_refine<ORDER, DIV, 1>), dim3(nf), dim3(64 * 3), 0, sm, fx, fy, fz, meta, st,
                            best_coef, thf, tile_counts, hstride, tiles_max, final_coef, acct,
                            (unsigned long long*)nullptr, 2, (const int32_t*)nullptr, phase);
+    PITT_CHECK_LAUNCH("k_refine", -1, phase);
         ctx->prof_end(rec);
 #else
         const int P = ctx->refine_producers;
@@ -2656,14 +2685,17 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     acct_recs[kAcSelMark] = rec;
     hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st,
                        final_coef, thf, nf, tiles_max, tile_box, group_box, sel_bits, sel_cnt, acct_tiles);
+    PITT_CHECK_LAUNCH("k_sel_mark", -1, phase);
     ctx->prof_end(rec);
     rec = ctx->prof_begin("k_sel_write", 0.0);
     acct_recs[kAcSelWrite] = rec;
     hipLaunchKernelGGL(k_sel_write, dim3(sel_blocks), dim3(kBlock), 0, sm, meta, st, nf, tiles_max, sel_bits, sel_cnt,
                        inliers_dev, n_final, acct_tiles ? acct_tiles + tile_words : nullptr);
+    PITT_CHECK_LAUNCH("k_sel_write", -1, phase);
     ctx->prof_end(rec);
     hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
                        hcap, nf, dres);
+    PITT_CHECK_LAUNCH("k_finalize", -1, phase);
     PITT_HIP_TRY(hipGetLastError());
     PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
     PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
@@ -2689,7 +2721,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
                                      (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score * 2 + (uint64_t)ctx->inside_cull, (uint64_t)(ORDER * 2 + DIV),
                                      (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
-                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K};
+                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K,
+                                     (uint64_t)(xs ? xs_T : 0)};  // the walk's stream stride and grids
         pitt_ctx::GraphEntry* hit = nullptr;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
@@ -2730,6 +2763,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         if (hit) {
             hit->last_use = ++ctx->graph_clock;
             PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
+#ifdef PITT_SYNC_CHECK
+            std::fprintf(stderr, "PITT_SYNC_CHECK graph launch nf %d K %d: %s\n", nf, K,
+                         hipGetErrorString(hipStreamSynchronize(sm)));
+#endif
             ++ctx->graph_replays;
         } else {
             const int erc = enqueue_front();
@@ -2777,6 +2814,9 @@ int finish_batch(pitt_ctx* ctx) {
     if (ctx->inflight_cont && cs[ctx->inflight_k].tiles > 0) {
         // frames still running after the scheduled chunks: the rest of the chunks, then their frames'
         // decisions, refinements and the selection (direct launches; rare once the hint has learnt)
+#ifdef PITT_SYNC_CHECK
+        std::fprintf(stderr, "PITT_SYNC_CHECK continuation after %d of %d chunks\n", ctx->inflight_k, nchunks);
+#endif
         std::function<int(std::vector<int>&, std::vector<int>&)> cont = std::move(ctx->inflight_cont);
         ctx->inflight_cont = nullptr;
         const int rc = cont(ctx->inflight_acct_recs, ctx->inflight_score_recs);
