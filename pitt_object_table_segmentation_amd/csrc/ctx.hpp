@@ -123,7 +123,7 @@ struct pitt_ctx {
     // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the
     // GPU, otherwise bounds the pipelined throughput.  $PITT_GRAPHS=0 disables.
     bool use_graphs = pitt_env_flag("PITT_GRAPHS", true);
-    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 1, 1, 1 << 30);  // smaller batches launch directly
+    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 64, 1, 1 << 30);  // smaller batches launch directly
     // Adaptive chunk schedule (plane_ransac.hip): a batch launches the scoring chunks that the last
     // batches of its layout needed; a frame still running after them is finished by a continuation.
     // Exact either way; $PITT_ADAPTIVE_CHUNKS=0 always launches the whole schedule.
@@ -173,11 +173,16 @@ struct pitt_ctx {
         std::vector<uint64_t> key;
         hipGraphExec_t exec = nullptr;
         uint64_t last_use = 0;
+        uint64_t epoch = 0;  // direct_epoch when it last ran
     };
+    // Counts the context's direct (non-graph) work: every scratch request outside the plane path, every
+    // direct plane enqueue and continuation.  A graph replays only if none happened since it last ran;
+    // otherwise it is captured afresh ("Graph replays and direct work").
+    uint64_t direct_epoch = 0;
     std::vector<GraphEntry> graphs;
     std::vector<std::vector<uint64_t>> graph_seen;  // keys launched once (captured on a repeat)
     uint64_t graph_clock = 0;
-    int64_t graph_captures = 0, graph_replays = 0;
+    int64_t graph_captures = 0, graph_replays = 0, graph_recaptures = 0;
 
     // profiling
     bool prof = false;
@@ -224,6 +229,11 @@ struct pitt_ctx {
     }
     // Waits for the work queued on the context's stream and its side streams.
     void drain();
+    // Debug builds (-DPITT_SYNC_CHECK): every arena block carries a 256 KB canary past its rounded size,
+    // and a 256 MB sentinel block catches wild writes; check_canaries names any corrupted one (a no-op
+    // in the product build).
+    void check_canaries(const char* where);
+    void* sentinel = nullptr;
     // Device scratch buffer `name` of at least `bytes` (grows, never shrinks).  A block that moves
     // is freed only after drain(), and bumps arena_gen so that no cached graph replays it.
     void* buf(const std::string& name, size_t bytes);

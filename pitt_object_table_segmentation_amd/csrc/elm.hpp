@@ -875,6 +875,9 @@ inline int launch_elm_batch(pitt_ctx* ctx, hipStream_t s, std::vector<ElmJob>& j
     PITT_HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_elm<F>, dim3((unsigned)jobs.size()), dim3(kElmThreads), 0, s, d);
     PITT_HIP_TRY(hipGetLastError());
+#ifdef PITT_SYNC_CHECK
+    ctx->check_canaries(name);
+#endif
     return PITT_OK;
 }
 

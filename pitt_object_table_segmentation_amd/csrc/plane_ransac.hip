@@ -2392,6 +2392,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            pitt_plane_result* results, int32_t* inliers_dev) {
     const int nf = fr->n_frames;
     hipStream_t sm = ctx->stream;
+    const uint64_t epoch0 = ctx->direct_epoch;  // this batch's own scratch requests are not direct work
+#ifdef PITT_SYNC_CHECK
+    ctx->check_canaries("plane batch entry");
+#endif
     // --- sizes ---
     int tiles_max = 1;
     for (int f = 0; f < nf; ++f) tiles_max = std::max<int>(tiles_max, (int)((fr->counts[f] + kTile - 1) / kTile));
@@ -2708,8 +2712,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     return PITT_OK;
     };
     auto enqueue_front = [&]() -> int { return enqueue(0, K, 1, true, acct_recs, score_recs); };
-    // Graphs from ctx->graph_min_frames frames up (1 by default; DESIGN.md s3d: the round-3 fault was a
-    // stale pinned address, fixed by the arena generation in the key).
+    ctx->direct_epoch = epoch0;
+    // Graphs from ctx->graph_min_frames frames up (64 by default), replayed only while no direct work
+    // ran on the context since the graph last ran ("Graph replays and direct work").
     if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
         const double log_prob_k = std::log(1.0 - p->probability);
         uint64_t thb = 0, lpb = 0;
@@ -2724,13 +2729,23 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K,
                                      (uint64_t)(xs ? xs_T : 0)};  // the walk's stream stride and grids
         pitt_ctx::GraphEntry* hit = nullptr;
+        bool recapture = false;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
+        if (hit && hit->epoch != ctx->direct_epoch) {
+            // direct work ran on this context since the graph last ran: capture it afresh instead of
+            // replaying (one-frame graphs replayed after the primitive services' launches faulted)
+            (void)hipGraphExecDestroy(hit->exec);
+            ctx->graphs.erase(ctx->graphs.begin() + (hit - ctx->graphs.data()));
+            hit = nullptr;
+            recapture = true;
+            ++ctx->graph_recaptures;
+        }
         if (!hit) {
             // capture on the second sight of a key (a one-off layout, e.g. a support-loop iteration,
             // launches directly: capture and instantiation cost more than one enqueue)
             auto seen = std::find(ctx->graph_seen.begin(), ctx->graph_seen.end(), key);
-            if (seen == ctx->graph_seen.end()) {
+            if (seen == ctx->graph_seen.end() && !recapture) {
                 ctx->graph_seen.push_back(key);
                 if (ctx->graph_seen.size() > 16) ctx->graph_seen.erase(ctx->graph_seen.begin());
             } else {
@@ -2762,20 +2777,42 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         }
         if (hit) {
             hit->last_use = ++ctx->graph_clock;
+            hit->epoch = ctx->direct_epoch;
             PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
 #ifdef PITT_SYNC_CHECK
-            std::fprintf(stderr, "PITT_SYNC_CHECK graph launch nf %d K %d: %s\n", nf, K,
-                         hipGetErrorString(hipStreamSynchronize(sm)));
+            {
+                const hipError_t e0 = hipStreamSynchronize(sm);
+                std::fprintf(stderr, "PITT_SYNC_CHECK graph launch nf %d K %d: %s\n", nf, K, hipGetErrorString(e0));
+                if (e0 == hipSuccess) {
+                    std::vector<int32_t> hc((size_t)nchunks + 2), hl((size_t)(nchunks + 1) * nf);
+                    (void)hipMemcpy(hc.data(), counters, hc.size() * 4, hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(hl.data(), lists, hl.size() * 4, hipMemcpyDeviceToHost);
+                    std::fprintf(stderr, "PITT_SYNC_CHECK   counters");
+                    for (int32_t v : hc) std::fprintf(stderr, " %d", v);
+                    std::fprintf(stderr, " | lists");
+                    for (size_t i = 0; i < hl.size() && i < 16; ++i) std::fprintf(stderr, " %d", hl[i]);
+                    std::fprintf(stderr, "\n");
+                    for (int c = 0; c <= nchunks; ++c)
+                        if (hc[(size_t)c] > nf) return ctx->fail(PITT_E_HIP, "sync check: stale chunk counters");
+                }
+            }
 #endif
             ++ctx->graph_replays;
         } else {
             const int erc = enqueue_front();
             if (erc) return erc;
+            ++ctx->direct_epoch;
         }
     } else {
         const int erc = enqueue_front();
         if (erc) return erc;
+        ++ctx->direct_epoch;
     }
+#ifdef PITT_SYNC_CHECK
+    std::fprintf(stderr, "PITT_SYNC_CHECK call nf %d n0 %lld K %d/%d xs %d xs_T %lld tiles_max %d gen %llu\n", nf,
+                 (long long)fr->counts[0], K, nchunks, (int)xs, (long long)xs_T, tiles_max,
+                 (unsigned long long)ctx->arena_gen);
+#endif
     // the continuation, should a frame still be running after the K chunks (finish_batch)
     ctx->inflight_k = K;
     ctx->inflight_hint_key = hint_key;
@@ -2820,6 +2857,7 @@ int finish_batch(pitt_ctx* ctx) {
         std::function<int(std::vector<int>&, std::vector<int>&)> cont = std::move(ctx->inflight_cont);
         ctx->inflight_cont = nullptr;
         const int rc = cont(ctx->inflight_acct_recs, ctx->inflight_score_recs);
+        ++ctx->direct_epoch;
         if (rc) return rc;
         PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
         ++ctx->continuations;

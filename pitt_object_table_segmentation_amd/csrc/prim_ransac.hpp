@@ -345,6 +345,13 @@ struct PrimRun final : PrimRunBase {
 // the device; a phase's synchronisation then waits for all of them.
 inline int prim_ransac_lockstep(pitt_ctx* ctx, const std::vector<PrimRunBase*>& runs,
                                 const std::vector<hipStream_t>& streams = {}) {
+#ifdef PITT_SYNC_CHECK
+    ctx->check_canaries("primitive lockstep entry");
+    struct ExitCheck {
+        pitt_ctx* c;
+        ~ExitCheck() { c->check_canaries("primitive lockstep exit"); }
+    } exit_check{ctx};
+#endif
     std::vector<hipStream_t> used;
     for (size_t i = 0; i < runs.size(); ++i) {
         hipStream_t st = i < streams.size() && streams[i] ? streams[i] : ctx->stream;

@@ -4,11 +4,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
 #include <tuple>
 #include <unordered_map>
+#include <vector>
 
 #include "ctx.hpp"
 
@@ -57,6 +59,10 @@ float float_threshold(double th) {
 }
 }  // namespace pitt
 
+#ifdef PITT_SYNC_CHECK
+static constexpr size_t kCanaryBytes = (size_t)256 << 10;
+#endif
+
 void pitt_ctx::drain() {
     if (stream) (void)hipStreamSynchronize(stream);
     for (hipStream_t sd : side)
@@ -64,6 +70,7 @@ void pitt_ctx::drain() {
 }
 
 void* pitt_ctx::buf(const std::string& name, size_t bytes) {
+    ++direct_epoch;  // scratch for direct work (the plane path restores the count for its own)
     pitt::DevBuf& b = bufs[name];
     if (b.bytes < bytes || !b.p) {
         // work queued on the context's streams may still use the old block: let it drain first
@@ -74,11 +81,18 @@ void* pitt_ctx::buf(const std::string& name, size_t bytes) {
         size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
         nb = (nb + ((size_t)1 << 21) - 1) & ~(((size_t)1 << 21) - 1);
         if (nb == 0) nb = (size_t)1 << 21;
+#ifdef PITT_SYNC_CHECK
+        if (hipMalloc(&b.p, nb + kCanaryBytes) != hipSuccess) {
+#else
         if (hipMalloc(&b.p, nb) != hipSuccess) {
+#endif
             b.p = nullptr;
             b.bytes = 0;
             return nullptr;
         }
+#ifdef PITT_SYNC_CHECK
+        (void)hipMemset((char*)b.p + nb, 0xA5, kCanaryBytes);
+#endif
         b.bytes = nb;
         ++arena_gen;  // captured graphs that hold the old pointer are stale
         if (name == "tables") pool_keys.clear();  // device table pool lost
@@ -86,7 +100,41 @@ void* pitt_ctx::buf(const std::string& name, size_t bytes) {
     return b.p;
 }
 
+void pitt_ctx::check_canaries(const char* where) {
+#ifdef PITT_SYNC_CHECK
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned char> h(kCanaryBytes);
+    for (auto& kv : bufs) {
+        if (!kv.second.p) continue;
+        (void)hipMemcpy(h.data(), (char*)kv.second.p + kv.second.bytes, kCanaryBytes, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < kCanaryBytes; ++i)
+            if (h[i] != 0xA5) {
+                std::fprintf(stderr, "PITT_SYNC_CHECK canary of %s (%zu B) corrupted at +%zu (%s)\n", kv.first.c_str(),
+                             kv.second.bytes, i, where);
+                break;
+            }
+    }
+    const size_t kSentinel = (size_t)256 << 20;
+    if (!sentinel) {
+        if (hipMalloc(&sentinel, kSentinel) != hipSuccess) sentinel = nullptr;
+        if (sentinel) (void)hipMemset(sentinel, 0xA5, kSentinel);
+        return;
+    }
+    std::vector<unsigned char> s(kSentinel);
+    (void)hipMemcpy(s.data(), sentinel, kSentinel, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < kSentinel; ++i)
+        if (s[i] != 0xA5) {
+            std::fprintf(stderr, "PITT_SYNC_CHECK sentinel corrupted at +%zu (%s)\n", i, where);
+            (void)hipMemset(sentinel, 0xA5, kSentinel);
+            break;
+        }
+#else
+    (void)where;
+#endif
+}
+
 void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
+    ++direct_epoch;
     auto& e = host_pinned[name];
     if (e.second < bytes || !e.first) {
         // an async copy queued on the stream may still read or write the old block; cached graphs
@@ -209,6 +257,7 @@ void pitt_destroy(pitt_ctx* ctx) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
+    if (ctx->sentinel) (void)hipFree(ctx->sentinel);
     for (auto& kv : ctx->host_pinned)
         if (kv.second.first) (void)hipHostFree(kv.second.first);
     for (auto& r : ctx->pending) {

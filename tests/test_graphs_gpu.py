@@ -1,14 +1,13 @@
-"""HIP-graph replay of the plane pipeline ("HIP graphs" and "The round-3 graph fault").
+"""HIP-graph replay of the plane pipeline ("HIP graphs" and "Graph replays and direct work").
 
 A batch layout seen twice is captured into a graph whose nodes hold device-arena and pinned-host
-addresses (the result / chunk-stat copy nodes write pinned host blocks).  A graph may only replay
-while every address it holds is live: any arena or pinned block that moves bumps the context's
-arena generation, which is part of the graph key.  The round-3 fault was a one-frame graph replayed
-after a larger batch on the same context had grown the pinned result block (`pinned()` freed the old
-block without bumping the generation before c6cc7e9): the replay's copy node wrote to freed host
-memory.  These tests drive exactly that sequence -- one-frame graphs, interleaved with batches and
-service calls that grow the arena and the pinned blocks -- with the graph floor at one frame, and hold
-every result to direct launches and the oracle."""
+addresses (the result / chunk-stat copy nodes write pinned host blocks).  A graph replays only while
+every address it holds is live (any arena or pinned block that moves bumps the arena generation, part
+of the key) and while no direct work ran on its context since it last ran (the direct epoch): a
+one-frame graph replayed after the primitive services' launches on the same stream faulted, in round 3
+and again in round 4 with the floor at one frame, so batches below 64 frames launch directly and a graph
+is captured afresh after direct work.  These tests hold replays, recaptures and direct launches to the
+same bits."""
 import os
 
 import numpy as np
@@ -62,40 +61,46 @@ def test_hip_graph_replay_bit_exact():
         graphed.close()
 
 
-def _one(ctx, b, inl):
+def _run(ctx, b, inl):
     inl.fill_(-7)
     res = ctx.plane_segment_batch(b, pitt.sac_params(), inl)
-    return res, inl[:int(res[0]["n_inliers"])].cpu().numpy()
+    return res, inl.cpu().numpy().copy()
 
 
-def test_one_frame_graph_survives_arena_and_pinned_growth():
-    """The round-3 fault's sequence: a one-frame layout captured into a graph, then batches that grow
-    the pinned result / chunk-stat blocks and the device arena, then the one-frame layout again.  The
-    stale graph must not replay (the arena generation moved, so the key is new: first sight launches
-    directly, the second recaptures), and every result stays bit-exact."""
-    frame = [pitt.synth_frame(0, 7100, 160, 120)]
-    big = [pitt.synth_frame(s % 3, 7200 + s, 160, 120) for s in range(160)]  # 160 records > one 4 KB pinned block
-    b1 = pitt.FrameBatch.from_host(frame, device="cuda:0")
+def _frames(n, seed, w=160, h=120):
+    return [pitt.synth_frame(s % 3, seed + s, w, h) for s in range(n)]
+
+
+def test_graph_survives_arena_and_pinned_growth():
+    """A 64-frame layout captured into a graph, then batches that grow the pinned result / chunk-stat
+    blocks and the device arena, then the 64-frame layout again: the stale graph is not replayed (the
+    arena generation moved, so the key is new: first sight launches directly, the second recaptures), and
+    every result stays bit-exact."""
+    small = _frames(64, 7100)
+    big = _frames(160, 7200)  # 160 records > one 4 KB pinned block
+    b1 = pitt.FrameBatch.from_host(small, device="cuda:0")
     bb = pitt.FrameBatch.from_host(big, device="cuda:0")
     inl1 = torch.empty(b1.capacity, dtype=torch.int32, device="cuda:0")
     inlb = torch.empty(bb.capacity, dtype=torch.int32, device="cuda:0")
-    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1)
+    ctx = _ctx(PITT_GRAPHS=1)
     try:
-        ref, ref_inl = _one(ctx, b1, inl1)               # first sight: direct
+        ref, ref_inl = _run(ctx, b1, inl1)               # first sight: direct
         for _ in range(2):                               # capture, then replay
-            r, i = _one(ctx, b1, inl1)
+            r, i = _run(ctx, b1, inl1)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl)
-        assert ctx.graph_stats() == (1, 1)
-        # grows "results_h" (160 x 48 B > 4096 B), the device arena (tiles x frames), "meta_h" ...
+        assert ctx.graph_stats() == (1, 2)
+        # grows "results_h" (160 x 56 B > 4096 B), the device arena (tiles x frames), "meta_h" ...
         res_b = ctx.plane_segment_batch(bb, pitt.sac_params(), inlb)
         # ... and more iterations per frame: more chunks, a larger "cstat_h" and larger hypothesis buffers
         res_c = ctx.plane_segment_batch(bb, pitt.sac_params(max_iterations=5000), inlb)
         caps, reps = ctx.graph_stats()
         for k in range(3):                               # new generation: direct, capture, replay
-            r, i = _one(ctx, b1, inl1)
+            r, i = _run(ctx, b1, inl1)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-        assert ctx.graph_stats() == (caps + 1, reps + 1), "a graph from before the arena moved was replayed"
-        P._check(ctx, frame, ref, [ref_inl])
+        assert ctx.graph_stats() == (caps + 1, reps + 2), "a graph from before the arena moved was replayed"
+        sample = [0, 1, 2, 33, 63]
+        P._check(ctx, [small[f] for f in sample], ref[sample],
+                 [ref_inl[b1.offsets[f]:b1.offsets[f] + ref[f]["n_inliers"]] for f in sample])
         ib = inlb.cpu().numpy()
         sample = [0, 1, 2, 77, 159]
         P._check(ctx, [big[f] for f in sample], res_c[sample],
@@ -105,29 +110,38 @@ def test_one_frame_graph_survives_arena_and_pinned_growth():
         ctx.close()
 
 
-def test_one_frame_graphs_between_service_calls():
-    """One-frame plane graphs replayed between the primitive services' direct launches on the same
-    context and stream (the round-3 setting), with clusters of growing size so that every service
-    grows its scratch between replays: the plane results equal a graph-free context's."""
-    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1)
+def test_graph_recaptured_after_service_calls():
+    """Service calls between two batches of a graphed layout are direct work on the context: the next
+    batch captures the graph afresh instead of replaying it, the one after replays, and every result
+    equals a graph-free context's.  The services' one-frame plane batches launch directly (below the
+    64-frame floor) and never capture."""
+    ctx = _ctx(PITT_GRAPHS=1)
     ref_ctx = _ctx(PITT_GRAPHS=0)
     srv, ref_srv = pitt.Services(ctx), pitt.Services(ref_ctx)
     try:
-        frame = [pitt.synth_frame(0, 7300, 160, 120)]
-        b1 = pitt.FrameBatch.from_host(frame, device="cuda:0")
-        inl1 = torch.empty(b1.capacity, dtype=torch.int32, device="cuda:0")
-        ref, ref_inl = _one(ref_ctx, b1, inl1)
-        replays0 = ctx.graph_stats()[1]
-        for k, n in enumerate((300, 300, 1200, 1200, 4000, 9000, 300)):
+        frames = _frames(64, 7300)
+        b = pitt.FrameBatch.from_host(frames, device="cuda:0")
+        inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+        ref, ref_inl = _run(ref_ctx, b, inl)
+        for _ in range(3):                                 # direct, capture, replay
+            r, i = _run(ctx, b, inl)
+            assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl)
+        assert ctx.graph_stats() == (1, 2)
+        for k, n in enumerate((300, 1200, 4000)):
             cloud = sphere_scene(n, n // 5, 900 + k).astype(np.float32)
+            caps, reps = ctx.graph_stats()
             a = srv.ransac_sphere(cloud)
-            c = srv.ransac_plane(cloud)     # a one-frame batch through the single-cloud ABI (pinned staging)
+            c = srv.ransac_plane(cloud)                    # one frame: direct, no capture
+            assert ctx.graph_stats() == (caps, reps)
             assert a[0] == ref_srv.ransac_sphere(cloud)[0]
             d = ref_srv.ransac_plane(cloud)
             assert c[0] == d[0] and np.array_equal(c[1], d[1]) and np.array_equal(c[2].view(np.int32), d[2].view(np.int32))
-            r, i = _one(ctx, b1, inl1)
+            r, i = _run(ctx, b, inl)                       # after direct work: captured afresh
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-        assert ctx.graph_stats()[1] > replays0  # some of those one-frame batches did replay a graph
+            assert ctx.graph_stats() == (caps + 1, reps + 1), k
+            r, i = _run(ctx, b, inl)                       # nothing in between: replayed
+            assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
+            assert ctx.graph_stats() == (caps + 1, reps + 2), k
     finally:
         srv.close()
         ref_srv.close()

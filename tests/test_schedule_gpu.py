@@ -45,7 +45,7 @@ def test_continuation_after_a_learnt_short_schedule(graphs):
     bm = pitt.FrameBatch.from_host(mixed, device="cuda:0")
     assert b.capacity == bm.capacity and list(b.offsets) == list(bm.offsets)
     inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
-    ctx = _ctx(PITT_GRAPHS=graphs)
+    ctx = _ctx(PITT_GRAPHS=graphs, PITT_GRAPH_MIN_FRAMES=1)  # graphs (when on) for this 6-frame layout
     full = _ctx(PITT_ADAPTIVE_CHUNKS=0)
     try:
         for _ in range(3):  # the table layout: the hint learns the short schedule
