@@ -90,7 +90,7 @@ int run_obj(const std::string& in, const std::string& out, const std::string& ar
         set_param("arm_filter=int:0");
     } else if (arm != "missing") {  // the reference's arm filter service, stood in by the identity or a crop on x
         const bool crop = arm.rfind("crop:", 0) == 0;
-        const double cx = crop ? std::strtod(arm.c_str() + 5, nullptr) : 0.0;
+        const float cx = crop ? std::strtof(arm.c_str() + 5, nullptr) : 0.0f;  // compared in float, as the test's oracle side
         ros::stub::services()["arm_filter_srv"] = [crop, cx](void* p) {
             pitt_msgs::ArmFilter& s = *static_cast<pitt_msgs::ArmFilter*>(p);
             const std::vector<float> pts = pitt_ros::to_xyz16(s.request.input_cloud);

@@ -94,10 +94,14 @@ def test_graph_survives_arena_and_pinned_growth():
         # ... and more iterations per frame: more chunks, a larger "cstat_h" and larger hypothesis buffers
         res_c = ctx.plane_segment_batch(bb, pitt.sac_params(max_iterations=5000), inlb)
         caps, reps = ctx.graph_stats()
-        for k in range(3):                               # new generation: direct, capture, replay
+        r, i = _run(ctx, b1, inl1)                       # the arena moved: a new key's first sight (direct)
+        assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl)
+        c1, r1 = ctx.graph_stats()
+        assert (c1, r1) == (caps, reps), "a graph from before the arena moved was replayed"
+        for k in range(2):                               # capture, replay
             r, i = _run(ctx, b1, inl1)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-        assert ctx.graph_stats() == (caps + 1, reps + 2), "a graph from before the arena moved was replayed"
+        assert ctx.graph_stats() == (caps + 1, reps + 2)
         sample = [0, 1, 2, 33, 63]
         P._check(ctx, [small[f] for f in sample], ref[sample],
                  [ref_inl[b1.offsets[f]:b1.offsets[f] + ref[f]["n_inliers"]] for f in sample])
@@ -136,12 +140,17 @@ def test_graph_recaptured_after_service_calls():
             assert a[0] == ref_srv.ransac_sphere(cloud)[0]
             d = ref_srv.ransac_plane(cloud)
             assert c[0] == d[0] and np.array_equal(c[1], d[1]) and np.array_equal(c[2].view(np.int32), d[2].view(np.int32))
-            r, i = _run(ctx, b, inl)                       # after direct work: captured afresh
+            # after direct work the old graph never replays: the batch is captured afresh (or, when the
+            # services' scratch grew and moved the arena, launched directly as a new key's first sight)
+            r, i = _run(ctx, b, inl)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-            assert ctx.graph_stats() == (caps + 1, reps + 1), k
-            r, i = _run(ctx, b, inl)                       # nothing in between: replayed
-            assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-            assert ctx.graph_stats() == (caps + 1, reps + 2), k
+            c1, r1 = ctx.graph_stats()
+            assert c1 - caps == r1 - reps and c1 - caps <= 1, (k, caps, reps, c1, r1)
+            for _ in range(2):                             # nothing in between: capture / replay
+                r, i = _run(ctx, b, inl)
+                assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
+            c2, r2 = ctx.graph_stats()
+            assert c2 == caps + 1 and r2 == r1 + 2, (k, caps, reps, c2, r2)
     finally:
         srv.close()
         ref_srv.close()
