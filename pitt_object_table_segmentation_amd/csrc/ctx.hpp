@@ -179,6 +179,12 @@ struct pitt_ctx {
     // direct plane enqueue and continuation.  A graph replays only if none happened since it last ran;
     // otherwise it is captured afresh ("Graph replays and direct work").
     uint64_t direct_epoch = 0;
+    uint32_t call_seq = 0;  // plane batches enqueued; stamped into each frame's metadata (FrameMeta.pad)
+#ifdef PITT_SYNC_CHECK
+    // debug knobs for the graph-ordering investigation
+    bool dbg_no_epoch = pitt_env_flag("PITT_DBG_NO_EPOCH", false);
+    bool dbg_sync_before_graph = pitt_env_flag("PITT_DBG_SYNC_BEFORE_GRAPH", false);
+#endif
     std::vector<GraphEntry> graphs;
     std::vector<std::vector<uint64_t>> graph_seen;  // keys launched once (captured on a repeat)
     uint64_t graph_clock = 0;

@@ -66,6 +66,24 @@ __device__ __forceinline__ void acct_add(unsigned long long* acct, int k, unsign
     if (acct && bytes) atomicAdd(&acct[k * kAcShards + (blockIdx.x & (kAcShards - 1))], bytes);
 }
 
+// Debug builds (-DPITT_SYNC_CHECK): every batch stamps its frame metadata with a call sequence number,
+// and k_hypothesize compares the stamp it reads with the one the host wrote into a pinned (host-
+// coherent) word just before the launch.  A mismatch means the batch's kernels started before the
+// metadata copy enqueued ahead of them had landed: k_hypothesize records it and every later kernel of
+// the path returns at entry, so stale metadata is reported instead of being indexed with.
+#ifdef PITT_SYNC_CHECK
+__device__ unsigned int g_dbg_stale;
+__device__ unsigned int g_dbg_seen[4];
+#define PITT_DBG_GUARD()                                                  \
+    do {                                                                  \
+        if (*(volatile unsigned int*)&g_dbg_stale) return;                \
+    } while (0)
+#else
+#define PITT_DBG_GUARD() \
+    do {                 \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------------------------------
 // Hypotheses, generated lazily in windows of kBlock sampler-table attempts.  Attempt a uses table
 // triple a (the sampler's draws depend only on (n, seed) until a sample is rejected; rejected
@@ -161,10 +179,31 @@ __global__ __launch_bounds__(kBlock) void k_hypothesize(
     const FrameMeta* __restrict__ meta, const int32_t* __restrict__ tables, int A, int hcap, int target,
     int runnable_all, float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt,
     FrameState* __restrict__ st, int32_t* __restrict__ list0, int32_t* __restrict__ cnt0,
-    ChunkStat* __restrict__ stat0, unsigned long long* __restrict__ acct) {
+    ChunkStat* __restrict__ stat0, unsigned long long* __restrict__ acct, const unsigned int* dbg_seq) {
     __shared__ GenLds G;
     const int f = blockIdx.x;
     const FrameMeta m = meta[f];
+#ifdef PITT_SYNC_CHECK
+    {
+        __shared__ int stale;
+        if (threadIdx.x == 0) {
+            const unsigned int want = dbg_seq ? *(const volatile unsigned int*)dbg_seq : (unsigned int)m.pad;
+            stale = (unsigned int)m.pad != want;
+            if (stale) {
+                g_dbg_seen[0] = (unsigned int)m.pad;
+                g_dbg_seen[1] = want;
+                g_dbg_seen[2] = (unsigned int)m.n;
+                g_dbg_seen[3] = (unsigned int)f;
+                __threadfence();
+                atomicExch(&g_dbg_stale, 1u);
+            }
+        }
+        __syncthreads();
+        if (stale || *(volatile unsigned int*)&g_dbg_stale) return;
+    }
+#else
+    (void)dbg_seq;
+#endif
     const bool runnable = runnable_all && m.n >= 3;
     if (threadIdx.x == 0) {
         FrameState& s = G.s;
@@ -681,6 +720,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box,
     float* __restrict__ group_box) {
+    PITT_DBG_GUARD();
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
     __shared__ float4 wlist[kScoreWaves][64];  // four 16-entry survivor lists, one per group
     __shared__ float4 wbox[kScoreWaves][BOX ? 1 : 64];  // later chunks: the item's 32 group boxes
@@ -769,6 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     ChunkStat* __restrict__ next_stat, const float* __restrict__ X, const float* __restrict__ Y,
     const float* __restrict__ Z, const int32_t* __restrict__ tables, int A, int target_next,
     float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt, unsigned long long* __restrict__ acct) {
+    PITT_DBG_GUARD();
     __shared__ GenLds G;
     __shared__ int32_t part[kBlock / 64][kMaxChunk];
     __shared__ int32_t tot[kMaxChunk];
@@ -866,6 +907,7 @@ extend:
 __global__ void k_decide(const FrameMeta* __restrict__ meta, FrameState* __restrict__ st,
                          const float4* __restrict__ hyp_coef, int hcap, int n_frames, int optimize,
                          float4* __restrict__ best_coef, float4* __restrict__ final_coef, int phase) {
+    PITT_DBG_GUARD();
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_frames) return;
     FrameState s = st[f];
@@ -1389,6 +1431,7 @@ __global__ __launch_bounds__(64 * (P + 2)) void k_refine(
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
     int tiles_max, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct,
     unsigned long long* __restrict__ rdbg, int mode, const int32_t* __restrict__ only, int phase) {
+    PITT_DBG_GUARD();
     __shared__ RefineLds<P> L;
     const long long t_start = rdbg ? clock64() : 0;
     const int f = blockIdx.x;
@@ -1582,6 +1625,7 @@ __global__ __launch_bounds__(64 * (F + 2)) void k_refine_multi(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st,
     const float4* __restrict__ best_coef, float thf, const int32_t* __restrict__ tile_counts, int hstride,
     int tiles_max, int n_frames, float4* __restrict__ final_coef, unsigned long long* __restrict__ acct, int mode) {
+    PITT_DBG_GUARD();
     __shared__ RefineLdsP LL[F];
     __shared__ int act[F];
     const int lane = threadIdx.x & 63;
@@ -1738,6 +1782,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xrefine(
     float thf, const int32_t* __restrict__ tile_counts, int hstride, int tiles_max, float4* __restrict__ final_coef,
     int32_t* __restrict__ fallback, int32_t* __restrict__ fallback_count, unsigned long long* __restrict__ acct,
     int force_fallback, unsigned long long* __restrict__ rdbg) {
+    PITT_DBG_GUARD();
     __shared__ XRefineLds L;
     const long long t_start = rdbg ? clock64() : 0;
     unsigned long long n_seq = 0, n_run = 0, n_wait = 0;
@@ -2010,6 +2055,7 @@ __global__ __launch_bounds__(kBlock) void k_cov_tiles(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
     float thf, const int32_t* __restrict__ tile_counts, int hstride, int n_frames, int tiles_max,
     CovPart* __restrict__ part) {
+    PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -2060,6 +2106,7 @@ template <int ORDER>
 __global__ __launch_bounds__(64) void k_cov_final(const FrameMeta* __restrict__ meta,
                                                   const FrameState* __restrict__ st, const CovPart* __restrict__ part,
                                                   int n_frames, int tiles_max, float4* __restrict__ final_coef) {
+    PITT_DBG_GUARD();
     const int f = blockIdx.x;
     const int lane = threadIdx.x;
     if (f >= n_frames) return;
@@ -2110,6 +2157,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ final_coef,
     float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, const float* __restrict__ group_box,
     uint32_t* __restrict__ sel_bits, int32_t* __restrict__ sel_cnt, uint32_t* __restrict__ acct_tile) {
+    PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -2157,6 +2205,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, int n_frames, int tiles_max,
     const uint32_t* __restrict__ sel_bits, const int32_t* __restrict__ sel_cnt, int32_t* __restrict__ inliers,
     int32_t* __restrict__ n_final, uint32_t* __restrict__ acct_tile) {
+    PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -2188,6 +2237,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
 __global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __restrict__ hyp_attempt,
                            const float4* __restrict__ final_coef, const int32_t* __restrict__ n_final,
                            int hcap, int n_frames, pitt_plane_result* __restrict__ res) {
+    PITT_DBG_GUARD();
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_frames) return;
     const FrameState s = st[f];
@@ -2236,6 +2286,7 @@ __global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X
                                                      const FrameState* __restrict__ st, const float4* __restrict__ best_coef,
                                                      float thf, int n_frames, int tiles_max, int32_t* __restrict__ tcnt,
                                                      int phase) {
+    PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -2260,6 +2311,7 @@ __global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X
 __global__ __launch_bounds__(256) void k_xr_scan(const FrameMeta* __restrict__ meta, int tiles_max,
                                                  int32_t* __restrict__ tcnt, XsSeg* __restrict__ seg,
                                                  int32_t* __restrict__ blk_seg) {
+    PITT_DBG_GUARD();
     const int f = blockIdx.x;
     __shared__ int64_t base;
     __shared__ int32_t part[256];
@@ -2304,6 +2356,7 @@ __global__ __launch_bounds__(kBlock) void k_xr_write(const float* __restrict__ X
                                                      float thf, int n_frames, int tiles_max, const int32_t* __restrict__ toff,
                                                      const XsSeg* __restrict__ seg, float* __restrict__ V, int64_t T,
                                                      int phase) {
+    PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
@@ -2345,6 +2398,7 @@ __global__ __launch_bounds__(kBlock) void k_xr_write(const float* __restrict__ X
 template <int ORDER, int DIV>
 __global__ void k_xr_plane(const FrameState* __restrict__ st, const XsSeg* __restrict__ seg,
                            const float* __restrict__ sums, int n_frames, float4* __restrict__ final_coef, int phase) {
+    PITT_DBG_GUARD();
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_frames || !xr_eligible(st[f], phase)) return;
     float a9[9];
@@ -2435,12 +2489,18 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         }
     }
     // --- frame metadata ---
+    const uint32_t seq = ++ctx->call_seq;
+    unsigned int* dbg_seq = nullptr;  // the debug build's pinned copy of the stamp (k_hypothesize compares)
+#ifdef PITT_SYNC_CHECK
+    dbg_seq = as<unsigned int>(ctx->pinned("dbg_seq_h", 16));
+    if (!dbg_seq) return ctx->fail(PITT_E_NOMEM, "pinned stamp");
+#endif
     FrameMeta* hm = as<FrameMeta>(ctx->pinned("meta_h", (size_t)nf * sizeof(FrameMeta)));
     for (int f = 0; f < nf; ++f) {
         hm[f].off = fr->offsets[f];
         hm[f].n = fr->counts[f];
         hm[f].tiles = (int32_t)((fr->counts[f] + kTile - 1) / kTile);
-        hm[f].pad = 0;
+        hm[f].pad = (int32_t)seq;
         int64_t ti = 0;
         for (size_t i = 0; i < distinct.size(); ++i)
             if (distinct[i] == fr->counts[f]) ti = (int64_t)(i * tab_ints);
@@ -2572,7 +2632,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     acct_recs[kAcHyp] = rec;
     hipLaunchKernelGGL((k_hypothesize<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, fx, fy, fz, meta,
                        tables, A, hcap, std::min(chunks[0], hcap), runnable_all, hyp_coef, hyp_attempt, st, lists,
-                       counters, cstat, acct);
+                       counters, cstat, acct, dbg_seq);
     PITT_CHECK_LAUNCH("k_hypothesize", -1, phase);
     ctx->prof_end(rec);
     }
@@ -2713,6 +2773,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     };
     auto enqueue_front = [&]() -> int { return enqueue(0, K, 1, true, acct_recs, score_recs); };
     ctx->direct_epoch = epoch0;
+#ifdef PITT_SYNC_CHECK
+    *(volatile unsigned int*)dbg_seq = seq;
+#endif
     // Graphs from ctx->graph_min_frames frames up (64 by default), replayed only while no direct work
     // ran on the context since the graph last ran ("Graph replays and direct work").
     if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
@@ -2732,7 +2795,12 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         bool recapture = false;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
-        if (hit && hit->epoch != ctx->direct_epoch) {
+#ifdef PITT_SYNC_CHECK
+        const bool epoch_rule = !ctx->dbg_no_epoch;
+#else
+        const bool epoch_rule = true;
+#endif
+        if (hit && hit->epoch != ctx->direct_epoch && epoch_rule) {
             // direct work ran on this context since the graph last ran: capture it afresh instead of
             // replaying (one-frame graphs replayed after the primitive services' launches faulted)
             (void)hipGraphExecDestroy(hit->exec);
@@ -2778,6 +2846,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         if (hit) {
             hit->last_use = ++ctx->graph_clock;
             hit->epoch = ctx->direct_epoch;
+#ifdef PITT_SYNC_CHECK
+            if (ctx->dbg_sync_before_graph) PITT_HIP_TRY(hipStreamSynchronize(sm));
+#endif
             PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
 #ifdef PITT_SYNC_CHECK
             {
@@ -2809,8 +2880,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         ++ctx->direct_epoch;
     }
 #ifdef PITT_SYNC_CHECK
-    std::fprintf(stderr, "PITT_SYNC_CHECK call nf %d n0 %lld K %d/%d xs %d xs_T %lld tiles_max %d gen %llu\n", nf,
-                 (long long)fr->counts[0], K, nchunks, (int)xs, (long long)xs_T, tiles_max,
+    std::fprintf(stderr, "PITT_SYNC_CHECK call seq %u nf %d n0 %lld K %d/%d xs %d xs_T %lld tiles_max %d gen %llu\n",
+                 seq, nf, (long long)fr->counts[0], K, nchunks, (int)xs, (long long)xs_T, tiles_max,
                  (unsigned long long)ctx->arena_gen);
 #endif
     // the continuation, should a frame still be running after the K chunks (finish_batch)
@@ -2846,6 +2917,20 @@ int finish_batch(pitt_ctx* ctx) {
     if (!ctx->inflight) return PITT_OK;
     ctx->inflight = false;
     PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+#ifdef PITT_SYNC_CHECK
+    {
+        unsigned int stale = 0, seen[4] = {0, 0, 0, 0};
+        (void)hipMemcpyFromSymbol(&stale, HIP_SYMBOL(g_dbg_stale), sizeof stale);
+        if (stale) {
+            (void)hipMemcpyFromSymbol(seen, HIP_SYMBOL(g_dbg_seen), sizeof seen);
+            std::fprintf(stderr, "PITT_SYNC_CHECK STALE METADATA: k_hypothesize read stamp %u (n %u, frame %u), host wrote %u\n",
+                         seen[0], seen[2], seen[3], seen[1]);
+            const unsigned int zero = 0;
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_stale), &zero, sizeof zero);
+            return ctx->fail(PITT_E_HIP, "sync check: a batch read stale frame metadata");
+        }
+    }
+#endif
     const ChunkStat* cs = (const ChunkStat*)ctx->inflight_hstat;
     const int nchunks = (int)ctx->inflight_chunks.size();
     if (ctx->inflight_cont && cs[ctx->inflight_k].tiles > 0) {

@@ -102,13 +102,18 @@ def test_graph_survives_arena_and_pinned_growth():
             r, i = _run(ctx, b1, inl1)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
         assert ctx.graph_stats() == (caps + 1, reps + 2)
+        # per-hypothesis counts are read from the context's last batch: b1 ran last here
         sample = [0, 1, 2, 33, 63]
         P._check(ctx, [small[f] for f in sample], ref[sample],
-                 [ref_inl[b1.offsets[f]:b1.offsets[f] + ref[f]["n_inliers"]] for f in sample])
+                 [ref_inl[b1.offsets[f]:b1.offsets[f] + ref[f]["n_inliers"]] for f in sample], frame_ids=sample)
+        # run the 160-frame layout again so that its counts are the last batch's, then check a sample of it
+        res_c2 = ctx.plane_segment_batch(bb, pitt.sac_params(max_iterations=5000), inlb)
+        assert res_c2.tobytes() == res_c.tobytes()
         ib = inlb.cpu().numpy()
         sample = [0, 1, 2, 77, 159]
         P._check(ctx, [big[f] for f in sample], res_c[sample],
-                 [ib[bb.offsets[f]:bb.offsets[f] + res_c[f]["n_inliers"]] for f in sample], max_iterations=5000)
+                 [ib[bb.offsets[f]:bb.offsets[f] + res_c[f]["n_inliers"]] for f in sample], frame_ids=sample,
+                 max_iterations=5000)
         assert res_b["hypotheses"].min() > 0
     finally:
         ctx.close()

@@ -31,7 +31,8 @@ def _check(ctx, frames, res, inls, frame_ids=None, **kw):
                                                   "optimize", "seed", "probability")}
     for i, (f, r, inl) in enumerate(zip(frames, res, inls)):
         o = orc.plane_segment(*f, **okw)
-        tag = f"frame {i}"
+        fid = i if frame_ids is None else frame_ids[i]  # the frame's index in the context's last batch
+        tag = f"frame {fid}"
         assert r["hypotheses"] == o.hypotheses, tag
         if o.coefficients.size == 0:
             assert r["n_coeff"] == 0 and r["n_inliers"] == 0, tag
@@ -39,7 +40,7 @@ def _check(ctx, frames, res, inls, frame_ids=None, **kw):
         assert r["status"] == 0 and r["n_coeff"] == 4, tag
         assert r["best_hypothesis"] == o.best_hypothesis and r["best_count"] == o.best_count, tag
         assert r["rejected_samples"] == o.rejected_samples, tag
-        assert np.array_equal(ctx.hypothesis_counts(i, o.hypotheses), o.hyp_counts), tag
+        assert np.array_equal(ctx.hypothesis_counts(fid, o.hypotheses), o.hyp_counts), tag
         assert np.array_equal(inl, o.inliers), tag
         assert np.array_equal(r["coefficients"], o.coefficients, equal_nan=True), tag  # NaN: degenerate covariance
         if np.all(np.isfinite(o.coefficients)):
@@ -118,12 +119,13 @@ def _oracle_all(frames, **okw):
 
 def _check_all(ctx, frames, res, inls, oracle_out):
     for i, (r, inl, o) in enumerate(zip(res, inls, oracle_out)):
-        tag = f"frame {i}"
+        fid = i
+        tag = f"frame {fid}"
         assert r["hypotheses"] == o.hypotheses, tag
         assert r["status"] == 0 and r["n_coeff"] == 4, tag
         assert r["best_hypothesis"] == o.best_hypothesis and r["best_count"] == o.best_count, tag
         assert r["rejected_samples"] == o.rejected_samples, tag
-        assert np.array_equal(ctx.hypothesis_counts(i, o.hypotheses), o.hyp_counts), tag
+        assert np.array_equal(ctx.hypothesis_counts(fid, o.hypotheses), o.hyp_counts), tag
         assert np.array_equal(inl, o.inliers), tag
         assert np.array_equal(r["coefficients"].view(np.int32), o.coefficients.view(np.int32)), tag
         assert r["flags"] == 0, tag
