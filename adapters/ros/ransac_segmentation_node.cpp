@@ -99,8 +99,13 @@ void clustersAcquisition(const pitt_msgs::ClustersOutputConstPtr& clusterObj) {
         const int rc = pitt_srv_classify_clusters(pitt_ros::node().srv, x.data(), y.data(), z.data(), off.data(),
                                                   cnt.data(), nc, shapes.data());
         if (rc != PITT_OK) {
+            // the reference treats a failed service call as 0 inliers (:82, :118, :156, :197) and still
+            // publishes one shape per cluster, which the arbitration then tags unknown (:298-302)
             ROS_ERROR_STREAM("ransac segmentation (MI355X) failed: " << pitt_last_error(pitt_ros::node().ctx));
-            return;  // nothing published for the frame
+            for (pitt_cluster_shape& s : shapes) {
+                s = {};
+                s.tag = PITT_SHAPE_UNKNOWN;
+            }
         }
         for (int32_t j = 0; j < nc; ++j) {
             const pitt_cluster_shape& s = shapes[(size_t)j];

@@ -47,7 +47,9 @@
 extern "C" {
 #endif
 
-/* 3: pitt_sac_params.cov_mode (A6), pitt_cylinder_params / pitt_cone_params.eigen33, pitt_build_flags */
+/* 3: pitt_sac_params.cov_mode (A6), pitt_cylinder_params / pitt_cone_params.eigen33, pitt_build_flags.
+ * Callers check pitt_abi_version() == PITT_ABI_VERSION when they load the library: the structs passed
+ * by pointer are read in this ABI's layout. */
 #define PITT_ABI_VERSION 3
 /* Points per scoring tile; frames are scored in tiles of this many points. */
 #define PITT_TILE_POINTS 2048
@@ -162,9 +164,13 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
 int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev);
 
-/* Asynchronous form: enqueues the whole batch on the context's stream and returns; `results` is
- * filled by pitt_wait (or by the next call on the context).  One batch in flight per context --
- * overlap consecutive batches with two contexts on two streams. */
+/* Asynchronous form: enqueues the batch on the context's stream and returns; `results` is filled by
+ * pitt_wait (or by the next call on the context).  One batch in flight per context -- overlap
+ * consecutive batches with two contexts on two streams.  With the adaptive chunk schedule a frame
+ * that needs more scoring chunks than recent batches of the layout did is finished by pitt_wait
+ * (the remaining chunks are enqueued there), so inliers_dev and the results are complete only after
+ * pitt_wait (or any later call on the context, pitt_memcpy included): device work the caller orders
+ * after this call on the stream must follow pitt_wait. */
 int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
                                    pitt_plane_result* results, int32_t* inliers_dev);
 int pitt_wait(pitt_ctx* ctx);

@@ -216,6 +216,8 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 
 # name -> (restype, argtypes); every symbol declared in include/pitt_seg.h
+PITT_ABI_VERSION = 3  # include/pitt_seg.h
+
 SIGNATURES = {
     "pitt_abi_version": (_i32, []),
     "pitt_build_flags": (_i32, []),
@@ -346,6 +348,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the structs below are laid out for this ABI: a library of another ABI would read or write past
+    # them (pitt_seg.h: callers check pitt_abi_version() at load)
+    if lib.pitt_abi_version() != PITT_ABI_VERSION:
+        raise ImportError(f"{path} implements ABI {lib.pitt_abi_version()}, this binding ABI {PITT_ABI_VERSION}")
     return lib
 
 

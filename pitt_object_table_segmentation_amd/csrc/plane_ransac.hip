@@ -2588,6 +2588,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
              ctx->refine_mode == 2 && !ctx->refine_debug;
     int64_t xs_blocks = 0;
     for (int f = 0; f < nf; ++f) xs_blocks += (fr->counts[f] + kXsBlk - 1) / kXsBlk;
+    if (xs_blocks == 0) xs = false;  // every frame empty: nothing to refine (and no block -> segment map)
     const int64_t xs_T = std::max<int64_t>(1, xs_blocks) * kXsBlk;
     float* xr_v = nullptr;
     int32_t *xr_tcnt = nullptr, *xr_bseg = nullptr;

@@ -313,6 +313,9 @@ int pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     if (bytes < 0 || (bytes > 0 && (!dst || !src))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (bytes == 0) return PITT_OK;
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    // a batch in flight may still have chunks to run (the adaptive schedule's continuation): complete
+    // it first, so that a copy of its inliers_dev sees the whole batch
+    if (int rc = pitt::finish_batch(ctx)) return rc;
     PITT_HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, ctx->stream));
     PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return PITT_OK;
@@ -346,8 +349,8 @@ int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* fr, const p
         return ctx->fail(PITT_E_INVALID, "inliers_dev must be 4-byte aligned");
     if (p->reduce_order < 0 || p->reduce_order > 2 || p->div_mode < 0 || p->div_mode > 1)
         return ctx->fail(PITT_E_INVALID, "reduce_order / div_mode out of range");
-    // a caller built against ABI 2 passes the shorter struct: whatever lies past its end is
-    // rejected here unless it happens to read as a valid mode (ABI 3 added cov_mode)
+    // cov_mode is an ABI-3 field: callers check pitt_abi_version() == PITT_ABI_VERSION at load
+    // (pitt_seg.h), so the struct passed here is always the ABI-3 layout
     if (p->cov_mode != PITT_COV_EXACT && p->cov_mode != PITT_COV_FAST)
         return ctx->fail(PITT_E_INVALID, "cov_mode out of range");
     for (int f = 0; f < fr->n_frames; ++f) {
