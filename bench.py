@@ -17,6 +17,8 @@ Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, 
                 the data-dependent ones) and its launch time
   clutter       a clutter-scene batch (T = 1001 hypotheses per frame) against the VALU roof
   pcie_fed      frames/s when every batch starts in pinned host memory (H2D copy in the step)
+  streaming     every step's buffers receive new frames (a clutter-bearing batch among them): frames/s,
+                continuations and graph captures per 100 batches
   config2       one cloud through the single-cloud ABI (host in, host out), median latency
   config5       find_supports + euclidean_clusters on the 1.2M-point fused scene, GPU vs oracle
   cpu_baseline  the oracle (CPU restatement of PCL's path) on the host: frame-parallel on the
@@ -274,6 +276,96 @@ def pcie_pass(pitt, ctxs, host_batches, dev, params, steps):
             "h2d_bytes_per_batch": nbytes, "h2d_GBps": round(nbytes * steps / dt / 1e9, 1), "steps": steps}
 
 
+def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per_batch=8, pool_n=5):
+    """The streaming case a drop-in sees: every step's batch buffers receive new
+    frames.  A pool of `pool_n` distinct batches is staged in HBM; pool batch 0 holds `clutter_per_batch`
+    clutter frames (T = 1001) among its table frames, the others table frames only, so 1 batch in
+    `pool_n` needs the whole chunk schedule.  Step i copies pool batch i % pool_n into the buffers of
+    context i % len(ctxs) (a device-to-device copy on that context's stream, ahead of its batch), so a
+    context's buffers hold new content at every use.  Reported: frames/s with the copies inside the
+    steps, the copies' own time (a copy-only pass), continuations and graph captures per 100 batches."""
+    import torch
+    B = batches[0].n_frames
+    rng = np.random.default_rng(77)
+    clutter_at = set(rng.choice(B, clutter_per_batch, replace=False).tolist())
+    pool = []
+    for q in range(pool_n):
+        ids = range(20000 + q * B, 20000 + (q + 1) * B)
+        fr = make_frames(ids, threads)
+        if q == 0:
+            cl = make_frames([20000 + q * B + f for f in sorted(clutter_at)], threads, pitt.SCENE_CLUTTER)
+            for f, c in zip(sorted(clutter_at), cl):
+                fr[f] = c
+        pool.append(pitt.FrameBatch.from_host(fr, device=dev))
+    assert all(p.capacity == batches[0].capacity and list(p.offsets) == list(batches[0].offsets) for p in pool)
+    streams = [torch.cuda.Stream(device=dev) for _ in ctxs]
+    outs = [torch.empty(b.capacity, dtype=torch.int32, device=dev) for b in batches]
+    for c, st in zip(ctxs, streams):
+        c.set_stream(st)
+    pending = [False] * len(ctxs)
+
+    def step(i, run=True):
+        j = i % len(ctxs)
+        if pending[j]:
+            ctxs[j].wait()
+            pending[j] = False
+        src = pool[i % pool_n]
+        with torch.cuda.stream(streams[j]):
+            for d, h in zip((batches[j].x, batches[j].y, batches[j].z), (src.x, src.y, src.z)):
+                d.copy_(h, non_blocking=True)
+        if run:
+            ctxs[j].plane_segment_batch_async(batches[j], params, outs[j])
+            pending[j] = True
+
+    def drain():
+        for j, c in enumerate(ctxs):
+            if pending[j]:
+                c.wait()
+                pending[j] = False
+        torch.cuda.synchronize()
+
+    for i in range(2 * len(ctxs) * pool_n):  # every context sees every pool batch (hint and graph settle)
+        step(i)
+    drain()
+    cont0 = sum(c.schedule_stats()[0] for c in ctxs)
+    cap0 = sum(c.graph_stats()[0] for c in ctxs)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    drain()
+    dt = time.perf_counter() - t0
+    cont = sum(c.schedule_stats()[0] for c in ctxs) - cont0
+    caps = sum(c.graph_stats()[0] for c in ctxs) - cap0
+    t1 = time.perf_counter()
+    for i in range(steps):
+        step(i, run=False)
+    drain()
+    dc = time.perf_counter() - t1
+    # the last batch of every context against its pool batch, through the oracle on one frame each
+    ok = True
+    for j in range(len(ctxs)):
+        i = steps - len(ctxs) + j
+        if i < 0:
+            continue
+        src = pool[i % pool_n]
+        res = ctxs[i % len(ctxs)].plane_segment_batch(src, params, outs[i % len(ctxs)])
+        f = min(clutter_at) if i % pool_n == 0 else 0
+        o = oracle().plane_segment(*(t[int(src.offsets[f]):int(src.offsets[f]) + int(src.counts[f])].cpu().numpy()
+                                     for t in (src.x, src.y, src.z)))
+        ok &= bool(res[f]["hypotheses"] == o.hypotheses and np.array_equal(res[f]["coefficients"], o.coefficients))
+    for c in ctxs:
+        c.set_stream(None)
+    nbytes = sum(t.numel() * 4 for t in (pool[0].x, pool[0].y, pool[0].z))
+    return {"frames_per_s": round(B * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+            "copy_ms_per_step": round(dc / steps * 1e3, 4), "copy_bytes_per_step": nbytes,
+            "frames_per_s_copies_excluded": round(B * steps / max(1e-9, dt - dc), 1),
+            "clutter_frames": f"{clutter_per_batch} of {B} in 1 of {pool_n} pool batches",
+            "continuations_per_100_batches": round(100.0 * cont / steps, 2),
+            "graph_captures_per_100_batches": round(100.0 * caps / steps, 2),
+            "spot_check_vs_oracle": ok,
+            "note": "a step = a device-to-device copy of new frames into the context's buffers, then its batch"}
+
+
 def config2_pass(pitt, ctx, frame, reps=10):
     """BASELINE config 2: one 640x480 cloud through the single-cloud ABI (pitt_plane_segment: PointXYZ
     host array in, inliers and coefficients back on the host -- the service handler's path, PCIe
@@ -288,9 +380,32 @@ def config2_pass(pitt, ctx, frame, reps=10):
         r = ctx.plane_segment(cloud)
         ts.append((time.perf_counter() - t) * 1e3)
     o = oracle().plane_segment(*frame)
+    # where the time goes: the same frame as a device-resident one-frame batch (no PCIe, no AoS -> SoA),
+    # and that batch's kernels by the library's HIP-event profiler
+    import torch
+    b = pitt.FrameBatch.from_host([frame], device="cuda")
+    out = torch.empty(b.capacity, dtype=torch.int32, device="cuda")
+    ctx.plane_segment_batch(b, pitt.sac_params(), out)
+    td = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        ctx.plane_segment_batch(b, pitt.sac_params(), out)
+        td.append((time.perf_counter() - t) * 1e3)
+    ctx.profile(True)
+    ctx.profile_reset()
+    for _ in range(reps):
+        ctx.plane_segment_batch(b, pitt.sac_params(), out)
+    kern = {}
+    for k in ("k_hypothesize", "k_score", "k_replay", "k_refine:xsum", "k_refine", "k_sel_mark", "k_sel_write"):
+        n, ms, _ = ctx.profile_get(k)
+        if n:
+            kern[k] = round(ms / reps * 1e3, 1)
+    ctx.profile(False)
     return {"ms_per_frame": round(float(np.median(ts)), 3), "statistic": f"median of {reps} after 1 warm-up",
             "inliers": int(len(r.inliers)), "matches_oracle": bool(np.array_equal(r.inliers, o.inliers) and
-                                                                 np.array_equal(r.coefficients, o.coefficients))}
+                                                                 np.array_equal(r.coefficients, o.coefficients)),
+            "device_resident_ms_per_frame": round(float(np.median(td)), 3),
+            "device_kernels_us": kern}
 
 
 def config5_pass(pitt, ctx, threads, reps=5):
@@ -729,6 +844,8 @@ def main():
                                 b.counts, b.capacity) for b in batches]
         line["pcie_fed"] = pcie_pass(pitt, ctxs, host, dev, params, max(3, min(args.steps, 10)))
         log(f"[rank 0] pcie_fed: {line['pcie_fed']}")
+        line["streaming"] = streaming_pass(pitt, ctxs, batches, dev, threads, params, max(20, args.steps))
+        log(f"[rank 0] streaming: {line['streaming']}")
         line["config2"] = config2_pass(pitt, ctx, frames0[0])
         log(f"[rank 0] config2: {line['config2']}")
         line["config5"] = config5_pass(pitt, ctx, threads)
