@@ -588,6 +588,8 @@ def main():
     ap.add_argument("--dump-records", default="",
                     help="rank 0 writes the (gathered) records of batch slot 0's last step to this .npy")
     args = ap.parse_args()
+    # $PITT_GRAPHS=1 (opt-in HIP graphs) needs the runtime's graph packet capture off, before HIP starts
+    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     if args.hw_queues > 0:  # hardware queues per process (one per in-flight context's stream); before HIP init
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 

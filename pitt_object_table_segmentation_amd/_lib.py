@@ -10,6 +10,25 @@ import importlib.util
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _graph_packet_capture_off() -> None:
+    """HIP graphs of the plane path (opt-in, $PITT_GRAPHS=1) need the runtime's graph packet capture off
+    (DESIGN.md s3d): ask for it before the HIP runtime starts.  When torch has already started HIP the
+    variable would no longer reach the runtime, so it is left unset and the library keeps graphs off."""
+    import sys
+    if "DEBUG_CLR_GRAPH_PACKET_CAPTURE" in os.environ:
+        return
+    torch = sys.modules.get("torch")
+    try:
+        started = torch is not None and torch.cuda.is_initialized()
+    except AttributeError:
+        started = False
+    if not started:
+        os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"
+
+
+_graph_packet_capture_off()
 # PITT_LIB_PATH: an alternative build of the same library (A/B experiments, tools/ only)
 LIB_PATH = os.environ.get("PITT_LIB_PATH") or os.path.join(_HERE, "libpitt_seg.so")
 

@@ -55,6 +55,12 @@ inline bool pitt_env_flag(const char* name, bool dflt) {
     return v && *v ? (v[0] != '0') : dflt;
 }
 // A small integer knob from the environment, clamped to [lo, hi].
+// The HIP runtime's graph packet capture is off only when DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 was in the
+// environment when the runtime started (the Python package and bench.py set it before torch starts HIP).
+inline bool graph_packet_capture_off() {
+    const char* v = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
+    return v && v[0] == '0' && v[1] == 0;
+}
 inline int pitt_env_int(const char* name, int dflt, int lo, int hi) {
     const char* v = std::getenv(name);
     const int x = v && *v ? std::atoi(v) : dflt;
@@ -119,11 +125,15 @@ struct pitt_ctx {
     int64_t xrefine_batches = 0, xrefine_fallbacks = 0;  // frames k_xrefine handed back to k_refine
     void* refine_dbg_h = nullptr;
 
-    // HIP graphs of the plane pipeline: a batch's ~20 launches are captured once per (layout,
-    // parameters, arena) and replayed with one hipGraphLaunch -- the host's enqueue cost, not the
-    // GPU, otherwise bounds the pipelined throughput.  $PITT_GRAPHS=0 disables.
-    bool use_graphs = pitt_env_flag("PITT_GRAPHS", true);
-    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 64, 1, 1 << 30);  // smaller batches launch directly
+    // HIP graphs of the plane pipeline (opt-in, $PITT_GRAPHS=1): a batch's ~20 launches captured once per
+    // (layout, parameters, arena) and replayed with one hipGraphLaunch.  Only with the HIP runtime's graph
+    // packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before the runtime starts):
+    // replays through the packet-capture path faulted whenever a replay's kernels met work-list entries
+    // their producers had not yet written -- the path does not keep the captured kernels in stream order
+    // (DESIGN.md s3d).  Direct launches measured the same throughput (profiles/r05_graph_ab.json), so
+    // they are the default.
+    bool use_graphs = pitt_env_flag("PITT_GRAPHS", false) && graph_packet_capture_off();
+    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 1, 1, 1 << 30);  // smaller batches launch directly
     // Adaptive chunk schedule (plane_ransac.hip): a batch launches the scoring chunks that the last
     // batches of its layout needed; a frame still running after them is finished by a continuation.
     // Exact either way; $PITT_ADAPTIVE_CHUNKS=0 always launches the whole schedule.
@@ -173,22 +183,16 @@ struct pitt_ctx {
         std::vector<uint64_t> key;
         hipGraphExec_t exec = nullptr;
         uint64_t last_use = 0;
-        uint64_t epoch = 0;  // direct_epoch when it last ran
     };
-    // Counts the context's direct (non-graph) work: every scratch request outside the plane path, every
-    // direct plane enqueue and continuation.  A graph replays only if none happened since it last ran;
-    // otherwise it is captured afresh ("Graph replays and direct work").
-    uint64_t direct_epoch = 0;
     uint32_t call_seq = 0;  // plane batches enqueued; stamped into each frame's metadata (FrameMeta.pad)
 #ifdef PITT_SYNC_CHECK
-    // debug knobs for the graph-ordering investigation
-    bool dbg_no_epoch = pitt_env_flag("PITT_DBG_NO_EPOCH", false);
+    // debug knob of the graph-ordering investigation
     bool dbg_sync_before_graph = pitt_env_flag("PITT_DBG_SYNC_BEFORE_GRAPH", false);
 #endif
     std::vector<GraphEntry> graphs;
     std::vector<std::vector<uint64_t>> graph_seen;  // keys launched once (captured on a repeat)
     uint64_t graph_clock = 0;
-    int64_t graph_captures = 0, graph_replays = 0, graph_recaptures = 0;
+    int64_t graph_captures = 0, graph_replays = 0;
 
     // profiling
     bool prof = false;

@@ -2446,7 +2446,6 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            pitt_plane_result* results, int32_t* inliers_dev) {
     const int nf = fr->n_frames;
     hipStream_t sm = ctx->stream;
-    const uint64_t epoch0 = ctx->direct_epoch;  // this batch's own scratch requests are not direct work
 #ifdef PITT_SYNC_CHECK
     ctx->check_canaries("plane batch entry");
 #endif
@@ -2773,12 +2772,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     return PITT_OK;
     };
     auto enqueue_front = [&]() -> int { return enqueue(0, K, 1, true, acct_recs, score_recs); };
-    ctx->direct_epoch = epoch0;
 #ifdef PITT_SYNC_CHECK
     *(volatile unsigned int*)dbg_seq = seq;
 #endif
-    // Graphs from ctx->graph_min_frames frames up (64 by default), replayed only while no direct work
-    // ran on the context since the graph last ran ("Graph replays and direct work").
+    // Graphs (opt-in, ctx.hpp: only with the runtime's graph packet capture off) from
+    // ctx->graph_min_frames frames up
     if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
         const double log_prob_k = std::log(1.0 - p->probability);
         uint64_t thb = 0, lpb = 0;
@@ -2793,28 +2791,13 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                                      (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K,
                                      (uint64_t)(xs ? xs_T : 0)};  // the walk's stream stride and grids
         pitt_ctx::GraphEntry* hit = nullptr;
-        bool recapture = false;
         for (auto& g : ctx->graphs)
             if (g.key == key) hit = &g;
-#ifdef PITT_SYNC_CHECK
-        const bool epoch_rule = !ctx->dbg_no_epoch;
-#else
-        const bool epoch_rule = true;
-#endif
-        if (hit && hit->epoch != ctx->direct_epoch && epoch_rule) {
-            // direct work ran on this context since the graph last ran: capture it afresh instead of
-            // replaying (one-frame graphs replayed after the primitive services' launches faulted)
-            (void)hipGraphExecDestroy(hit->exec);
-            ctx->graphs.erase(ctx->graphs.begin() + (hit - ctx->graphs.data()));
-            hit = nullptr;
-            recapture = true;
-            ++ctx->graph_recaptures;
-        }
         if (!hit) {
             // capture on the second sight of a key (a one-off layout, e.g. a support-loop iteration,
             // launches directly: capture and instantiation cost more than one enqueue)
             auto seen = std::find(ctx->graph_seen.begin(), ctx->graph_seen.end(), key);
-            if (seen == ctx->graph_seen.end() && !recapture) {
+            if (seen == ctx->graph_seen.end()) {
                 ctx->graph_seen.push_back(key);
                 if (ctx->graph_seen.size() > 16) ctx->graph_seen.erase(ctx->graph_seen.begin());
             } else {
@@ -2846,7 +2829,6 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         }
         if (hit) {
             hit->last_use = ++ctx->graph_clock;
-            hit->epoch = ctx->direct_epoch;
 #ifdef PITT_SYNC_CHECK
             if (ctx->dbg_sync_before_graph) PITT_HIP_TRY(hipStreamSynchronize(sm));
 #endif
@@ -2873,12 +2855,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         } else {
             const int erc = enqueue_front();
             if (erc) return erc;
-            ++ctx->direct_epoch;
         }
     } else {
         const int erc = enqueue_front();
         if (erc) return erc;
-        ++ctx->direct_epoch;
     }
 #ifdef PITT_SYNC_CHECK
     std::fprintf(stderr, "PITT_SYNC_CHECK call seq %u nf %d n0 %lld K %d/%d xs %d xs_T %lld tiles_max %d gen %llu\n",
@@ -2943,7 +2923,6 @@ int finish_batch(pitt_ctx* ctx) {
         std::function<int(std::vector<int>&, std::vector<int>&)> cont = std::move(ctx->inflight_cont);
         ctx->inflight_cont = nullptr;
         const int rc = cont(ctx->inflight_acct_recs, ctx->inflight_score_recs);
-        ++ctx->direct_epoch;
         if (rc) return rc;
         PITT_HIP_TRY(hipStreamSynchronize(ctx->stream));
         ++ctx->continuations;

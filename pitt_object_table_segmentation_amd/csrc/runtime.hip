@@ -70,7 +70,6 @@ void pitt_ctx::drain() {
 }
 
 void* pitt_ctx::buf(const std::string& name, size_t bytes) {
-    ++direct_epoch;  // scratch for direct work (the plane path restores the count for its own)
     pitt::DevBuf& b = bufs[name];
     if (b.bytes < bytes || !b.p) {
         // work queued on the context's streams may still use the old block: let it drain first
@@ -134,7 +133,6 @@ void pitt_ctx::check_canaries(const char* where) {
 }
 
 void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
-    ++direct_epoch;
     auto& e = host_pinned[name];
     if (e.second < bytes || !e.first) {
         // an async copy queued on the stream may still read or write the old block; cached graphs

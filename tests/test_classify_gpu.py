@@ -166,3 +166,33 @@ def test_batch_time_per_frame(ctx):
     ms = (time.perf_counter() - t0) / 3 * 1e3
     print(f"classify: {ms:.2f} ms per frame of {len(clusters)} clusters")
     assert ms < 1000.0
+
+
+def test_batch_and_services_with_graphs():
+    """The round-4 graph fault's own test (tests/test_classify_gpu.py with one-frame graphs): the same
+    comparison on a context whose plane batches are graphed from one frame up ($PITT_GRAPHS=1,
+    $PITT_GRAPH_MIN_FRAMES=1; the runtime's graph packet capture off, tests/conftest.py)."""
+    import os
+    import torch
+    old = {k: os.environ.get(k) for k in ("PITT_GRAPHS", "PITT_GRAPH_MIN_FRAMES")}
+    os.environ.update({"PITT_GRAPHS": "1", "PITT_GRAPH_MIN_FRAMES": "1"})
+    try:
+        c = pitt.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    s = pitt.Services(c)
+    try:
+        clusters = frame_clusters(0)
+        xyz, offs, cnt = _layout(clusters)
+        d = [torch.from_numpy(np.ascontiguousarray(xyz[:, k])).cuda() for k in range(3)]
+        got = s.classify_clusters(*d, offs, cnt)
+        _check_against_services(c, s, clusters, got)
+        _check_against_services(c, s, clusters, got)  # the services' plane layouts now replay
+        assert c.graph_stats()[1] > 0, c.graph_stats()
+    finally:
+        s.close()
+        c.close()

@@ -1,13 +1,14 @@
-"""HIP-graph replay of the plane pipeline ("HIP graphs" and "Graph replays and direct work").
+"""HIP-graph replay of the plane pipeline (opt-in, $PITT_GRAPHS=1; DESIGN.md s3d, "HIP graphs").
 
 A batch layout seen twice is captured into a graph whose nodes hold device-arena and pinned-host
 addresses (the result / chunk-stat copy nodes write pinned host blocks).  A graph replays only while
-every address it holds is live (any arena or pinned block that moves bumps the arena generation, part
-of the key) and while no direct work ran on its context since it last ran (the direct epoch): a
-one-frame graph replayed after the primitive services' launches on the same stream faulted, in round 3
-and again in round 4 with the floor at one frame, so batches below 64 frames launch directly and a graph
-is captured afresh after direct work.  These tests hold replays, recaptures and direct launches to the
-same bits."""
+every address it holds is live: any arena or pinned block that moves bumps the arena generation, part
+of the key.  Graphs run only with the HIP runtime's graph packet capture off
+(DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, set by tests/conftest.py before HIP starts): replays through the
+packet-capture path faulted in rounds 3 and 4 and in round 5's continuation test, and the same replays
+pass with it off.  These tests hold replays, captures and direct launches to the same bits, including
+the sequences that used to fault (one-frame graphs between the primitive services, cluster sizes
+shrinking under a captured layout)."""
 import os
 
 import numpy as np
@@ -82,7 +83,7 @@ def test_graph_survives_arena_and_pinned_growth():
     bb = pitt.FrameBatch.from_host(big, device="cuda:0")
     inl1 = torch.empty(b1.capacity, dtype=torch.int32, device="cuda:0")
     inlb = torch.empty(bb.capacity, dtype=torch.int32, device="cuda:0")
-    ctx = _ctx(PITT_GRAPHS=1)
+    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1)
     try:
         ref, ref_inl = _run(ctx, b1, inl1)               # first sight: direct
         for _ in range(2):                               # capture, then replay
@@ -119,11 +120,10 @@ def test_graph_survives_arena_and_pinned_growth():
         ctx.close()
 
 
-def test_graph_recaptured_after_service_calls():
-    """Service calls between two batches of a graphed layout are direct work on the context: the next
-    batch captures the graph afresh instead of replaying it, the one after replays, and every result
-    equals a graph-free context's.  The services' one-frame plane batches launch directly (below the
-    64-frame floor) and never capture."""
+def test_graph_replays_after_service_calls():
+    """Service calls between two batches of a graphed layout: the next batch replays its graph (or, when the
+    services' scratch grew and moved the arena, launches as a new key's first sight), and every result equals
+    a graph-free context's; the services' own one-frame plane batches are graphed as well."""
     ctx = _ctx(PITT_GRAPHS=1)
     ref_ctx = _ctx(PITT_GRAPHS=0)
     srv, ref_srv = pitt.Services(ctx), pitt.Services(ref_ctx)
@@ -136,26 +136,49 @@ def test_graph_recaptured_after_service_calls():
             r, i = _run(ctx, b, inl)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl)
         assert ctx.graph_stats() == (1, 2)
-        for k, n in enumerate((300, 1200, 4000)):
+        assert ref_ctx.graph_stats() == (0, 0)
+        for k, n in enumerate((300, 1200, 4000, 1200, 300)):
             cloud = sphere_scene(n, n // 5, 900 + k).astype(np.float32)
-            caps, reps = ctx.graph_stats()
             a = srv.ransac_sphere(cloud)
-            c = srv.ransac_plane(cloud)                    # one frame: direct, no capture
-            assert ctx.graph_stats() == (caps, reps)
+            c = srv.ransac_plane(cloud)
             assert a[0] == ref_srv.ransac_sphere(cloud)[0]
             d = ref_srv.ransac_plane(cloud)
             assert c[0] == d[0] and np.array_equal(c[1], d[1]) and np.array_equal(c[2].view(np.int32), d[2].view(np.int32))
-            # after direct work the old graph never replays: the batch is captured afresh (or, when the
-            # services' scratch grew and moved the arena, launched directly as a new key's first sight)
+            caps, reps = ctx.graph_stats()
             r, i = _run(ctx, b, inl)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
             c1, r1 = ctx.graph_stats()
-            assert c1 - caps == r1 - reps and c1 - caps <= 1, (k, caps, reps, c1, r1)
-            for _ in range(2):                             # nothing in between: capture / replay
-                r, i = _run(ctx, b, inl)
-                assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
-            c2, r2 = ctx.graph_stats()
-            assert c2 == caps + 1 and r2 == r1 + 2, (k, caps, reps, c2, r2)
+            assert (c1, r1) in ((caps, reps + 1), (caps, reps)), (k, caps, reps, c1, r1)
+        assert ctx.graph_stats()[1] > 2
+    finally:
+        srv.close()
+        ref_srv.close()
+        ctx.close()
+        ref_ctx.close()
+
+
+def test_one_frame_graphs_between_primitive_services():
+    """The round-4 fault's sequence (profiles/r04_graph_fault_syncheck.log): the plane service's one-frame
+    layout captured on one cluster, then replayed on clusters of other sizes -- larger and much smaller
+    (1150 -> 1500 -> 340 points) -- with the sphere, cylinder and cone services' launches on the same
+    stream in between.  Every plane response equals a graph-free context's, and the layout did replay."""
+    from test_cone import cone_scene
+    from test_cylinder import cylinder_scene
+    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1)
+    ref_ctx = _ctx(PITT_GRAPHS=0)
+    srv, ref_srv = pitt.Services(ctx), pitt.Services(ref_ctx)
+    try:
+        for k, n in enumerate((1050, 1400, 1150, 1500, 340, 900, 1800, 200)):
+            cloud = sphere_scene(n, n // 4, 500 + k).astype(np.float32)
+            pc, pn = cylinder_scene(max(n, 60), max(n // 5, 10), 600 + k)
+            cc, cn = cone_scene(max(n, 60), max(n // 5, 10), 700 + k, half_deg=30.0)
+            srv.ransac_sphere(cloud)
+            srv.ransac_cylinder(pc.astype(np.float32), pn.astype(np.float32))
+            srv.ransac_cone(cc.astype(np.float32), cn.astype(np.float32))
+            got, want = srv.ransac_plane(cloud), ref_srv.ransac_plane(cloud)
+            assert got[0] == want[0] and np.array_equal(got[1], want[1]), (k, n)
+            assert np.array_equal(got[2].view(np.int32), want[2].view(np.int32)), (k, n)
+        assert ctx.graph_stats()[1] >= 3, ctx.graph_stats()
     finally:
         srv.close()
         ref_srv.close()
