@@ -148,7 +148,9 @@ def test_graph_replays_after_service_calls():
             r, i = _run(ctx, b, inl)
             assert r.tobytes() == ref.tobytes() and np.array_equal(i, ref_inl), k
             c1, r1 = ctx.graph_stats()
-            assert (c1, r1) in ((caps, reps + 1), (caps, reps)), (k, caps, reps, c1, r1)
+            # a replay; or, when the services' scratch grew and moved the arena, the new key's first sight
+            # (direct) or second (captured and launched)
+            assert (c1, r1) in ((caps, reps + 1), (caps, reps), (caps + 1, reps + 1)), (k, caps, reps, c1, r1)
         assert ctx.graph_stats()[1] > 2
     finally:
         srv.close()
@@ -170,8 +172,8 @@ def test_one_frame_graphs_between_primitive_services():
     try:
         for k, n in enumerate((1050, 1400, 1150, 1500, 340, 900, 1800, 200)):
             cloud = sphere_scene(n, n // 4, 500 + k).astype(np.float32)
-            pc, pn = cylinder_scene(max(n, 60), max(n // 5, 10), 600 + k)
-            cc, cn = cone_scene(max(n, 60), max(n // 5, 10), 700 + k, half_deg=30.0)
+            pc, pn = cylinder_scene(max(n, 60), max(n // 5, 10), 600 + k)[:2]
+            cc, cn = cone_scene(max(n, 60), max(n // 5, 10), 700 + k, half_deg=30.0)[:2]
             srv.ransac_sphere(cloud)
             srv.ransac_cylinder(pc.astype(np.float32), pn.astype(np.float32))
             srv.ransac_cone(cc.astype(np.float32), cn.astype(np.float32))

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import pitt_object_table_segmentation_amd as pitt  # noqa: E402
 
 
-def main(reps=5):
+def main(reps=5, dev_only=False):
     import torch
     x, y, z = pitt.synth_fused(1000, 4)
     dx, dy, dz = (torch.from_numpy(a).cuda() for a in (x, y, z))
@@ -28,6 +28,8 @@ def main(reps=5):
                 ts.append((time.perf_counter() - t) * 1e3)
         print(f"config5 device path: {len(n_on)} supports, {len(sizes)} clusters; {np.median(ts):.2f} ms "
               f"(median of {reps})", flush=True)
+        if dev_only:
+            return
         ts = []
         for r in range(reps + 1):
             t = time.perf_counter()
@@ -50,4 +52,4 @@ def main(reps=5):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 5, "--dev-only" in sys.argv)
