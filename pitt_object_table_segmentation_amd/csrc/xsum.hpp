@@ -241,41 +241,58 @@ __global__ __launch_bounds__(256) void k_xs_summ(const float* __restrict__ v, in
     }
 }
 
-// xs_walk: one wave per (segment, stream); lane 0 walks.  out[k * S + s] = the segment's float sum.
+// xs_walk: one wave per (segment, stream).  The walk itself is serial (the sum s is one value), but
+// every summary and element it may need is loaded by the whole wave ahead of time: lane j holds block
+// w0 + j's summary of the current 64-block window while the next window's are in flight, and the walk
+// reads them with v_readlane; a block whose summary fails brings in its 16 sub-block summaries (lanes
+// 0-15), a sub-block that fails its 16 elements (lanes 0-15).  The adds and their order are exactly
+// those of a lane walking element by element.  out[k * S + s] = the segment's float sum.
+__device__ __forceinline__ float xs_lane(float v, int i) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+
 template <int = 0>  // a template: the header is included by several translation units
 __global__ __launch_bounds__(64) void k_xs_walk(const float* __restrict__ v, int64_t T, int S, int64_t nblk,
                                                 int nseg, const XsSeg* __restrict__ seg,
                                                 const XsSum* __restrict__ sblk, const XsSum* __restrict__ ssub,
                                                 float* __restrict__ out) {
     const int k = blockIdx.x % nseg, s = blockIdx.x / nseg;
-    if (threadIdx.x != 0) return;
+    const int lane = threadIdx.x;
     const XsSeg g = seg[k];
-    const float* vs = v + (int64_t)s * T;
-    const XsSum* sb = sblk + (int64_t)s * nblk;
-    const XsSum* ss = ssub + (int64_t)s * nblk * kXsSubs;
-    float acc = 0.0f;
+    const float* vs = v + (int64_t)s * T + g.blk0 * kXsBlk;
+    const XsSum* sb = sblk + (int64_t)s * nblk + g.blk0;
+    const XsSum* ss = ssub + ((int64_t)s * nblk + g.blk0) * kXsSubs;
     const int64_t nb = (g.len + kXsBlk - 1) / kXsBlk;
-    for (int64_t i = 0; i < nb; ++i) {
-        const int64_t b = g.blk0 + i;
-        const XsSum a = sb[b];
-        if (acc >= a.lo && acc <= a.hi) {
-            acc = acc + a.ru;  // exactly (K + R) u
-            continue;
-        }
-        const int64_t base = i * kXsBlk;
-        for (int j = 0; j < kXsSubs; ++j) {
-            const int64_t e0 = base + j * kXsSub;
-            if (e0 >= g.len) break;
-            const XsSum c = ss[b * kXsSubs + j];
-            if (acc >= c.lo && acc <= c.hi) {
-                acc = acc + c.ru;
+    float acc = 0.0f;  // the same value in every lane
+    XsSum cur = lane < nb ? sb[lane] : xs_never();
+    for (int64_t w0 = 0; w0 < nb; w0 += 64) {
+        const int64_t ni = w0 + 64 + lane;
+        const XsSum nxt = ni < nb ? sb[ni] : xs_never();  // the next window, in flight under this one
+        const int cnt = (int)(nb - w0 < 64 ? nb - w0 : 64);
+        for (int i = 0; i < cnt; ++i) {
+            const float lo = xs_lane(cur.lo, i), hi = xs_lane(cur.hi, i);
+            if (acc >= lo && acc <= hi) {
+                acc = acc + xs_lane(cur.ru, i);  // exactly (K + R) u
                 continue;
             }
-            const int64_t e1 = e0 + kXsSub < g.len ? e0 + kXsSub : g.len;
-            for (int64_t t = e0; t < e1; ++t) acc = acc + vs[g.blk0 * kXsBlk + t];
+            const int64_t b = w0 + i, base = b * kXsBlk;
+            const XsSum sub = lane < kXsSubs ? ss[b * kXsSubs + lane] : xs_never();
+            for (int j = 0; j < kXsSubs; ++j) {
+                const int64_t e0 = base + j * kXsSub;
+                if (e0 >= g.len) break;
+                const float clo = xs_lane(sub.lo, j), chi = xs_lane(sub.hi, j);
+                if (acc >= clo && acc <= chi) {
+                    acc = acc + xs_lane(sub.ru, j);
+                    continue;
+                }
+                const int64_t e1 = e0 + kXsSub < g.len ? e0 + kXsSub : g.len;
+                const float ev = lane < e1 - e0 ? vs[e0 + lane] : 0.0f;
+                for (int t = 0; t < (int)(e1 - e0); ++t) acc = acc + xs_lane(ev, t);
+            }
         }
+        cur = nxt;
     }
-    out[(int64_t)k * S + s] = acc;
+    if (lane == 0) out[(int64_t)k * S + s] = acc;
 }
 
 // Scratch of the four launches over S streams of nblk blocks, allocated before any enqueue (a captured
