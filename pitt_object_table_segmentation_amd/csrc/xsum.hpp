@@ -241,58 +241,103 @@ __global__ __launch_bounds__(256) void k_xs_summ(const float* __restrict__ v, in
     }
 }
 
-// xs_walk: one wave per (segment, stream).  The walk itself is serial (the sum s is one value), but
-// every summary and element it may need is loaded by the whole wave ahead of time: lane j holds block
-// w0 + j's summary of the current 64-block window while the next window's are in flight, and the walk
-// reads them with v_readlane; a block whose summary fails brings in its 16 sub-block summaries (lanes
-// 0-15), a sub-block that fails its 16 elements (lanes 0-15).  The adds and their order are exactly
-// those of a lane walking element by element.  out[k * S + s] = the segment's float sum.
+// xs_walk: one 256-thread block per (segment, stream).  The walk itself is serial (the sum s is one
+// value; wave 0 carries it), but nothing it reads comes from memory at its own latency: the segment is
+// staged in windows of kXsWin blocks -- the block summaries, their sub-block summaries and the elements
+// -- into a double-buffered LDS area by all four waves, the next window's loads in flight while wave 0
+// walks the current one.  Per block the walk reads its summary by v_readlane; a block whose summary
+// fails reads its 16 sub-block summaries (lanes 0-15, one LDS read), a sub-block that fails its 16
+// elements.  The adds and their order are exactly those of a lane walking element by element.
+// out[k * S + s] = the segment's float sum.
+constexpr int kXsWin = 32;  // blocks per staged window
+struct XsWalkLds {
+    float4 el[2][kXsWin * kXsBlk / 4];   // elements (32 KB per window)
+    XsSum sub[2][kXsWin * kXsSubs];      // sub-block summaries
+    XsSum blk[2][kXsWin];                // block summaries
+};
+
 __device__ __forceinline__ float xs_lane(float v, int i) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
 }
 
 template <int = 0>  // a template: the header is included by several translation units
-__global__ __launch_bounds__(64) void k_xs_walk(const float* __restrict__ v, int64_t T, int S, int64_t nblk,
-                                                int nseg, const XsSeg* __restrict__ seg,
-                                                const XsSum* __restrict__ sblk, const XsSum* __restrict__ ssub,
-                                                float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_xs_walk(const float* __restrict__ v, int64_t T, int S, int64_t nblk,
+                                                 int nseg, const XsSeg* __restrict__ seg,
+                                                 const XsSum* __restrict__ sblk, const XsSum* __restrict__ ssub,
+                                                 float* __restrict__ out) {
+    __shared__ XsWalkLds L;
     const int k = blockIdx.x % nseg, s = blockIdx.x / nseg;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const XsSeg g = seg[k];
-    const float* vs = v + (int64_t)s * T + g.blk0 * kXsBlk;
+    const float4* vs4 = reinterpret_cast<const float4*>(v + (int64_t)s * T + g.blk0 * kXsBlk);
     const XsSum* sb = sblk + (int64_t)s * nblk + g.blk0;
     const XsSum* ss = ssub + ((int64_t)s * nblk + g.blk0) * kXsSubs;
     const int64_t nb = (g.len + kXsBlk - 1) / kXsBlk;
-    float acc = 0.0f;  // the same value in every lane
-    XsSum cur = lane < nb ? sb[lane] : xs_never();
-    for (int64_t w0 = 0; w0 < nb; w0 += 64) {
-        const int64_t ni = w0 + 64 + lane;
-        const XsSum nxt = ni < nb ? sb[ni] : xs_never();  // the next window, in flight under this one
-        const int cnt = (int)(nb - w0 < 64 ? nb - w0 : 64);
-        for (int i = 0; i < cnt; ++i) {
-            const float lo = xs_lane(cur.lo, i), hi = xs_lane(cur.hi, i);
-            if (acc >= lo && acc <= hi) {
-                acc = acc + xs_lane(cur.ru, i);  // exactly (K + R) u
-                continue;
-            }
-            const int64_t b = w0 + i, base = b * kXsBlk;
-            const XsSum sub = lane < kXsSubs ? ss[b * kXsSubs + lane] : xs_never();
-            for (int j = 0; j < kXsSubs; ++j) {
-                const int64_t e0 = base + j * kXsSub;
-                if (e0 >= g.len) break;
-                const float clo = xs_lane(sub.lo, j), chi = xs_lane(sub.hi, j);
-                if (acc >= clo && acc <= chi) {
-                    acc = acc + xs_lane(sub.ru, j);
+    constexpr int kEl = kXsWin * kXsBlk / 4 / 256, kSub = kXsWin * kXsSubs / 256;  // per thread
+    float4 re[kEl];
+    XsSum rs[kSub], rb;
+    auto load = [&](int64_t w0) {  // window w0 .. w0 + kXsWin into registers (blocks past nb: never read)
+        const int64_t nbw = nb - w0 < kXsWin ? nb - w0 : kXsWin;
+#pragma unroll
+        for (int q = 0; q < kEl; ++q) {
+            const int i = tid + 256 * q;  // float4 index in the window
+            re[q] = i < nbw * (kXsBlk / 4) ? vs4[w0 * (kXsBlk / 4) + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+            const int i = tid + 256 * q;
+            rs[q] = i < nbw * kXsSubs ? ss[w0 * kXsSubs + i] : xs_never();
+        }
+        rb = tid < nbw ? sb[w0 + tid] : xs_never();
+    };
+    auto store = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < kEl; ++q) L.el[slot][tid + 256 * q] = re[q];
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) L.sub[slot][tid + 256 * q] = rs[q];
+        if (tid < kXsWin) L.blk[slot][tid] = rb;
+    };
+    const float* el0 = reinterpret_cast<const float*>(&L.el[0][0]);
+    const float* el1 = reinterpret_cast<const float*>(&L.el[1][0]);
+    float acc = 0.0f;  // wave 0: the same value in every lane
+    if (nb > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int64_t w0 = 0, w = 0; w0 < nb; w0 += kXsWin, ++w) {
+        const int slot = (int)(w & 1);
+        if (w0 + kXsWin < nb) load(w0 + kXsWin);  // in flight while wave 0 walks this window
+        if (tid < 64) {
+            const int cnt = (int)(nb - w0 < kXsWin ? nb - w0 : kXsWin);
+            const XsSum cur = lane < kXsWin ? L.blk[slot][lane] : xs_never();
+            const float* el = slot ? el1 : el0;
+            for (int i = 0; i < cnt; ++i) {
+                const float lo = xs_lane(cur.lo, i), hi = xs_lane(cur.hi, i);
+                if (acc >= lo && acc <= hi) {
+                    acc = acc + xs_lane(cur.ru, i);  // exactly (K + R) u
                     continue;
                 }
-                const int64_t e1 = e0 + kXsSub < g.len ? e0 + kXsSub : g.len;
-                const float ev = lane < e1 - e0 ? vs[e0 + lane] : 0.0f;
-                for (int t = 0; t < (int)(e1 - e0); ++t) acc = acc + xs_lane(ev, t);
+                const int64_t base = (w0 + i) * kXsBlk;  // the block's first element in the segment
+                const XsSum sub = lane < kXsSubs ? L.sub[slot][i * kXsSubs + lane] : xs_never();
+                for (int j = 0; j < kXsSubs; ++j) {
+                    const int64_t e0 = base + j * kXsSub;
+                    if (e0 >= g.len) break;
+                    const float clo = xs_lane(sub.lo, j), chi = xs_lane(sub.hi, j);
+                    if (acc >= clo && acc <= chi) {
+                        acc = acc + xs_lane(sub.ru, j);
+                        continue;
+                    }
+                    const int n_e = (int)(g.len - e0 < kXsSub ? g.len - e0 : kXsSub);
+                    const float ev = lane < n_e ? el[i * kXsBlk + j * kXsSub + lane] : 0.0f;
+                    for (int t = 0; t < n_e; ++t) acc = acc + xs_lane(ev, t);
+                }
             }
         }
-        cur = nxt;
+        if (w0 + kXsWin < nb) store(slot ^ 1);  // the other slot was last read in the previous window
+        __syncthreads();
     }
-    if (lane == 0) out[(int64_t)k * S + s] = acc;
+    if (tid == 0) out[(int64_t)k * S + s] = acc;
 }
 
 // Scratch of the four launches over S streams of nblk blocks, allocated before any enqueue (a captured
@@ -322,7 +367,7 @@ inline void xs_enqueue(hipStream_t st, const float* v, int64_t T, int S, int nse
     hipLaunchKernelGGL(k_xs_scan<>, dim3((unsigned)(nseg * S)), dim3(256), 0, st, nseg, S, nblk, seg, x.dblk, x.eblk);
     hipLaunchKernelGGL(k_xs_summ<>, dim3(waves), dim3(256), 0, st, v, T, S, nblk, seg, blk_seg, x.dsub, x.eblk, x.sblk,
                        x.ssub);
-    hipLaunchKernelGGL(k_xs_walk<>, dim3((unsigned)(nseg * S)), dim3(64), 0, st, v, T, S, nblk, nseg, seg, x.sblk,
+    hipLaunchKernelGGL(k_xs_walk<>, dim3((unsigned)(nseg * S)), dim3(256), 0, st, v, T, S, nblk, nseg, seg, x.sblk,
                        x.ssub, out);
 }
 

@@ -166,11 +166,14 @@ def test_one_frame_graphs_between_primitive_services():
     stream in between.  Every plane response equals a graph-free context's, and the layout did replay."""
     from test_cone import cone_scene
     from test_cylinder import cylinder_scene
-    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1)
-    ref_ctx = _ctx(PITT_GRAPHS=0)
+    # the round-4 conditions: the chain refinement for one-frame batches (the exact walk's stream stride,
+    # which follows the cloud size, would otherwise make every size a layout of its own), and scratch
+    # grown by the largest cloud first, so that the layout's key (arena generation included) repeats
+    ctx = _ctx(PITT_GRAPHS=1, PITT_GRAPH_MIN_FRAMES=1, PITT_XS_MAX_FRAMES=0)
+    ref_ctx = _ctx(PITT_GRAPHS=0, PITT_XS_MAX_FRAMES=0)
     srv, ref_srv = pitt.Services(ctx), pitt.Services(ref_ctx)
     try:
-        for k, n in enumerate((1050, 1400, 1150, 1500, 340, 900, 1800, 200)):
+        for k, n in enumerate((1800, 1050, 1400, 1150, 1500, 340, 900, 1800, 200)):
             cloud = sphere_scene(n, n // 4, 500 + k).astype(np.float32)
             pc, pn = cylinder_scene(max(n, 60), max(n // 5, 10), 600 + k)[:2]
             cc, cn = cone_scene(max(n, 60), max(n // 5, 10), 700 + k, half_deg=30.0)[:2]
