@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <climits>
 #include <cstdint>
 #include <string>
 
@@ -241,14 +242,19 @@ __global__ __launch_bounds__(256) void k_xs_summ(const float* __restrict__ v, in
     }
 }
 
-// xs_walk: one 256-thread block per (segment, stream).  The walk itself is serial (the sum s is one
-// value; wave 0 carries it), but nothing it reads comes from memory at its own latency: the segment is
-// staged in windows of kXsWin blocks -- the block summaries, their sub-block summaries and the elements
-// -- into a double-buffered LDS area by all four waves, the next window's loads in flight while wave 0
-// walks the current one.  Per block the walk reads its summary by v_readlane; a block whose summary
-// fails reads its 16 sub-block summaries (lanes 0-15, one LDS read), a sub-block that fails its 16
-// elements.  The adds and their order are exactly those of a lane walking element by element.
-// out[k * S + s] = the segment's float sum.
+// xs_walk: one 256-thread block per (segment, stream).  The sum s is one value (wave 0 carries it), but
+// the walk does not take one summary at a time.  While s stays in one binade e (s = +-K u, u = 2^(e-23),
+// K the 24-bit significand), a summary (L, H, R u) holds exactly when its binade and sign are s's and K
+// lies in its integer range [klo, khi]; after it K becomes K + R.  So a run of summaries is tested at
+// once: lane j holds summary j, an integer prefix scan of the R's gives every lane the K it would enter
+// with if all before it held, and the first lane whose test fails ends the run (every lane before it
+// held, so s after them is exact: K plus the scan, rebuilt as a float).  Only the failing summary's
+// range is walked below it: a failing block runs the same test over its 16 sub-block summaries, a
+// failing sub-block adds its elements one by one.  Every step is an exact float add of the sequential
+// chain, so the result is the chain's bit for bit.
+// The segment is staged in windows of kXsWin blocks (block summaries, sub-block summaries, elements)
+// into a double-buffered LDS area by all four waves, the next window's loads in flight while wave 0
+// walks the current one.  out[k * S + s] = the segment's float sum.
 constexpr int kXsWin = 32;  // blocks per staged window
 struct XsWalkLds {
     float4 el[2][kXsWin * kXsBlk / 4];   // elements (32 KB per window)
@@ -256,11 +262,71 @@ struct XsWalkLds {
     XsSum blk[2][kXsWin];                // block summaries
 };
 
-__device__ __forceinline__ float xs_lane(float v, int i) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+// a normal float as sign, binade and 24-bit significand (ok: a normal float)
+struct XsK {
+    int e, s, K;
+    bool ok;
+};
+__device__ __forceinline__ XsK xs_k(float a) {
+    const uint32_t b = __float_as_uint(a);
+    const int ef = (int)((b >> 23) & 0xffu);
+    return XsK{ef - 127, (int)(b >> 31), (int)((b & 0x7fffffu) | 0x800000u), ef != 0 && ef != 255};
 }
 
-template <int = 0>  // a template: the header is included by several translation units
+// inclusive prefix sum over the wave's lanes (DPP row shifts, then the row broadcasts)
+__device__ __forceinline__ int xs_scan64(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// One lane's summary in significand units: its binade and sign (es = 2 e + s, or INT_MIN for a summary
+// that never holds), the significand range it holds for, its step R, and the inclusive prefix of the
+// steps over the lanes below n (decoded and scanned once per window or per failing block).
+struct XsLane {
+    int es, kmin, kmax, dk, incl;
+};
+__device__ __forceinline__ XsLane xs_decode(const XsSum& c, int n, int lane) {
+    const XsK l = xs_k(c.lo), h = xs_k(c.hi);
+    const bool valid = lane < n && c.lo <= c.hi && l.ok && h.ok;  // xs_never: lo > hi
+    XsLane d;
+    d.es = valid ? 2 * l.e + l.s : INT_MIN;
+    d.kmin = l.K < h.K ? l.K : h.K;
+    d.kmax = l.K < h.K ? h.K : l.K;
+    d.dk = 0;
+    if (valid) {
+        const int r = (int)ldexpf(c.ru, 23 - l.e);  // R u / u, exact
+        d.dk = l.s ? -r : r;
+    }
+    d.incl = xs_scan64(lane < n ? d.dk : 0);
+    return d;
+}
+
+// The summaries of lanes [i0, n) applied to acc in order, as far as they hold: returns the first lane
+// whose summary does not hold for the value acc has when it is reached (n if all hold), with acc advanced
+// over the lanes before it.  All lanes of the wave call it with the same acc, i0 and n.
+__device__ __forceinline__ int xs_run(float& acc, const XsLane& d, int i0, int n, int lane) {
+    const XsK a = xs_k(acc);
+    const int base = i0 > 0 ? __builtin_amdgcn_readlane(d.incl, i0 - 1) : 0;
+    const int kj = a.K + (d.incl - d.dk - base);  // the significand this lane's summary would see
+    const bool holds = a.ok && d.es == 2 * a.e + a.s && kj >= d.kmin && kj <= d.kmax;
+    const uint64_t fail = __builtin_amdgcn_ballot_w64(lane >= i0 && lane < n && !holds);
+    const int f = fail ? (int)__builtin_ctzll(fail) : n;
+    if (f > i0) {  // lanes [i0, f) held: s = +-(K + their R's) u, inside binade e
+        const int kf = a.K + (__builtin_amdgcn_readlane(d.incl, f - 1) - base);
+        acc = __uint_as_float(((uint32_t)a.s << 31) | ((uint32_t)(a.e + 127) << 23) | ((uint32_t)kf & 0x7fffffu));
+    }
+    return f;
+}
+
+// MODE (tools/wbench only, a measurement): 1 = the staging without the walk, 3 = the exact walk with
+// wave 0's cycles per phase written after the sums (out[nseg S + 4 s + k]: runs, failing blocks, staging
+// and barriers); the library uses 0.
+template <int MODE = 0>  // a template: the header is included by several translation units
 __global__ __launch_bounds__(256) void k_xs_walk(const float* __restrict__ v, int64_t T, int S, int64_t nblk,
                                                  int nseg, const XsSeg* __restrict__ seg,
                                                  const XsSum* __restrict__ sblk, const XsSum* __restrict__ ssub,
@@ -297,9 +363,8 @@ __global__ __launch_bounds__(256) void k_xs_walk(const float* __restrict__ v, in
         for (int q = 0; q < kSub; ++q) L.sub[slot][tid + 256 * q] = rs[q];
         if (tid < kXsWin) L.blk[slot][tid] = rb;
     };
-    const float* el0 = reinterpret_cast<const float*>(&L.el[0][0]);
-    const float* el1 = reinterpret_cast<const float*>(&L.el[1][0]);
     float acc = 0.0f;  // wave 0: the same value in every lane
+    long long cyc_run = 0, cyc_fail = 0, cyc_stage = 0, t_mark = MODE == 3 ? clock64() : 0;
     if (nb > 0) {
         load(0);
         store(0);
@@ -308,36 +373,69 @@ __global__ __launch_bounds__(256) void k_xs_walk(const float* __restrict__ v, in
     for (int64_t w0 = 0, w = 0; w0 < nb; w0 += kXsWin, ++w) {
         const int slot = (int)(w & 1);
         if (w0 + kXsWin < nb) load(w0 + kXsWin);  // in flight while wave 0 walks this window
-        if (tid < 64) {
+        if (MODE == 3) {
+            const long long t = clock64();
+            cyc_stage += t - t_mark;
+            t_mark = t;
+        }
+        if (tid < 64 && MODE != 1) {
+            // every loop bound and index below is wave-uniform (a ballot's first bit, a readlane): scalar
+            // control flow; indices are window-local 32-bit
             const int cnt = (int)(nb - w0 < kXsWin ? nb - w0 : kXsWin);
-            const XsSum cur = lane < kXsWin ? L.blk[slot][lane] : xs_never();
-            const float* el = slot ? el1 : el0;
-            for (int i = 0; i < cnt; ++i) {
-                const float lo = xs_lane(cur.lo, i), hi = xs_lane(cur.hi, i);
-                if (acc >= lo && acc <= hi) {
-                    acc = acc + xs_lane(cur.ru, i);  // exactly (K + R) u
-                    continue;
+            const int rem = (int)(g.len - w0 * kXsBlk < (int64_t)kXsWin * kXsBlk ? g.len - w0 * kXsBlk
+                                                                                 : (int64_t)kXsWin * kXsBlk);
+            const XsLane cur = xs_decode(lane < kXsWin ? L.blk[slot][lane] : xs_never(), cnt, lane);
+            const float* el = reinterpret_cast<const float*>(&L.el[slot][0]);
+            int i = 0;
+            while (i < cnt) {
+                const int f = xs_run(acc, cur, i, cnt, lane);
+                if (f >= cnt) break;
+                long long tf = 0;
+                if (MODE == 3) {
+                    tf = clock64();
+                    cyc_run += tf - t_mark;
                 }
-                const int64_t base = (w0 + i) * kXsBlk;  // the block's first element in the segment
-                const XsSum sub = lane < kXsSubs ? L.sub[slot][i * kXsSubs + lane] : xs_never();
-                for (int j = 0; j < kXsSubs; ++j) {
-                    const int64_t e0 = base + j * kXsSub;
-                    if (e0 >= g.len) break;
-                    const float clo = xs_lane(sub.lo, j), chi = xs_lane(sub.hi, j);
-                    if (acc >= clo && acc <= chi) {
-                        acc = acc + xs_lane(sub.ru, j);
-                        continue;
-                    }
-                    const int n_e = (int)(g.len - e0 < kXsSub ? g.len - e0 : kXsSub);
-                    const float ev = lane < n_e ? el[i * kXsBlk + j * kXsSub + lane] : 0.0f;
-                    for (int t = 0; t < n_e; ++t) acc = acc + xs_lane(ev, t);
+                // block f does not hold: its sub-blocks (those that hold elements of the segment)
+                const int nsub = rem - f * kXsBlk >= kXsBlk ? kXsSubs : (rem - f * kXsBlk + kXsSub - 1) / kXsSub;
+                const XsLane sub = xs_decode(lane < kXsSubs ? L.sub[slot][f * kXsSubs + lane] : xs_never(), nsub, lane);
+                int j = 0;
+                while (j < nsub) {
+                    const int q = xs_run(acc, sub, j, nsub, lane);
+                    if (q >= nsub) break;
+                    // sub-block q does not hold: its elements, in order (one broadcast read of all 16)
+                    const int e0 = f * kXsBlk + q * kXsSub;
+                    const int n_e = rem - e0 < kXsSub ? rem - e0 : kXsSub;
+                    const float4* p = reinterpret_cast<const float4*>(el + e0);
+                    const float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+                    const float ev[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                          a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+                    for (int t = 0; t < kXsSub; ++t)
+                        if (t < n_e) acc = acc + ev[t];
+                    j = q + 1;
                 }
+                if (MODE == 3) {
+                    t_mark = clock64();
+                    cyc_fail += t_mark - tf;
+                }
+                i = f + 1;
+            }
+            if (MODE == 3) {
+                const long long t = clock64();
+                cyc_run += t - t_mark;
+                t_mark = t;
             }
         }
         if (w0 + kXsWin < nb) store(slot ^ 1);  // the other slot was last read in the previous window
         __syncthreads();
     }
     if (tid == 0) out[(int64_t)k * S + s] = acc;
+    if (MODE == 3 && tid == 0) {
+        cyc_stage += clock64() - t_mark;
+        out[(int64_t)nseg * S + 4 * s] = (float)cyc_run;
+        out[(int64_t)nseg * S + 4 * s + 1] = (float)cyc_fail;
+        out[(int64_t)nseg * S + 4 * s + 2] = (float)cyc_stage;
+    }
 }
 
 // Scratch of the four launches over S streams of nblk blocks, allocated before any enqueue (a captured
