@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -239,8 +240,10 @@ __global__ void k_cell_iota(int32_t* __restrict__ parent, const int32_t* __restr
 
 // One wave per cell: against each of the 62 cells after it in the 5x5x5 neighbourhood (the other 62
 // see it from their side), unless the two are already joined, look for one point pair closer than
-// the radius (PCL's float order) -- lanes hold the cell's points, the neighbour's points are walked
-// one by one -- and join the cells at the first such pair.
+// the radius (PCL's float order) and join the cells at the first such pair.  The 62 neighbours are
+// looked up at once (lane o probes offset o); per neighbour its points are loaded 64 at a time (lane q
+// holds point q) and walked by v_readlane against the cell's points (one per lane, loaded once per
+// cell), eight at a time between ballots: no load waits inside the pair loop.
 __global__ __launch_bounds__(256) void k_cell_union(Grid g, const int32_t* __restrict__ ncells,
                                                     const uint64_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
                                                     const int32_t* __restrict__ cpts, float r2,
@@ -248,53 +251,112 @@ __global__ __launch_bounds__(256) void k_cell_union(Grid g, const int32_t* __res
     const int nc = *ncells;
     const int lane = threadIdx.x & 63;
     const int nw = gridDim.x * 4;
+    const float qnan = __builtin_nanf("");
     for (int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6))); c < nc; c += nw) {
         const uint64_t key = ckey[c];
         const int64_t cx = (int64_t)(key & 0x1FFFFF), cy = (int64_t)((key >> 21) & 0x1FFFFF), cz = (int64_t)(key >> 42);
         const int b0 = cstart[c], e0 = cstart[c + 1];
-        for (int o = 63; o < 125; ++o) {  // offsets after (0, 0, 0) in this order; the rest is the neighbours' half
+        // the neighbours: lane o < 62 probes offset 63 + o (the offsets after (0, 0, 0))
+        int32_t d = -1;
+        if (lane < 62) {
+            const int o = 63 + lane;
             const int dx = o / 25 - 2, dy = (o / 5) % 5 - 2, dz = o % 5 - 2;
-            if (cx + dx < 0 || cy + dy < 0 || cz + dz < 0) continue;
-            const int32_t h = hash_find(g, cell_key(cx + dx, cy + dy, cz + dz));
-            if (h < 0) continue;
-            const int32_t d = g.hcid[h];
-            if (uf_find(parent, c) == uf_find(parent, d)) continue;
-            const int b1 = cstart[d], e1 = cstart[d + 1];
+            if (cx + dx >= 0 && cy + dy >= 0 && cz + dz >= 0) {
+                const int32_t h = hash_find(g, cell_key(cx + dx, cy + dy, cz + dz));
+                if (h >= 0) d = g.hcid[h];
+            }
+        }
+        uint64_t cand = __builtin_amdgcn_ballot_w64(d >= 0);
+        if (!cand) continue;
+        // the cell's first 64 points, one per lane (NaN past its end: never closer than the radius)
+        float cx0 = qnan, cy0 = qnan, cz0 = qnan;
+        if (b0 + lane < e0) {
+            const int32_t i = cpts[b0 + lane];
+            cx0 = g.x[i];
+            cy0 = g.y[i];
+            cz0 = g.z[i];
+        }
+        while (cand) {
+            const int t = (int)__builtin_ctzll(cand);
+            cand &= cand - 1;
+            const int32_t dn = __builtin_amdgcn_readlane(d, t);
+            if (uf_find(parent, c) == uf_find(parent, dn)) continue;
+            const int b1 = cstart[dn], e1 = cstart[dn + 1];
             bool hit = false;
-            for (int p0 = b0; p0 < e0 && !hit; p0 += 64) {
-                const int pk = p0 + lane;
-                float px = __builtin_nanf(""), py = px, pz = px;
-                if (pk < e0) {
-                    const int32_t i = cpts[pk];
-                    px = g.x[i];
-                    py = g.y[i];
-                    pz = g.z[i];
+            for (int q0 = b1; q0 < e1 && !hit; q0 += 64) {
+                float qx = qnan, qy = qnan, qz = qnan;
+                if (q0 + lane < e1) {
+                    const int32_t j = cpts[q0 + lane];
+                    qx = g.x[j];
+                    qy = g.y[j];
+                    qz = g.z[j];
                 }
-                for (int q = b1; q < e1; ++q) {
-                    const int32_t j = __builtin_amdgcn_readfirstlane(cpts[q]);
-                    const float ex = px - g.x[j], ey = py - g.y[j], ez = pz - g.z[j];
-                    const float dd = ex * ex + ey * ey + ez * ez;  // FLANN L2_Simple order
-                    if (__builtin_amdgcn_ballot_w64(dd < r2)) {
-                        hit = true;
-                        break;
+                const int nq = __builtin_amdgcn_readfirstlane(e1 - q0 < 64 ? e1 - q0 : 64);
+                for (int p0 = b0; p0 < e0 && !hit; p0 += 64) {
+                    float px = cx0, py = cy0, pz = cz0;
+                    if (p0 != b0) {  // cells of more than 64 points: the next 64
+                        px = py = pz = qnan;
+                        if (p0 + lane < e0) {
+                            const int32_t i = cpts[p0 + lane];
+                            px = g.x[i];
+                            py = g.y[i];
+                            pz = g.z[i];
+                        }
+                    }
+                    for (int u0 = 0; u0 < nq && !hit; u0 += 8) {
+                        bool any = false;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const int tt = u0 + u < nq ? u0 + u : nq - 1;  // a repeated pair changes nothing
+                            const float bx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), tt));
+                            const float by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), tt));
+                            const float bz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), tt));
+                            const float ex = px - bx, ey = py - by, ez = pz - bz;
+                            const float dd = ex * ex + ey * ey + ez * ez;  // FLANN L2_Simple order
+                            any = any || dd < r2;
+                        }
+                        hit = __builtin_amdgcn_ballot_w64(any) != 0;
                     }
                 }
             }
-            if (hit && lane == 0) uf_union(parent, c, d);
+            if (hit && lane == 0) uf_union(parent, c, dn);
         }
     }
 }
 
-// Components: per cell its root; per root the size (sum of its cells' counts) and the seed (the
-// smallest point index -- PCL's BFS discovers components in ascending seed order).
+// Per cell: its points added to its root's size, its smallest index folded into the root's seed.  Cells
+// of one wave that share a root (a large component: most of them) are reduced in the wave first, so a
+// root takes one atomic per wave instead of one per cell.
 __global__ void k_cell_roots(int32_t* __restrict__ parent, const int32_t* __restrict__ ncells,
                              const int32_t* __restrict__ ccnt, const int32_t* __restrict__ cmin,
                              int32_t* __restrict__ csize, int32_t* __restrict__ cseed) {
     const int nc = *ncells;
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += gridDim.x * blockDim.x) {
-        const int32_t r = uf_find(parent, c);
-        atomicAdd(&csize[r], ccnt[c]);
-        atomicMin(&cseed[r], cmin[c]);
+    const int lane = threadIdx.x & 63;
+    for (int base = blockIdx.x * blockDim.x; base < nc; base += gridDim.x * blockDim.x) {  // uniform per wave
+        const int c = base + (int)threadIdx.x;
+        int32_t r = -1, cnt = 0, mn = INT_MAX;
+        if (c < nc) {
+            r = uf_find(parent, c);
+            cnt = ccnt[c];
+            mn = cmin[c];
+        }
+        uint64_t pend = __builtin_amdgcn_ballot_w64(c < nc);
+        while (pend) {
+            const int32_t r0 = __builtin_amdgcn_readlane(r, (int)__builtin_ctzll(pend));
+            const bool mine = ((pend >> lane) & 1u) && r == r0;
+            int sv = mine ? cnt : 0, mv = mine ? mn : INT_MAX;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                sv += __shfl_xor(sv, off, 64);
+                const int o = __shfl_xor(mv, off, 64);
+                mv = o < mv ? o : mv;
+            }
+            if (lane == 0) {
+                atomicAdd(&csize[r0], sv);
+                atomicMin(&cseed[r0], mv);
+            }
+            pend &= ~__builtin_amdgcn_ballot_w64(mine);
+        }
     }
 }
 

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=${1:-walk}
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_xsum_gpu.py tests/test_golden.py tests/test_supports_clusters_gpu.py -m gpu -x -v \
+timeout -k 10 300 python -u -m pytest tests/test_xsum_gpu.py tests/test_golden.py tests/test_supports_clusters_gpu.py tests/test_independent.py tests/test_services_gpu.py -m gpu -x -v \
     --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
 cd /tmp && export TMPDIR=/tmp
