@@ -29,6 +29,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdint>
 #include <string>
@@ -661,8 +662,15 @@ __device__ __forceinline__ void elm_eval(const ElmJob& j, const typename F::Pre&
     }
 }
 
+// The workspace ((N + 2) m floats: the Jacobian, f(x) and the trial residuals) lives in LDS when the
+// batch's largest job fits (lds != 0: the launch's dynamic LDS holds it), else in HBM (ElmJob::work).
+// Every m-long serial chain of the LM reads it: from LDS a chain step waits ~100 cycles for its operand,
+// from L2/HBM several hundred.
+extern __shared__ float elm_dyn[];
+constexpr size_t kElmLdsMax = 144 * 1024;  // dynamic LDS budget per block (of the CU's 160 KB)
+
 template <class F>
-__global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ jobs) {
+__global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ jobs, int lds) {
     constexpr int N = F::N;
     __shared__ ElmShared<F> s;
     __shared__ float red[kElmThreads / 64];
@@ -676,7 +684,7 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
         }
         return;
     }
-    float* fjac = j.work;
+    float* fjac = lds ? elm_dyn : j.work;
     float* rbuf[2] = {j.work + (int64_t)N * m, j.work + (int64_t)(N + 1) * m};
     constexpr float factor = 100.0f;
     const float ftol = sqrtf(FLT_EPSILON), xtol = sqrtf(FLT_EPSILON), gtol = 0.0f, eps = FLT_EPSILON;
@@ -860,7 +868,21 @@ template <class F>
 inline int launch_elm_batch(pitt_ctx* ctx, hipStream_t s, std::vector<ElmJob>& jobs, const char* name) {
     if (jobs.empty()) return PITT_OK;
     size_t words = 0;
-    for (const ElmJob& jb : jobs) words += (size_t)(F::N + 2) * (size_t)jb.m + 64;
+    int64_t m_max = 0;
+    for (const ElmJob& jb : jobs) {
+        words += (size_t)(F::N + 2) * (size_t)jb.m + 64;
+        m_max = std::max<int64_t>(m_max, jb.m);
+    }
+    const size_t lds_bytes = (size_t)(F::N + 2) * (size_t)m_max * sizeof(float);
+    const int lds = lds_bytes <= kElmLdsMax ? 1 : 0;
+    if (lds) {
+        static bool attr_set = false;  // once per kernel instantiation (one per model kind)
+        if (!attr_set) {
+            PITT_HIP_TRY(hipFuncSetAttribute((const void*)k_elm<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)kElmLdsMax));
+            attr_set = true;
+        }
+    }
     float* work = (float*)ctx->buf(std::string(name) + "_elm_work", words * 4);
     const size_t bytes = jobs.size() * sizeof(ElmJob);
     auto* h = (ElmJob*)ctx->pinned(std::string(name) + "_elm_jobs_h", bytes);
@@ -873,7 +895,7 @@ inline int launch_elm_batch(pitt_ctx* ctx, hipStream_t s, std::vector<ElmJob>& j
     }
     std::copy(jobs.begin(), jobs.end(), h);
     PITT_HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_elm<F>, dim3((unsigned)jobs.size()), dim3(kElmThreads), 0, s, d);
+    hipLaunchKernelGGL(k_elm<F>, dim3((unsigned)jobs.size()), dim3(kElmThreads), lds ? lds_bytes : 0, s, d, lds);
     PITT_HIP_TRY(hipGetLastError());
 #ifdef PITT_SYNC_CHECK
     ctx->check_canaries(name);
