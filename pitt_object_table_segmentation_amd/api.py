@@ -219,7 +219,7 @@ class Context:
         nc = ctypes.c_int32()
         rc = self._check(lib.pitt_plane_segment(self.h, _fp(cloud), n, stride, ctypes.byref(p), _ip(inl),
                                                 ctypes.byref(ni), _fp(co), ctypes.byref(nc)), "pitt_plane_segment")
-        return PlaneModel(inl[:ni.value].copy(), co[:nc.value].copy(), rc)
+        return PlaneModel(inl[:ni.value], co[:nc.value].copy(), rc)
 
     def plane_segment_batch(self, batch: FrameBatch, params: Optional[L.SacParams] = None,
                             inliers_out=None) -> np.ndarray:

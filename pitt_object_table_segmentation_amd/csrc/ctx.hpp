@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <chrono>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -23,6 +24,10 @@
     } while (0)
 
 namespace pitt {
+
+inline double wall_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // One growable device buffer.
 struct DevBuf {
@@ -141,16 +146,24 @@ struct pitt_ctx {
     // batches of up to this many frames refine through the chip-wide exact walk (xsum.hpp) instead of
     // k_refine's per-frame chain (same sums, lower latency); $PITT_XS_MAX_FRAMES=0 keeps the chain always
     int xs_max_frames = pitt_env_int("PITT_XS_MAX_FRAMES", 8, 0, 1 << 30);
+    // pitt_plane_segment: points converted (AoS -> SoA) per staged H2D copy; 0 = one copy of the cloud.
+    // $PITT_HOST_TIMING=1 prints its host phases to stderr.
+    int64_t single_chunk = pitt_env_int("PITT_SINGLE_CHUNK", 1 << 16, 0, 1 << 30);
+    bool host_timing = pitt_env_flag("PITT_HOST_TIMING", false);
     struct ChunkHint {
         std::array<uint64_t, 4> key;  // frame planes, frames, hypothesis cap, tiles
-        int need[4];                  // chunks with active frames in the last batches (0: none yet)
+        int need[16];                 // chunks with active frames in the last batches (0: none yet)
         int pos;
         uint64_t last_use;
     };
     std::vector<ChunkHint> chunk_hints;
     uint64_t hint_clock = 0;
     int64_t continuations = 0;        // batches that ran past their scheduled chunks
-    // chunks to launch for a layout: the most the last four batches needed (all of them when unknown)
+    // chunks to launch for a layout: the most the last sixteen batches needed (all of them when unknown).
+    // A long window: a continuation re-runs the decision / refinement / selection launches for the frames
+    // it finishes, which costs about one refinement latency (~0.7 ms on the table batch), while a
+    // scoring chunk with no active frame costs ~10 us -- a layout that needed more chunks once in a
+    // while keeps launching them (bench.py streaming: a cluttered batch in every five).
     int chunk_hint(const std::array<uint64_t, 4>& key, int all) {
         for (ChunkHint& h : chunk_hints)
             if (h.key == key) {
@@ -172,11 +185,11 @@ struct pitt_ctx {
                     if (chunk_hints[i].last_use < chunk_hints[lru].last_use) lru = i;
                 chunk_hints.erase(chunk_hints.begin() + (long)lru);
             }
-            chunk_hints.push_back(ChunkHint{key, {0, 0, 0, 0}, 0, ++hint_clock});
+            chunk_hints.push_back(ChunkHint{key, {}, 0, ++hint_clock});
             h = &chunk_hints.back();
         }
         h->need[h->pos] = need;
-        h->pos = (h->pos + 1) & 3;
+        h->pos = (h->pos + 1) & 15;
     }
     uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
     struct GraphEntry {

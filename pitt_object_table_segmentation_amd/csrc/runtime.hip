@@ -57,6 +57,19 @@ float float_threshold(double th) {
     if ((double)f < th) f = std::nextafter(f, INFINITY);
     return f;
 }
+
+// pitt_plane_segment's staging layout -> the frame's planes: chunk c of C points arrives as
+// [x(C) y(C) z(C)] (one H2D copy per chunk); point i of the cloud lands at x[i], y[i], z[i].
+__global__ __launch_bounds__(256) void k_single_planes(const float* __restrict__ stage, int64_t n, int64_t C,
+                                                       int64_t cap, float* __restrict__ d) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = i / C, j = i - c * C, b = c * 3 * C + j;
+        const int64_t m = std::min(C, n - c * C);  // the last chunk is packed to its own length
+        d[i] = stage[b];
+        d[cap + i] = stage[b + m];
+        d[2 * cap + i] = stage[b + 2 * m];
+    }
+}
 }  // namespace pitt
 
 #ifdef PITT_SYNC_CHECK
@@ -373,18 +386,52 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     *n_coeff = 0;
     const int64_t cap = std::max<int64_t>(PITT_TILE_POINTS,
                                           (n + PITT_TILE_POINTS - 1) / PITT_TILE_POINTS * PITT_TILE_POINTS);
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    if (int rc = pitt::finish_batch(ctx)) return rc;  // a batch in flight completes first
+    const int64_t C = ctx->single_chunk > 0 ? std::min<int64_t>(ctx->single_chunk, std::max<int64_t>(n, 1))
+                                            : std::max<int64_t>(n, 1);
     float* h = (float*)ctx->pinned("single_h", (size_t)cap * 3 * sizeof(float));
-    if (!h) return ctx->fail(PITT_E_NOMEM, "pinned allocation failed");
-    const int sf = stride_bytes / 4;
-    for (int64_t i = 0; i < n; ++i) {
-        h[i] = xyz[i * sf];
-        h[cap + i] = xyz[i * sf + 1];
-        h[2 * cap + i] = xyz[i * sf + 2];
-    }
+    int32_t* hi = (int32_t*)ctx->pinned("single_hinl", (size_t)cap * sizeof(int32_t));
+    if (!h || !hi) return ctx->fail(PITT_E_NOMEM, "pinned allocation failed");
     float* d = (float*)ctx->buf("single_xyz", (size_t)cap * 3 * sizeof(float));
+    float* ds = (float*)ctx->buf("single_stage", (size_t)cap * 3 * sizeof(float));
     int32_t* di = (int32_t*)ctx->buf("single_inl", (size_t)cap * sizeof(int32_t));
-    if (!d || !di) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
-    PITT_HIP_TRY(hipMemcpyAsync(d, h, (size_t)cap * 3 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    if (!d || !ds || !di) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    // The cloud goes up in chunks of C points, each deinterleaved on the host into [x y z] runs of the
+    // pinned staging buffer and sent by ONE copy as soon as it is ready, so the DMA of chunk k runs under
+    // the deinterleave of chunk k+1; k_single_planes then lays the chunks out as the frame's planes.
+    const bool timing = ctx->host_timing;
+    const double t0 = timing ? pitt::wall_ms() : 0.0;
+    const int sf = stride_bytes / 4;
+    for (int64_t b = 0; b < n; b += C) {
+        const int64_t m = std::min(C, n - b);
+        float* hx = h + 3 * b;  // chunk b / C starts at 3 b (every earlier chunk is full)
+        float *hy = hx + m, *hz = hx + 2 * m;
+        const float* src = xyz + b * sf;
+        if (sf == 4) {
+            for (int64_t i = 0; i < m; ++i) {
+                float q[4];
+                std::memcpy(q, src + 4 * i, sizeof q);
+                hx[i] = q[0];
+                hy[i] = q[1];
+                hz[i] = q[2];
+            }
+        } else {
+            for (int64_t i = 0; i < m; ++i) {
+                hx[i] = src[3 * i];
+                hy[i] = src[3 * i + 1];
+                hz[i] = src[3 * i + 2];
+            }
+        }
+        PITT_HIP_TRY(hipMemcpyAsync(ds + 3 * b, hx, (size_t)(3 * m) * sizeof(float), hipMemcpyHostToDevice,
+                                    ctx->stream));
+    }
+    if (n > 0) {
+        hipLaunchKernelGGL(pitt::k_single_planes, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256),
+                           0, ctx->stream, ds, n, C, cap, d);
+        PITT_HIP_TRY(hipGetLastError());
+    }
+    const double t1 = timing ? pitt::wall_ms() : 0.0;
     int64_t off = 0;
     pitt_frames fr;
     fr.x = d;
@@ -395,12 +442,25 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     fr.n_frames = 1;
     fr.capacity = cap;
     pitt_plane_result r;
-    int rc = pitt_plane_segment_batch(ctx, &fr, p, &r, di);
+    int rc = pitt_plane_segment_batch_async(ctx, &fr, p, &r, di);
     if (rc < 0) return rc;
+    // the inlier list comes back with the batch: a copy of the whole list buffer into pinned memory
+    // enqueued behind it (a continuation would enqueue more work after this copy: then copy again)
+    const int64_t cont0 = ctx->continuations;
+    if (inliers_out && n > 0) PITT_HIP_TRY(hipMemcpyAsync(hi, di, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    rc = pitt_wait(ctx);
+    if (rc < 0) return rc;
+    const double t2 = timing ? pitt::wall_ms() : 0.0;
     if (r.status < 0) return ctx->fail(r.status, "plane segmentation failed");
     if (r.n_coeff == 0) return PITT_NO_MODEL;
-    if (inliers_out && r.n_inliers > 0)
-        PITT_HIP_TRY(hipMemcpy(inliers_out, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (inliers_out && r.n_inliers > 0) {
+        if (ctx->continuations != cont0)
+            PITT_HIP_TRY(hipMemcpy(hi, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
+        std::memcpy(inliers_out, hi, (size_t)r.n_inliers * sizeof(int32_t));
+    }
+    if (timing)
+        std::fprintf(stderr, "pitt_plane_segment n=%lld: convert+enqueue %.3f ms, batch+inliers D2H %.3f ms, copy out %.3f ms\n",
+                     (long long)n, t1 - t0, t2 - t1, pitt::wall_ms() - t2);
     *n_inliers = r.n_inliers;
     *n_coeff = 4;
     if (coeff_out) std::memcpy(coeff_out, r.coefficients, 4 * sizeof(float));

@@ -95,3 +95,31 @@ def test_profiled_short_schedule_has_no_empty_launches():
         P._check(ctx, frames, res, _lists(b, res, inl))
     finally:
         ctx.close()
+
+
+def test_single_cloud_continuation_copies_the_finished_inliers():
+    """pitt_plane_segment copies the inlier list back behind the batch; when the batch needs a
+    continuation (a clutter cloud after the single-cloud layout learnt the table's short schedule) the
+    list is copied again after it.  Bit-equal to a context that launches every chunk."""
+    w, h = 640, 480
+
+    def cloud(scene, seed):
+        x, y, z = pitt.synth_frame(scene, seed, w, h)
+        return np.stack([x, y, z, np.ones_like(x)], 1).astype(np.float32)
+
+    ctx = _ctx()
+    full = _ctx(PITT_ADAPTIVE_CHUNKS=0)
+    try:
+        for i in range(3):
+            ctx.plane_segment(cloud(pitt.SCENE_TABLE, 8300 + i))
+        cont0, k_table = ctx.schedule_stats()
+        assert k_table < 7, k_table
+        c = cloud(pitt.SCENE_CLUTTER, 8310)
+        got = ctx.plane_segment(c)
+        assert ctx.schedule_stats()[0] == cont0 + 1
+        ref = full.plane_segment(c)
+        assert np.array_equal(got.inliers, ref.inliers) and got.coefficients.tobytes() == ref.coefficients.tobytes()
+        assert len(got.inliers) > 0
+    finally:
+        ctx.close()
+        full.close()
