@@ -197,26 +197,71 @@ __device__ float elm_stable1(const float* v, int n) {
     return scale * sqrtf(ssq);
 }
 
-// ---- wave-level chains (wave 0 of the block; every lane of the wave calls them) --------------------
+// ---- wave-level chains (every lane of the calling wave calls them) ----------------------------------
+// a + g(i) + g(i + S) + ... over i < end, in that order (one dependent add per element).  Eight elements
+// per step, the next step's eight loads issued before this step's adds, so the adds cover the LDS latency.
+// 32-bit indices (m < 2^31): 64-bit compares and address arithmetic would double the loop's issue cost.
+template <int S, class G>
+__device__ __forceinline__ float elm_chain(int i, int end, float a, G g) {
+    constexpr int U = 8;
+    if (i + (U - 1) * S < end) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = g(i + u * S);
+        for (i += U * S; i + (U - 1) * S < end; i += U * S) {
+            float w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = g(i + u * S);
+#pragma unroll
+            for (int u = 0; u < U; ++u) a = a + v[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = w[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) a = a + v[u];
+    }
+    for (; i < end; i += S) a = a + g(i);
+    return a;
+}
+
+// Eigen's redux (elm_redux_wave below) of up to eight sums at once: lanes 8 q .. 8 q + 7 run sum q's
+// eight packet-lane chains over its own sz elements g(i) (sz = 0: no sum), and lane 8 q returns it.
+template <class G>
+__device__ __forceinline__ float elm_redux_wave8(int64_t size, G g, int lane) {
+    const int sz = (int)size;
+    const int l = lane & 7, base = lane & ~7;
+    const int asz2 = (sz / 8) * 8, asz = (sz / 4) * 4;
+    float acc = 0.0f;
+    if (asz > 4) acc = elm_chain<8>(8 + l, asz2, g(l), g);
+    else if (asz == 4 && l < 4) acc = g(l);
+    const float p1 = __shfl(acc, base + ((l + 4) & 7), 64);
+    if (asz > 4 && l < 4) {
+        acc = acc + p1;
+        if (asz > asz2) acc = acc + g(asz2 + l);
+    }
+    const float a0 = __shfl(acc, base, 64), a1 = __shfl(acc, base + 1, 64), a2 = __shfl(acc, base + 2, 64),
+                a3 = __shfl(acc, base + 3, 64);
+    float res = 0.0f;
+    if (l == 0) {
+        if (asz) {
+            res = (a0 + a2) + (a1 + a3);
+            for (int i = asz; i < sz; ++i) res = res + g(i);
+        } else if (sz > 0) {
+            res = elm_chain<1>(1, sz, g(0), g);
+        }
+    }
+    return res;
+}
+
+// ---- the single-sum form (wave 0 of the block; every lane of the wave calls it) ---------------------
 // Eigen's redux over g(0 .. size-1): lanes 0-7 run the two packets' 8 lane chains; the sum on lane 0.
 template <class G>
-__device__ float elm_redux_wave(int64_t size, G g, int lane) {
-    const int64_t asz2 = (size / 8) * 8, asz = (size / 4) * 4;
+__device__ __forceinline__ float elm_redux_wave(int64_t size64, G g, int lane) {
+    const int size = (int)size64;
+    const int asz2 = (size / 8) * 8, asz = (size / 4) * 4;
     float acc = 0.0f;
     if (asz > 4) {
-        if (lane < 8) {
-            float a = g(lane);
-            int64_t i = 8 + lane;
-            for (; i + 24 < asz2; i += 32) {  // loads ahead of the dependent adds
-                const float v0 = g(i), v1 = g(i + 8), v2 = g(i + 16), v3 = g(i + 24);
-                a = a + v0;
-                a = a + v1;
-                a = a + v2;
-                a = a + v3;
-            }
-            for (; i < asz2; i += 8) a = a + g(i);
-            acc = a;
-        }
+        if (lane < 8) acc = elm_chain<8>(8 + lane, asz2, g(lane), g);
         const float p1 = __shfl(acc, (lane + 4) & 63, 64);
         if (lane < 4) {
             acc = acc + p1;
@@ -230,10 +275,9 @@ __device__ float elm_redux_wave(int64_t size, G g, int lane) {
     if (lane == 0) {
         if (asz) {
             res = (a0 + a2) + (a1 + a3);
-            for (int64_t i = asz; i < size; ++i) res = res + g(i);
+            for (int i = asz; i < size; ++i) res = res + g(i);
         } else if (size > 0) {
-            res = g(0);
-            for (int64_t i = 1; i < size; ++i) res = res + g(i);
+            res = elm_chain<1>(1, size, g(0), g);
         }
     }
     return res;
@@ -258,19 +302,43 @@ struct ElmShared {
 };
 
 // ColPivHouseholderQR<MatrixXf>::compute on the Jacobian in place (A: column-major, m x N), the oracle's
-// ColPivQR::compute.  Every thread of the block calls it.
-template <class F>
-__device__ void elm_qr(float* A, int64_t m, ElmShared<F>& s) {
+// ColPivQR::compute, fused with householderQ().adjoint() * w (m floats, the oracle's ColPivQR::apply_qt):
+// reflector k is applied to w right after it is formed -- later steps never touch column k, and apply_qt
+// applies the reflectors to w in the same order k = 0, 1, ... -- so w's dot product (Eigen's redux, wave
+// 1) runs beside the block GEMV's (the row-major kernel's order, wave 0).  The pivot column's recomputed
+// norm and the reflector's tail norm are taken in one pass (the swap only moves the column).  Every thread
+// of the block calls it.
+#ifdef PITT_ELM_PROF
+#define PITT_QR_T(k)                             \
+    do {                                         \
+        const unsigned long long t_ = clock64(); \
+        qp[k] += t_ - qt;                        \
+        qt = t_;                                 \
+    } while (0)
+#else
+#define PITT_QR_T(k) \
+    do {             \
+    } while (0)
+#endif
+template <class F, class B>
+__device__ __forceinline__ void elm_qr(float* A, int64_t m, float* w, ElmShared<F>& s, B&& wave1_first,
+                                       unsigned long long* qp = nullptr) {
     constexpr int N = F::N;
+#ifdef PITT_ELM_PROF
+    unsigned long long qt = clock64();
+#else
+    (void)qp;
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr float kEps = FLT_EPSILON;
-    // column squared norms: 8 lanes per column
-    if (wave == 0)
-        for (int j = 0; j < N; ++j) {
-            const float* col = A + (int64_t)j * m;
-            const float r = elm_redux_wave(m, [&](int64_t i) { const float v = col[i]; return v * v; }, lane);
-            if (lane == 0) s.sq[j] = r;
-        }
+    // column squared norms: lanes 8 j .. 8 j + 7 for column j, all columns at once
+    if (wave == 0) {
+        const int q = lane >> 3;
+        const float* col = A + (int64_t)(q < N ? q : 0) * m;
+        const float r = elm_redux_wave8(q < N ? m : 0, [&](int i) { const float v = col[i]; return v * v; }, lane);
+        if ((lane & 7) == 0 && q < N) s.sq[q] = r;
+    }
+    if (wave == 1) wave1_first(lane);  // the caller's work beside the column norms (the blue norms)
     __syncthreads();
     if (tid == 0) {
         float mx = s.sq[0];
@@ -278,23 +346,27 @@ __device__ void elm_qr(float* A, int64_t m, ElmShared<F>& s) {
         s.bc[0] = mx * (kEps * kEps) / (float)m;  // threshold_helper
         s.nonzero_pivots = N;
         s.maxpivot = 0.0f;
+        int big = 0;  // the first pivot: the first maximum of the squared norms
+        for (int j = 1; j < N; ++j)
+            if (s.sq[j] > s.sq[big]) big = j;
+        s.ibc[0] = big;
     }
     __syncthreads();
+    PITT_QR_T(0);
     const float threshold_helper = s.bc[0];
     for (int k = 0; k < N; ++k) {
-        // the pivot: the first maximum of the running squared norms, its norm recomputed
-        if (tid == 0) {
-            int big = k;
-            for (int j = k + 1; j < N; ++j)
-                if (s.sq[j] > s.sq[big]) big = j;
-            s.ibc[0] = big;
-        }
-        __syncthreads();
         const int big = s.ibc[0];
+        const int64_t len = m - k;
         if (wave == 0) {
-            const float* col = A + (int64_t)big * m + k;
-            const float bigsq = elm_redux_wave(m - k, [&](int64_t i) { const float v = col[i]; return v * v; }, lane);
+            // lanes 0-7: the pivot column's norm from row k, recomputed; lanes 8-15: makeHouseholderInPlace's
+            // tail norm, rows k + 1.. of the same column (column k once swapped)
+            const int q = lane >> 3;
+            const float* col = A + (int64_t)big * m + k + (q == 1 ? 1 : 0);
+            const int64_t sz = q == 0 ? len : (q == 1 ? len - 1 : 0);
+            const float r = elm_redux_wave8(sz, [&](int i) { const float v = col[i]; return v * v; }, lane);
+            const float tail_sq = __shfl(r, 8, 64);
             if (lane == 0) {
+                const float bigsq = r;
                 s.sq[big] = bigsq;
                 if (s.nonzero_pivots == N && bigsq < threshold_helper * (float)(m - k)) s.nonzero_pivots = k;
                 s.transp[k] = big;
@@ -303,27 +375,7 @@ __device__ void elm_qr(float* A, int64_t m, ElmShared<F>& s) {
                     s.sq[k] = s.sq[big];
                     s.sq[big] = t;
                 }
-            }
-        }
-        __syncthreads();
-        if (k != big) {  // swap columns k and big (all rows)
-            float* a = A + (int64_t)k * m;
-            float* b = A + (int64_t)big * m;
-            for (int64_t r = tid; r < m; r += kElmThreads) {
-                const float t = a[r];
-                a[r] = b[r];
-                b[r] = t;
-            }
-        }
-        __syncthreads();
-        // makeHouseholderInPlace on A(k.., k)
-        float* v = A + (int64_t)k * m + k;
-        const int64_t len = m - k;
-        if (wave == 0) {
-            const float tail_sq =
-                len == 1 ? 0.0f : elm_redux_wave(len - 1, [&](int64_t i) { const float e = v[1 + i]; return e * e; }, lane);
-            if (lane == 0) {
-                const float c0 = v[0];
+                const float c0 = A[(int64_t)big * m + k];
                 float tau, beta, den = 1.0f;
                 int zero = 0;
                 if (tail_sq == 0.0f) {
@@ -345,73 +397,96 @@ __device__ void elm_qr(float* A, int64_t m, ElmShared<F>& s) {
             }
         }
         __syncthreads();
+        PITT_QR_T(1);
         const float tau = s.bc[1], beta = s.bc[2], den = s.bc[3];
         const bool zero = s.ibc[1] != 0;
-        for (int64_t i = 1 + tid; i < len; i += kElmThreads) v[i] = zero ? 0.0f : v[i] / den;
+        {  // columns k and big swapped (all rows); column k's essential part scaled, beta on the diagonal
+            float* a = A + (int64_t)k * m;
+            float* b = A + (int64_t)big * m;
+            for (int64_t r = tid; r < m; r += kElmThreads) {
+                float nk = b[r];
+                if (k != big) b[r] = a[r];
+                if (r > k) nk = zero ? 0.0f : nk / den;
+                else if (r == k) nk = beta;
+                a[r] = nk;
+            }
+        }
         __syncthreads();
-        if (tid == 0) v[0] = beta;
+        PITT_QR_T(2);
         // applyHouseholderOnTheLeft to the block A(k.., k+1..): tmp_c = essential^T * bottom (row-major GEMV
-        // order: head to the essential vector's 16-byte boundary, one packet, tail), lanes 4 c + l
+        // order: head to the essential vector's 16-byte boundary, one packet, tail), lanes 4 c + l of wave 0;
+        // and to w: tmp_w = essential . w(k+1..) + w(k) (Eigen's redux), wave 1
         const int cols = N - k - 1;
         const int64_t rows = m - k;
-        if (cols > 0) {
-            if (rows == 1) {
-                if (tid == 0)
-                    for (int c = 0; c < cols; ++c) A[(int64_t)(k + 1 + c) * m + k] = A[(int64_t)(k + 1 + c) * m + k] * (1.0f - tau);
-            } else {
-                const float* ess = A + (int64_t)k * m + k + 1;
-                const int64_t depth = rows - 1;
+        if (rows == 1) {
+            if (tid == 0) {
+                for (int c = 0; c < cols; ++c) A[(int64_t)(k + 1 + c) * m + k] = A[(int64_t)(k + 1 + c) * m + k] * (1.0f - tau);
+                w[k] = w[k] * (1.0f - tau);
+            }
+        } else {
+            const float* ess = A + (int64_t)k * m + k + 1;
+            const int64_t depth = rows - 1;
+            if (wave == 0 && cols > 0) {
                 const int64_t ess_off = (int64_t)k * m + k + 1;
                 int64_t as = (4 - (ess_off % 4)) % 4;
                 if (as > depth) as = depth;
                 const int64_t asize = as + ((depth - as) & ~(int64_t)3);
-                if (wave == 0) {
-                    const int c = lane >> 2, l = lane & 3;
-                    float pk = 0.0f;
-                    if (c < cols) {
-                        const float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
-                        int64_t j = as + l;
-                        for (; j + 12 < asize; j += 16) {
-                            const float p0 = col[j] * ess[j], p1 = col[j + 4] * ess[j + 4], p2 = col[j + 8] * ess[j + 8],
-                                        p3 = col[j + 12] * ess[j + 12];
-                            pk = pk + p0;
-                            pk = pk + p1;
-                            pk = pk + p2;
-                            pk = pk + p3;
-                        }
-                        for (; j < asize; j += 4) pk = pk + col[j] * ess[j];
-                    }
-                    const int b = lane & ~3;
-                    const float q0 = __shfl(pk, b, 64), q1 = __shfl(pk, b + 1, 64), q2 = __shfl(pk, b + 2, 64),
-                                q3 = __shfl(pk, b + 3, 64);
-                    if (c < cols && l == 0) {
-                        const float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
-                        float tmp = 0.0f;
-                        for (int64_t jj = 0; jj < as; ++jj) tmp = tmp + col[jj] * ess[jj];
-                        if (asize > as) tmp = tmp + ((q0 + q2) + (q1 + q3));
-                        for (int64_t jj = asize; jj < depth; ++jj) tmp = tmp + col[jj] * ess[jj];
-                        float* top = A + (int64_t)(k + 1 + c) * m + k;
-                        tmp = tmp + *top;
-                        *top = *top - tau * tmp;
-                        s.wa3[c] = tmp;            // scratch: tmp_c (wa3 is free during the QR)
-                    }
+                const int c = lane >> 2, l = lane & 3;
+                float pk = 0.0f;
+                if (c < cols) {
+                    const float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
+                    pk = elm_chain<4>((int)(as + l), (int)asize, 0.0f, [&](int j) { return col[j] * ess[j]; });
                 }
-                __syncthreads();
-                for (int64_t e = tid; e < (int64_t)cols * depth; e += kElmThreads) {
-                    const int c = (int)(e / depth);
-                    const int64_t i = e - (int64_t)c * depth;
-                    float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
-                    col[i] = col[i] - (tau * ess[i]) * s.wa3[c];
+                const int b = lane & ~3;
+                const float q0 = __shfl(pk, b, 64), q1 = __shfl(pk, b + 1, 64), q2 = __shfl(pk, b + 2, 64),
+                            q3 = __shfl(pk, b + 3, 64);
+                if (c < cols && l == 0) {
+                    const float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
+                    float tmp = 0.0f;
+                    for (int64_t jj = 0; jj < as; ++jj) tmp = tmp + col[jj] * ess[jj];
+                    if (asize > as) tmp = tmp + ((q0 + q2) + (q1 + q3));
+                    for (int64_t jj = asize; jj < depth; ++jj) tmp = tmp + col[jj] * ess[jj];
+                    float* top = A + (int64_t)(k + 1 + c) * m + k;
+                    tmp = tmp + *top;
+                    *top = *top - tau * tmp;
+                    s.wa3[c] = tmp;  // scratch: tmp_c (wa3 is free during the QR)
                 }
             }
+            if (wave == 1) {
+                const float* wb = w + k + 1;
+                const float tw = elm_redux_wave(depth, [&](int i) { return ess[i] * wb[i]; }, lane);
+                if (lane == 0) {
+                    const float tmp = tw + w[k];
+                    w[k] = w[k] - tau * tmp;
+                    s.bc[4] = tmp;
+                }
+            }
+            __syncthreads();
+            PITT_QR_T(3);
+            const float tmpw = s.bc[4];
+            for (int c = 0; c < cols; ++c) {
+                float* col = A + (int64_t)(k + 1 + c) * m + k + 1;
+                const float tc = s.wa3[c];
+                for (int64_t i = tid; i < depth; i += kElmThreads) col[i] = col[i] - (tau * ess[i]) * tc;
+            }
+            for (int64_t i = tid; i < depth; i += kElmThreads) w[k + 1 + i] = w[k + 1 + i] - (tau * ess[i]) * tmpw;
         }
         __syncthreads();
-        if (tid == 0)
+        PITT_QR_T(4);
+        if (tid == 0) {  // the norms downdated, the next pivot
             for (int j = k + 1; j < N; ++j) {
                 const float r = A[(int64_t)j * m + k];
                 s.sq[j] = s.sq[j] - r * r;
             }
+            if (k + 1 < N) {
+                int nb = k + 1;
+                for (int j = k + 2; j < N; ++j)
+                    if (s.sq[j] > s.sq[nb]) nb = j;
+                s.ibc[0] = nb;
+            }
+        }
         __syncthreads();
+        PITT_QR_T(5);
     }
     if (tid == 0) {
         for (int k = 0; k < N; ++k) s.perm[k] = k;
@@ -426,40 +501,10 @@ __device__ void elm_qr(float* A, int64_t m, ElmShared<F>& s) {
     __syncthreads();
 }
 
-// householderQ().adjoint() applied to w (m floats), the oracle's ColPivQR::apply_qt.
-template <class F>
-__device__ void elm_apply_qt(const float* A, int64_t m, float* w, ElmShared<F>& s) {
-    constexpr int N = F::N;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int k = 0; k < N; ++k) {
-        const int64_t rows = m - k;
-        const float tau = s.hc[k];
-        if (rows == 1) {
-            if (tid == 0) w[k] = w[k] * (1.0f - tau);
-            __syncthreads();
-            continue;
-        }
-        const float* ess = A + (int64_t)k * m + k + 1;
-        const float* wb = w + k + 1;
-        if (wave == 0) {
-            float tmp = elm_redux_wave(rows - 1, [&](int64_t i) { return ess[i] * wb[i]; }, lane);
-            if (lane == 0) {
-                tmp = tmp + w[k];
-                w[k] = w[k] - tau * tmp;
-                s.bc[0] = tmp;
-            }
-        }
-        __syncthreads();
-        const float tmp = s.bc[0];
-        for (int64_t i = tid; i < rows - 1; i += kElmThreads) w[k + 1 + i] = w[k + 1 + i] - (tau * ess[i]) * tmp;
-        __syncthreads();
-    }
-}
-
 // stableNorm of an m-vector (4096-element blocks scaled by the running max): every thread calls it; the
 // value is returned to all of them.
 template <class F>
-__device__ float elm_stable_block(const float* v, int64_t n, ElmShared<F>& s, float* red) {
+__device__ __forceinline__ float elm_stable_block(const float* v, int64_t n, ElmShared<F>& s, float* red) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float scale = 0.0f, inv = 1.0f, ssq = 0.0f;
     for (int64_t bi = 0; bi < n; bi += 4096) {
@@ -493,7 +538,7 @@ __device__ float elm_stable_block(const float* v, int64_t n, ElmShared<F>& s, fl
         }
         if (wave == 0) {
             const float* vb = v + bi;
-            const float sum = elm_redux_wave(len, [&](int64_t i) { const float t = vb[i] * inv; return t * t; }, lane);
+            const float sum = elm_redux_wave(len, [&](int i) { const float t = vb[i] * inv; return t * t; }, lane);
             if (lane == 0) s.bc[1] = sum;
         }
         __syncthreads();
@@ -663,14 +708,17 @@ __device__ __forceinline__ void elm_eval(const ElmJob& j, const typename F::Pre&
 }
 
 // The workspace ((N + 2) m floats: the Jacobian, f(x) and the trial residuals) lives in LDS when the
-// batch's largest job fits (lds != 0: the launch's dynamic LDS holds it), else in HBM (ElmJob::work).
+// batch's largest job fits (k_elm<F, true>: the launch's dynamic LDS holds it), else in HBM (ElmJob::work).
 // Every m-long serial chain of the LM reads it: from LDS a chain step waits ~100 cycles for its operand,
 // from L2/HBM several hundred.
 extern __shared__ float elm_dyn[];
 constexpr size_t kElmLdsMax = 144 * 1024;  // dynamic LDS budget per block (of the CU's 160 KB)
 
-template <class F>
-__global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ jobs, int lds) {
+// LDS: the Jacobian and both residual vectors live in dynamic LDS ((N + 2) m floats <= kElmLdsMax), every
+// pointer into them derived from elm_dyn so that the chains read them with ds_read (a pointer that may be
+// either LDS or HBM compiles to flat loads, about twice the latency); otherwise in the job's HBM workspace.
+template <class F, bool LDS>
+__global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ jobs) {
     constexpr int N = F::N;
     __shared__ ElmShared<F> s;
     __shared__ float red[kElmThreads / 64];
@@ -684,8 +732,9 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
         }
         return;
     }
-    float* fjac = lds ? elm_dyn : j.work;
-    float* rbuf[2] = {j.work + (int64_t)N * m, j.work + (int64_t)(N + 1) * m};
+    float* const ws = LDS ? elm_dyn : j.work;
+    float* fjac = ws;
+    float* rbuf[2] = {ws + (int64_t)N * m, ws + (int64_t)(N + 1) * m};
     constexpr float factor = 100.0f;
     const float ftol = sqrtf(FLT_EPSILON), xtol = sqrtf(FLT_EPSILON), gtol = 0.0f, eps = FLT_EPSILON;
     constexpr int maxfev = 400;
@@ -710,7 +759,25 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
         if (tid == 0) s.fnorm = fn;
     }
     __syncthreads();
+#ifdef PITT_ELM_PROF  // per-phase cycles of thread 0 (s_memtime), printed at the end
+    unsigned long long qprof[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = clock64();
+    int n_outer = 0, n_inner = 0;
+#define PITT_ELM_T(k)                          \
+    do {                                       \
+        const unsigned long long t_ = clock64(); \
+        pc[k] += t_ - pt;                      \
+        pt = t_;                               \
+    } while (0)
+#else
+#define PITT_ELM_T(k) \
+    do {              \
+    } while (0)
+#endif
     while (true) {
+#ifdef PITT_ELM_PROF
+        ++n_outer;
+#endif
         float* fvec = rbuf[s.cur];
         float* wa4 = rbuf[s.cur ^ 1];
         // NumericalDiff<Forward>::df: column c = (f(x + h_c e_c) - f(x)) / h_c, h_c = sqrt(eps) |x_c| (or sqrt(eps))
@@ -722,36 +789,67 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
             q[tid] = q[tid] + h;
             s.hstep[tid] = h;
             F::prep(q, s.pre[tid]);
+            if (tid == 0) s.ibc[3] = 0;
         }
         __syncthreads();
-        for (int64_t i = tid; i < m; i += kElmThreads) {
-            const int32_t id = j.inl[i];
-            const float px = j.x[id], py = j.y[id], pz = j.z[id];
-            const float f0 = fvec[i];
+        // the Jacobian, each column's "every element in blueNorm's middle range" test (bit c of ibc[3] set
+        // when some element is not: too big, too small but nonzero, or NaN), and wa4 = f(x) for Q^T f
+        {
+            const ElmBlue bc = elm_blue_consts();
+            const float ab2 = bc.b2 / (float)m;
+            int outside = 0;
+            for (int64_t i = tid; i < m; i += kElmThreads) {
+                const int32_t id = j.inl[i];
+                const float px = j.x[id], py = j.y[id], pz = j.z[id];
+                const float f0 = fvec[i];
 #pragma unroll
-            for (int c = 0; c < N; ++c) fjac[(int64_t)c * m + i] = (F::eval(s.pre[c], px, py, pz) - f0) / s.hstep[c];
-        }
-        __syncthreads();
-        if (tid == 0) s.nfev += N + 1;
-        // wa2 = the columns' blue norms (one lane per column, sequential in the column)
-        if (wave == 0 && lane < N) {
-            const ElmBlue c = elm_blue_consts();
-            const float ab2 = c.b2 / (float)m;
-            const float* col = fjac + (int64_t)lane * m;
-            float asml = 0.0f, amed = 0.0f, abig = 0.0f;
-            int64_t i = 0;
-            for (; i + 3 < m; i += 4) {
-                const float v0 = col[i], v1 = col[i + 1], v2 = col[i + 2], v3 = col[i + 3];
-                elm_blue_step(c, ab2, v0, asml, amed, abig);
-                elm_blue_step(c, ab2, v1, asml, amed, abig);
-                elm_blue_step(c, ab2, v2, asml, amed, abig);
-                elm_blue_step(c, ab2, v3, asml, amed, abig);
+                for (int c = 0; c < N; ++c) {
+                    const float v = (F::eval(s.pre[c], px, py, pz) - f0) / s.hstep[c];
+                    fjac[(int64_t)c * m + i] = v;
+                    const float ax = fabsf(v);
+                    if (!(ax <= ab2 && (ax >= bc.b1 || ax == 0.0f))) outside |= 1 << c;
+                }
+                wa4[i] = f0;
             }
-            for (; i < m; ++i) elm_blue_step(c, ab2, col[i], asml, amed, abig);
-            s.colnorm[lane] = elm_blue_finish(c, asml, amed, abig);
+            if (outside) atomicOr(&s.ibc[3], outside);
         }
         __syncthreads();
-        elm_qr<F>(fjac, m, s);
+        PITT_ELM_T(0);
+        if (tid == 0) s.nfev += N + 1;
+        // the columns' blue norms (wa2), wave 1 lane c for column c while wave 0 takes the QR's column norms:
+        // a column with every element in the middle range sums only ax^2 (the other two sums stay +0, and a
+        // zero element adds +0 to whichever sum takes it), one dependent add per element
+        auto blue = [&](int ln) {
+            if (ln >= N) return;
+            const float* col = fjac + (int64_t)ln * m;
+            float r;
+            if (!((s.ibc[3] >> ln) & 1)) {
+                r = sqrtf(elm_chain<1>(0, (int)m, 0.0f, [&](int i) { const float v = col[i]; return v * v; }));
+            } else {
+                const ElmBlue c = elm_blue_consts();
+                const float ab2 = c.b2 / (float)m;
+                float asml = 0.0f, amed = 0.0f, abig = 0.0f;
+                int64_t i = 0;
+                for (; i + 3 < m; i += 4) {
+                    const float v0 = col[i], v1 = col[i + 1], v2 = col[i + 2], v3 = col[i + 3];
+                    elm_blue_step(c, ab2, v0, asml, amed, abig);
+                    elm_blue_step(c, ab2, v1, asml, amed, abig);
+                    elm_blue_step(c, ab2, v2, asml, amed, abig);
+                    elm_blue_step(c, ab2, v3, asml, amed, abig);
+                }
+                for (; i < m; ++i) elm_blue_step(c, ab2, col[i], asml, amed, abig);
+                r = elm_blue_finish(c, asml, amed, abig);
+            }
+            s.colnorm[ln] = r;
+        };
+        PITT_ELM_T(1);
+        // the QR, with qtf = (Q^T f)(0..n) formed in wa4 on the way
+#ifdef PITT_ELM_PROF
+        elm_qr<F>(fjac, m, wa4, s, blue, qprof);
+#else
+        elm_qr<F>(fjac, m, wa4, s, blue);
+#endif
+        PITT_ELM_T(2);
         if (tid == 0 && s.iter == 1) {
             for (int k = 0; k < N; ++k) s.diag[k] = s.colnorm[k] == 0.0f ? 1.0f : s.colnorm[k];
             float dx[N];
@@ -760,10 +858,7 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
             s.delta = factor * s.xnorm;
             if (s.delta == 0.0f) s.delta = factor;
         }
-        // qtf = (Q^T f)(0..n)
-        for (int64_t i = tid; i < m; i += kElmThreads) wa4[i] = fvec[i];
-        __syncthreads();
-        elm_apply_qt<F>(fjac, m, wa4, s);
+        PITT_ELM_T(3);
         if (tid == 0) {
             for (int k = 0; k < N; ++k) s.qtf[k] = wa4[k];
             float gnorm = 0.0f;
@@ -785,6 +880,10 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
         if (s.status != kElmRunning) break;
         // the inner loop: trial steps until one is accepted (ratio >= 1e-4) or a test stops
         while (true) {
+#ifdef PITT_ELM_PROF
+            ++n_inner;
+#endif
+            PITT_ELM_T(4);
             if (tid == 0) {
                 float step[N];
                 elm_lmpar<F>(s, s.qtf, s.delta, s.par, step);
@@ -797,10 +896,13 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
                 F::prep(s.wa2, s.pre[N]);
             }
             __syncthreads();
+            PITT_ELM_T(5);
             float* trial = rbuf[s.cur ^ 1];
             elm_eval<F>(j, s.pre[N], trial);
             __syncthreads();
+            PITT_ELM_T(6);
             const float fnorm1 = elm_stable_block(trial, m, s, red);
+            PITT_ELM_T(7);
             if (tid == 0) {
                 ++s.nfev;
                 const float pnorm = s.bc[6];
@@ -855,8 +957,18 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
             __syncthreads();
             if (!s.ibc[2]) break;
         }
+        PITT_ELM_T(4);
         if (s.status != kElmRunning) break;
     }
+#ifdef PITT_ELM_PROF
+    if (tid == 0)
+        printf("PITT_ELM_PROF N %d m %lld outer %d inner %d nfev %d status %d cycles: jacobian %llu qr %llu post %llu "
+               "lmpar %llu eval %llu stable %llu logic %llu | qr: norms %llu pivnorm %llu swap %llu gemv %llu update %llu "
+               "downdate %llu\n",
+               N, (long long)m, n_outer, n_inner, s.nfev, s.status, pc[0], pc[2], pc[3], pc[5], pc[6], pc[7], pc[4],
+               qprof[0], qprof[1], qprof[2], qprof[3], qprof[4], qprof[5]);
+#endif
+#undef PITT_ELM_T
     if (tid == 0) {
         F::finish(s.x, j.out);
         if (j.info) j.info[0] = s.status, j.info[1] = s.nfev;
@@ -878,7 +990,7 @@ inline int launch_elm_batch(pitt_ctx* ctx, hipStream_t s, std::vector<ElmJob>& j
     if (lds) {
         static bool attr_set = false;  // once per kernel instantiation (one per model kind)
         if (!attr_set) {
-            PITT_HIP_TRY(hipFuncSetAttribute((const void*)k_elm<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            PITT_HIP_TRY(hipFuncSetAttribute((const void*)k_elm<F, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)kElmLdsMax));
             attr_set = true;
         }
@@ -895,7 +1007,10 @@ inline int launch_elm_batch(pitt_ctx* ctx, hipStream_t s, std::vector<ElmJob>& j
     }
     std::copy(jobs.begin(), jobs.end(), h);
     PITT_HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_elm<F>, dim3((unsigned)jobs.size()), dim3(kElmThreads), lds ? lds_bytes : 0, s, d, lds);
+    if (lds)
+        hipLaunchKernelGGL((k_elm<F, true>), dim3((unsigned)jobs.size()), dim3(kElmThreads), lds_bytes, s, d);
+    else
+        hipLaunchKernelGGL((k_elm<F, false>), dim3((unsigned)jobs.size()), dim3(kElmThreads), 0, s, d);
     PITT_HIP_TRY(hipGetLastError());
 #ifdef PITT_SYNC_CHECK
     ctx->check_canaries(name);

@@ -21,7 +21,7 @@ def load(path):
         rows = list(csv.DictReader(f))
     out = []
     for r in rows:
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip().split("::")[-1]
         q = r.get("Queue_Id") or r.get("Stream_Id") or "0"
         out.append(dict(name=name, q=q, s=int(r["Start_Timestamp"]), e=int(r["End_Timestamp"])))
     out.sort(key=lambda k: k["s"])
