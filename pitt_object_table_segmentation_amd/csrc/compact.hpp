@@ -56,6 +56,37 @@ __global__ __launch_bounds__(kBlock) void k_pred_apply(Pred pred, Action act, in
     }
 }
 
+// Several small clouds at once (pitt_classify_clusters' selections): one block per cloud walks its tiles in
+// order with a running offset -- count, scan and write in one launch.  cnt: the cloud's output count.
+template <class Pred, class Action>
+struct SelectItem {
+    Pred pred;
+    Action act;
+    int64_t n;
+    int32_t* cnt;
+};
+template <class Pred, class Action>
+__global__ __launch_bounds__(kBlock) void k_select_small(const SelectItem<Pred, Action>* __restrict__ items) {
+    __shared__ int32_t lds4[kBlock / 64];
+    const SelectItem<Pred, Action> it = items[blockIdx.x];
+    const int64_t nt = ctiles(it.n);
+    int64_t run = 0;
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t b = t * kCTile + threadIdx.x * 8;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bits |= ((b + k < it.n && it.pred(b + k)) ? 1u : 0u) << k;
+        int total;
+        int64_t pos = block_exscan(__builtin_popcount(bits), lds4, &total) + run;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if ((bits >> k) & 1u) it.act(b + k, pos++);
+        run += total;
+    }
+    if (threadIdx.x == 0) *it.cnt = (int32_t)run;
+}
+constexpr int64_t kSelectSmallTiles = 8;  // clouds up to 16k points take k_select_small
+
 inline int grid_for_tiles(int64_t nt) { return (int)(nt < 1 ? 1 : (nt > 2048 ? 2048 : nt)); }
 
 }  // namespace pitt

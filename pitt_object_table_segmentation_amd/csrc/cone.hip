@@ -187,6 +187,18 @@ __global__ void k_cone_prepare(Coef7 m, ConeCfg cfg, ConePrep* out) {
     *out = r;
 }
 
+// The same for several clouds' models (device coefficients), cloud c where sel[c] >= 0.
+__global__ void k_cone_prepare_multi(const Coef7* __restrict__ m, const int32_t* __restrict__ sel, int nc, ConeCfg cfg,
+                                     ConePrep* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc || sel[c] < 0) return;
+    const Coef7 mc = m[c];
+    ConePrep r;
+    r.q = cone_model(mc);
+    r.valid = cone_valid(mc, cfg) ? 1 : 0;
+    out[c] = r;
+}
+
 // prim_ransac.hpp traits of the cone service
 struct ConeModelT {
     using Coef = Coef7;
@@ -216,10 +228,19 @@ struct ConeModelT {
     void launch_prep(hipStream_t s, const Coef7& m, ConePrep* out) const {
         hipLaunchKernelGGL(k_cone_prepare, dim3(1), dim3(1), 0, s, m, cfg, out);
     }
+    void launch_prep_multi(hipStream_t s, const Coef7* m, const int32_t* sel, int nc, ConePrep* out) const {
+        hipLaunchKernelGGL(k_cone_prepare_multi, dim3((unsigned)((nc + 63) / 64)), dim3(64), 0, s, m, sel, nc, cfg, out);
+    }
     static bool prep_valid(const ConePrep& p) { return p.valid != 0; }
-    void launch_select(hipStream_t s, const PrimCloud& c, const Coef7&, const ConePrep& q, int32_t* tc, int32_t* to,
+    using SelPred = ConeIn;
+    using SelAct = ConeWriteIdx;
+    ConeIn sel_pred(const PrimCloud& c, const Coef7&, const ConePrep& q) const {
+        return ConeIn{c.x, c.y, c.z, c.nx, c.ny, c.nz, q.q, cfg};
+    }
+    static ConeWriteIdx sel_act(const PrimCloud& c) { return ConeWriteIdx{c.inliers}; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const Coef7& m, const ConePrep& q, int32_t* tc, int32_t* to,
                        int g) const {
-        ConeIn pred{c.x, c.y, c.z, c.nx, c.ny, c.nz, q.q, cfg};
+        ConeIn pred = sel_pred(c, m, q);
         hipLaunchKernelGGL(k_pred_count<ConeIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
         hipLaunchKernelGGL((k_pred_apply<ConeIn, ConeWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,

@@ -192,6 +192,14 @@ struct pitt_ctx {
         h->pos = (h->pos + 1) & 15;
     }
     uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
+    // prim_ransac.hpp: which sampler table each cloud slot of a model's device table buffer holds (the
+    // buffer's address and arena generation when they were uploaded), so a repeat skips the upload
+    struct PrimTableMemo {
+        const void* dev = nullptr;
+        uint64_t gen = 0;
+        std::vector<std::tuple<int64_t, uint32_t, int64_t>> keys;
+    };
+    std::unordered_map<std::string, PrimTableMemo> prim_tables;
     struct GraphEntry {
         std::vector<uint64_t> key;
         hipGraphExec_t exec = nullptr;

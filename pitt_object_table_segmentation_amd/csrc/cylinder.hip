@@ -177,9 +177,15 @@ struct CylModel {
     }
     void launch_prep(hipStream_t, const CylCoef&, CylPrep*) const {}
     static bool prep_valid(const CylPrep& p) { return p.valid != 0; }
-    void launch_select(hipStream_t s, const PrimCloud& c, const CylCoef& m, const CylPrep&, int32_t* tc, int32_t* to,
+    using SelPred = CylIn;
+    using SelAct = CylWriteIdx;
+    CylIn sel_pred(const PrimCloud& c, const CylCoef& m, const CylPrep&) const {
+        return CylIn{c.x, c.y, c.z, c.nx, c.ny, c.nz, m, w, th, eigen33};
+    }
+    static CylWriteIdx sel_act(const PrimCloud& c) { return CylWriteIdx{c.inliers}; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const CylCoef& m, const CylPrep& q, int32_t* tc, int32_t* to,
                        int g) const {
-        CylIn pred{c.x, c.y, c.z, c.nx, c.ny, c.nz, m, w, th, eigen33};
+        CylIn pred = sel_pred(c, m, q);
         hipLaunchKernelGGL(k_pred_count<CylIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
         hipLaunchKernelGGL((k_pred_apply<CylIn, CylWriteIdx>), dim3(g), dim3(kBlock), 0, s, pred,

@@ -58,6 +58,15 @@ struct PrimResult {
     float coef[7];
 };
 
+// The winning (or refined) model of every cloud c with sel[c] >= 0: coef[c * A + sel[c]] (A = 0, sel[c] = 0:
+// coef[c]) into out[c].
+template <class Coef>
+__global__ void k_gather_coef(const Coef* __restrict__ coef, int64_t A, const int32_t* __restrict__ sel, int nc,
+                              Coef* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < nc && sel[c] >= 0) out[c] = coef[(int64_t)c * A + sel[c]];
+}
+
 // The phase interface of one model's batch (PrimRun<M> below); pitt_classify_clusters drives runs of the
 // three models, built in their own translation units, through it.
 struct PrimRunBase {
@@ -108,6 +117,9 @@ struct PrimRun final : PrimRunBase {
     Coef *dcoef = nullptr, *dref = nullptr, *hcoef = nullptr;
     Prep *dprep = nullptr, *hprep = nullptr;
     int32_t *htab = nullptr, *hflag = nullptr, *hcnt = nullptr, *hto = nullptr;
+    int32_t *hsel = nullptr, *dsel = nullptr;  // per cloud: the best attempt (or 0 / -1) for k_gather_coef / prep
+    Coef* dbest = nullptr;
+    bool prep_ready = false;  // the device prep of `sel` already came back with the models
     std::vector<St> st;
     std::vector<Coef> cur;
     std::vector<int> with_model, sel;
@@ -151,8 +163,11 @@ struct PrimRun final : PrimRunBase {
         hcoef = (Coef*)ctx->pinned(nm + "_coef_h", (size_t)nc * sizeof(Coef));
         hprep = (Prep*)ctx->pinned(nm + "_prep_h", (size_t)nc * sizeof(Prep));
         hto = (int32_t*)ctx->pinned(nm + "_to_h", (size_t)nc * 4);
+        hsel = (int32_t*)ctx->pinned(nm + "_sel_idx_h", (size_t)nc * 4);
+        dsel = (int32_t*)ctx->buf(nm + "_sel_idx", (size_t)nc * 4);
+        dbest = (Coef*)ctx->buf(nm + "_best", (size_t)nc * sizeof(Coef));
         if (!dtab || !dcoef || !dflag || !dcnt || !tc || !to || !dref || !dprep || !htab || !hflag || !hcnt ||
-            !hcoef || !hprep || !hto)
+            !hcoef || !hprep || !hto || !hsel || !dsel || !dbest)
             return ctx->fail(PITT_E_NOMEM, nm + " scratch");
         st.assign((size_t)nc, St{});
         cur.assign((size_t)nc, Coef{});
@@ -161,22 +176,45 @@ struct PrimRun final : PrimRunBase {
     }
 
     // 1. every cloud's hypotheses and their validity flags
+    //    (the clouds' sampler tables go up in one copy and their flags come back in one)
+    //    (a slot that already holds the cloud's table from an earlier call -- same buffer, same arena
+    //    generation, same (n, seed, attempts) -- is not uploaded again)
     int issue_hyp() override {
+        pitt_ctx::PrimTableMemo& memo = ctx->prim_tables[nm];
+        if (memo.dev != (const void*)dtab || memo.gen != ctx->arena_gen) {
+            memo.dev = dtab;
+            memo.gen = ctx->arena_gen;
+            memo.keys.clear();
+        }
+        if (memo.keys.size() < (size_t)nc) memo.keys.resize((size_t)nc, std::make_tuple((int64_t)-1, 0u, (int64_t)0));
+        int c0 = nc, c1 = 0, u0 = nc, u1 = 0;  // the clouds that sample; those whose table goes up
         for (int c = 0; c < nc; ++c) {
             if (cl[c].n < M::kSample) continue;
             st[(size_t)c].run = true;
+            c0 = std::min(c0, c);
+            c1 = c + 1;
+            const auto key = std::make_tuple(cl[c].n, m.seed, A);
+            if (memo.keys[(size_t)c] == key) continue;
             const std::vector<int32_t>& tab = sampler_table(ctx, cl[c].n, m.seed, A, M::kSample);
-            int32_t* ht = htab + (size_t)c * A * M::kSample;
-            std::copy(tab.begin(), tab.end(), ht);
-            int32_t* dt = dtab + (size_t)c * A * M::kSample;
-            PITT_HIP_TRY(hipMemcpyAsync(dt, ht, (size_t)A * M::kSample * 4, hipMemcpyHostToDevice, s));
+            std::copy(tab.begin(), tab.end(), htab + (size_t)c * A * M::kSample);
+            memo.keys[(size_t)c] = key;
+            u0 = std::min(u0, c);
+            u1 = c + 1;
+        }
+        if (c0 >= c1) return PITT_OK;
+        if (u0 < u1)
+            PITT_HIP_TRY(hipMemcpyAsync(dtab + (size_t)u0 * A * M::kSample, htab + (size_t)u0 * A * M::kSample,
+                                        (size_t)(u1 - u0) * A * M::kSample * 4, hipMemcpyHostToDevice, s));
+        for (int c = c0; c < c1; ++c) {
+            if (!st[(size_t)c].run) continue;
             const int rec = ctx->prof_begin((nm + "_model").c_str(), (double)A * M::kModelBytes);
-            m.launch_model(s, cl[c], dt, (int)A, dcoef + (size_t)c * A, dflag + (size_t)c * A);
+            m.launch_model(s, cl[c], dtab + (size_t)c * A * M::kSample, (int)A, dcoef + (size_t)c * A,
+                           dflag + (size_t)c * A);
             ctx->prof_end(rec);
             PITT_HIP_TRY(hipGetLastError());
-            PITT_HIP_TRY(hipMemcpyAsync(hflag + (size_t)c * A, dflag + (size_t)c * A, (size_t)A * 4,
-                                        hipMemcpyDeviceToHost, s));
         }
+        PITT_HIP_TRY(hipMemcpyAsync(hflag + (size_t)c0 * A, dflag + (size_t)c0 * A, (size_t)(c1 - c0) * A * 4,
+                                    hipMemcpyDeviceToHost, s));
         return PITT_OK;
     }
 
@@ -240,16 +278,30 @@ struct PrimRun final : PrimRunBase {
     }
 
     // 3. the winning models
+    //    (gathered on the device and read back in one copy; the cone's device prep of them rides along)
     int issue_best() override {
         any_model = false;
+        prep_ready = false;
         with_model.clear();
         for (int c = 0; c < nc; ++c) {
             res[c].hypotheses = st[(size_t)c].iterations;
+            hsel[c] = st[(size_t)c].best;
             if (st[(size_t)c].best < 0) continue;
             any_model = true;
             with_model.push_back(c);
-            PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dcoef + (size_t)c * A + st[(size_t)c].best, sizeof(Coef),
-                                        hipMemcpyDeviceToHost, s));
+        }
+        if (!any_model) return PITT_OK;
+        PITT_HIP_TRY(hipMemcpyAsync(dsel, hsel, (size_t)nc * 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_gather_coef<Coef>, dim3((unsigned)((nc + 63) / 64)), dim3(64), 0, s, dcoef, A, dsel, nc, dbest);
+        PITT_HIP_TRY(hipGetLastError());
+        PITT_HIP_TRY(hipMemcpyAsync(hcoef, dbest, (size_t)nc * sizeof(Coef), hipMemcpyDeviceToHost, s));
+        if constexpr (M::kDevicePrep) {
+            if (!ctx->prof) {  // profiling runs keep the per-cloud prep launches
+                m.launch_prep_multi(s, dbest, dsel, nc, dprep);
+                PITT_HIP_TRY(hipGetLastError());
+                PITT_HIP_TRY(hipMemcpyAsync(hprep, dprep, (size_t)nc * sizeof(Prep), hipMemcpyDeviceToHost, s));
+                prep_ready = true;
+            }
         }
         return PITT_OK;
     }
@@ -260,7 +312,7 @@ struct PrimRun final : PrimRunBase {
 
     // 4. selectWithinDistance of the clouds in `sel`: isModelValid (+ the predicate's constants) first,
     //    on the device for the cone
-    bool needs_prep_sync() const override { return M::kDevicePrep && !sel.empty(); }
+    bool needs_prep_sync() const override { return M::kDevicePrep && !sel.empty() && !prep_ready; }
     int issue_prep() override {
         if constexpr (M::kDevicePrep) {
             for (int c : sel) m.launch_prep(s, cur[(size_t)c], dprep + c);
@@ -273,6 +325,33 @@ struct PrimRun final : PrimRunBase {
         launched = false;
         if constexpr (!M::kDevicePrep)
             for (int c : sel) m.prep_host(cur[(size_t)c], hprep + c);
+        // every selected cloud small (the classification's clusters): one k_select_small launch, one block
+        // per cloud, and their counts back in one copy
+        bool small = !ctx->prof;  // profiling runs keep the per-cloud kernels (their names are priced)
+        for (int c : sel) small = small && ctiles(cl[c].n) <= kSelectSmallTiles;
+        if (small && !sel.empty()) {
+            using Item = SelectItem<typename M::SelPred, typename M::SelAct>;
+            Item* hi = (Item*)ctx->pinned(nm + "_sel_h", (size_t)nc * sizeof(Item));
+            Item* di = (Item*)ctx->buf(nm + "_sel", (size_t)nc * sizeof(Item));
+            int32_t* dn = (int32_t*)ctx->buf(nm + "_sel_n", (size_t)nc * 4);
+            if (!hi || !di || !dn) return ctx->fail(PITT_E_NOMEM, nm + " selection");
+            int k = 0;
+            for (int c : sel) {
+                res[c].n_inliers = 0;
+                if (!m.prep_valid(hprep[c])) continue;
+                hi[k++] = Item{m.sel_pred(cl[c], cur[(size_t)c], hprep[c]), M::sel_act(cl[c]), cl[c].n, dn + c};
+            }
+            PITT_HIP_TRY(hipMemsetAsync(dn, 0, (size_t)nc * 4, s));
+            if (k > 0) {
+                PITT_HIP_TRY(hipMemcpyAsync(di, hi, (size_t)k * sizeof(Item), hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL((k_select_small<typename M::SelPred, typename M::SelAct>), dim3((unsigned)k),
+                                   dim3(kBlock), 0, s, di);
+                PITT_HIP_TRY(hipGetLastError());
+            }
+            PITT_HIP_TRY(hipMemcpyAsync(hto, dn, (size_t)nc * 4, hipMemcpyDeviceToHost, s));
+            launched = true;
+            return PITT_OK;
+        }
         for (int c : sel) {
             res[c].n_inliers = 0;
             hto[c] = 0;
@@ -322,7 +401,20 @@ struct PrimRun final : PrimRunBase {
         ctx->prof_end(rec);
         if (rc != PITT_OK) return rc;
         PITT_HIP_TRY(hipGetLastError());
-        for (int c : refined) PITT_HIP_TRY(hipMemcpyAsync(hcoef + c, dref + c, sizeof(Coef), hipMemcpyDeviceToHost, s));
+        prep_ready = false;
+        if (refined.empty()) return PITT_OK;
+        PITT_HIP_TRY(hipMemcpyAsync(hcoef, dref, (size_t)nc * sizeof(Coef), hipMemcpyDeviceToHost, s));
+        if constexpr (M::kDevicePrep) {
+            if (!ctx->prof) {  // the refined models' device prep rides along
+                for (int c = 0; c < nc; ++c) hsel[c] = -1;
+                for (int c : refined) hsel[c] = 0;
+                PITT_HIP_TRY(hipMemcpyAsync(dsel, hsel, (size_t)nc * 4, hipMemcpyHostToDevice, s));
+                m.launch_prep_multi(s, dref, dsel, nc, dprep);
+                PITT_HIP_TRY(hipGetLastError());
+                PITT_HIP_TRY(hipMemcpyAsync(hprep, dprep, (size_t)nc * sizeof(Prep), hipMemcpyDeviceToHost, s));
+                prep_ready = true;
+            }
+        }
         return PITT_OK;
     }
     void read_refine() override {

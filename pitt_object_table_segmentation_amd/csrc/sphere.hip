@@ -159,9 +159,13 @@ struct SphModel {
     }
     void launch_prep(hipStream_t, const float4&, SphPrep*) const {}
     static bool prep_valid(const SphPrep& p) { return p.valid != 0; }
-    void launch_select(hipStream_t s, const PrimCloud& c, const float4& m, const SphPrep&, int32_t* tc, int32_t* to,
+    using SelPred = SphIn;
+    using SelAct = WriteIdx;
+    SphIn sel_pred(const PrimCloud& c, const float4& m, const SphPrep&) const { return SphIn{c.x, c.y, c.z, m, t}; }
+    static WriteIdx sel_act(const PrimCloud& c) { return WriteIdx{c.inliers}; }
+    void launch_select(hipStream_t s, const PrimCloud& c, const float4& m, const SphPrep& q, int32_t* tc, int32_t* to,
                        int g) const {
-        SphIn pred{c.x, c.y, c.z, m, t};
+        SphIn pred = sel_pred(c, m, q);
         hipLaunchKernelGGL(k_pred_count<SphIn>, dim3(g), dim3(kBlock), 0, s, pred, c.n, tc);
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kBlock), 0, s, tc, ctiles(c.n), to);
         hipLaunchKernelGGL((k_pred_apply<SphIn, WriteIdx>), dim3(g), dim3(kBlock), 0, s, pred, WriteIdx{c.inliers}, c.n,
