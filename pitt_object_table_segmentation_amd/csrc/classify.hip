@@ -102,6 +102,25 @@ extern "C" void pitt_classify_params_default(pitt_classify_params* p) {
     p->cone_over_cylinder = 0.9f;  // DEFAULT_CONE_OVER_CYLINDER_PRIORITY, ransac_segmentation.cpp:37
 }
 
+namespace pitt {
+// The clusters staged into the tile-padded SoA: cluster blockIdx.y's points [0, span) of its slot, the
+// cluster's own points first, NaN after them.  meta: offsets [nc], counts [nc], slot starts [nc].
+__global__ __launch_bounds__(256) void k_stage_clusters(const float* __restrict__ x, const float* __restrict__ y,
+                                                        const float* __restrict__ z, const int64_t* __restrict__ meta,
+                                                        int nc, int64_t total, float* __restrict__ sx,
+                                                        float* __restrict__ sy, float* __restrict__ sz) {
+    const int c = blockIdx.y;
+    const int64_t off = meta[c], n = meta[nc + c], so = meta[2 * nc + c];
+    const int64_t end = c + 1 < nc ? meta[2 * nc + c + 1] : total;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (so + i >= end) return;
+    const bool in = i < n;
+    sx[so + i] = in ? x[off + i] : __builtin_nanf("");
+    sy[so + i] = in ? y[off + i] : __builtin_nanf("");
+    sz[so + i] = in ? z[off + i] : __builtin_nanf("");
+}
+}  // namespace pitt
+
 extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float* y, const float* z,
                                       const int64_t* offsets, const int64_t* counts, int32_t n_clusters,
                                       const pitt_classify_params* prm, pitt_cluster_shape* out) {
@@ -142,15 +161,36 @@ extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float
     int32_t* hfirst = (int32_t*)ctx->pinned("cls_first_h", (size_t)nc * 4 * 4);
     if (!sx || !sy || !sz || !nx || !ny || !nz || !curv || !inl || !dmeta || !dfirst || !hmeta || !hfirst)
         return ctx->fail(PITT_E_NOMEM, "classification scratch");
-    PITT_HIP_TRY(hipMemsetAsync(sx, 0xff, nb, s));  // NaN
-    PITT_HIP_TRY(hipMemsetAsync(sy, 0xff, nb, s));
-    PITT_HIP_TRY(hipMemsetAsync(sz, 0xff, nb, s));
-    for (int c = 0; c < nc; ++c) {
-        if (!cnt[(size_t)c]) continue;
-        const size_t b = (size_t)cnt[(size_t)c] * 4;
-        PITT_HIP_TRY(hipMemcpyAsync(sx + soff[(size_t)c], x + offsets[c], b, hipMemcpyDefault, s));
-        PITT_HIP_TRY(hipMemcpyAsync(sy + soff[(size_t)c], y + offsets[c], b, hipMemcpyDefault, s));
-        PITT_HIP_TRY(hipMemcpyAsync(sz + soff[(size_t)c], z + offsets[c], b, hipMemcpyDefault, s));
+    auto on_device = [](const void* p) {
+        hipPointerAttribute_t a;
+        return hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
+    };
+    if (on_device(x) && on_device(y) && on_device(z)) {  // one gather launch (its NaN padding included)
+        int64_t* hst = (int64_t*)ctx->pinned("cls_stage_h", (size_t)nc * 3 * 8);
+        int64_t* dst = (int64_t*)ctx->buf("cls_stage", (size_t)nc * 3 * 8);
+        if (!hst || !dst) return ctx->fail(PITT_E_NOMEM, "classification staging");
+        int64_t span = 1;
+        for (int c = 0; c < nc; ++c) {
+            hst[c] = offsets[c];
+            hst[nc + c] = cnt[(size_t)c];
+            hst[2 * nc + c] = soff[(size_t)c];
+            span = std::max<int64_t>(span, (c + 1 < nc ? soff[(size_t)c + 1] : total) - soff[(size_t)c]);
+        }
+        PITT_HIP_TRY(hipMemcpyAsync(dst, hst, (size_t)nc * 3 * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_stage_clusters, dim3((unsigned)((span + 255) / 256), (unsigned)nc), dim3(256), 0, s, x, y, z,
+                           (const int64_t*)dst, nc, total, sx, sy, sz);
+        PITT_HIP_TRY(hipGetLastError());
+    } else {
+        PITT_HIP_TRY(hipMemsetAsync(sx, 0xff, nb, s));  // NaN
+        PITT_HIP_TRY(hipMemsetAsync(sy, 0xff, nb, s));
+        PITT_HIP_TRY(hipMemsetAsync(sz, 0xff, nb, s));
+        for (int c = 0; c < nc; ++c) {
+            if (!cnt[(size_t)c]) continue;
+            const size_t b = (size_t)cnt[(size_t)c] * 4;
+            PITT_HIP_TRY(hipMemcpyAsync(sx + soff[(size_t)c], x + offsets[c], b, hipMemcpyDefault, s));
+            PITT_HIP_TRY(hipMemcpyAsync(sy + soff[(size_t)c], y + offsets[c], b, hipMemcpyDefault, s));
+            PITT_HIP_TRY(hipMemcpyAsync(sz + soff[(size_t)c], z + offsets[c], b, hipMemcpyDefault, s));
+        }
     }
 
     // --- normals (PCManager::estimateNormal per cluster) ---
@@ -215,7 +255,8 @@ extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float
         std::unique_ptr<PrimRunBase> runs[3] = {sphere_run(ctx, &prm->sphere, cls[0].data(), nc, rs.data()),
                                                 cylinder_run(ctx, &prm->cylinder, cls[1].data(), nc, ry.data()),
                                                 cone_run(ctx, &prm->cone, cls[2].data(), nc, rk.data())};
-        rc = prim_ransac_lockstep(ctx, {runs[0].get(), runs[1].get(), runs[2].get()}, {ctx->side[0], ctx->side[1], s});
+        // the cone first in every phase: its refinement is the longest, so its launches go out first
+        rc = prim_ransac_lockstep(ctx, {runs[2].get(), runs[1].get(), runs[0].get()}, {s, ctx->side[1], ctx->side[0]});
         if (rc != PITT_OK) {
             for (hipStream_t sd : ctx->side) (void)hipStreamSynchronize(sd);
             return rc;

@@ -138,20 +138,18 @@ __device__ __forceinline__ bool cone_in(float x, float y, float z, float nx, flo
     return fabs(c.w * d_normal + (1 - c.w) * d_euclid) < c.th;
 }
 
-__global__ __launch_bounds__(256) void k_cone_count(const float* __restrict__ X, const float* __restrict__ Y,
-                                                    const float* __restrict__ Z, const float* __restrict__ NX,
-                                                    const float* __restrict__ NY, const float* __restrict__ NZ,
-                                                    int64_t n, const Coef7* __restrict__ coef,
-                                                    const int32_t* __restrict__ flag, int a0, ConeCfg cfg,
-                                                    int32_t* __restrict__ counts) {
-    const int a = a0 + blockIdx.y;
+__device__ __forceinline__ void cone_count_block(const float* __restrict__ X, const float* __restrict__ Y,
+                                                 const float* __restrict__ Z, const float* __restrict__ NX,
+                                                 const float* __restrict__ NY, const float* __restrict__ NZ, int64_t n,
+                                                 const Coef7* __restrict__ coef, const int32_t* __restrict__ flag,
+                                                 int a, const ConeCfg& cfg, int32_t* __restrict__ count,
+                                                 int64_t base) {
     if (flag[a] != 1) return;
     const Coef7 m = coef[a];
     if (!cone_valid(m, cfg)) return;
     const ConeModel q = cone_model(m);
     __shared__ int part[4];
     int cnt = 0;
-    const int64_t base = (int64_t)blockIdx.x * 1024;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
@@ -160,7 +158,24 @@ __global__ __launch_bounds__(256) void k_cone_count(const float* __restrict__ X,
     }
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(counts + blockIdx.y, part[0] + part[1] + part[2] + part[3]);
+    if (threadIdx.x == 0) atomicAdd(count, part[0] + part[1] + part[2] + part[3]);
+}
+__global__ __launch_bounds__(256) void k_cone_count(const float* __restrict__ X, const float* __restrict__ Y,
+                                                    const float* __restrict__ Z, const float* __restrict__ NX,
+                                                    const float* __restrict__ NY, const float* __restrict__ NZ,
+                                                    int64_t n, const Coef7* __restrict__ coef,
+                                                    const int32_t* __restrict__ flag, int a0, ConeCfg cfg,
+                                                    int32_t* __restrict__ counts) {
+    cone_count_block(X, Y, Z, NX, NY, NZ, n, coef, flag, a0 + (int)blockIdx.y, cfg, counts + blockIdx.y,
+                     (int64_t)blockIdx.x * 1024);
+}
+// Several clouds' chunks in one launch: blockIdx.z = the job, blocks past its cloud or its attempts exit.
+__global__ __launch_bounds__(256) void k_cone_count_multi(const CountJob<Coef7>* __restrict__ jobs, ConeCfg cfg) {
+    const CountJob<Coef7>& j = jobs[blockIdx.z];
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+    if ((int)blockIdx.y >= j.nh || base >= j.cl.n) return;
+    cone_count_block(j.cl.x, j.cl.y, j.cl.z, j.cl.nx, j.cl.ny, j.cl.nz, j.cl.n, j.coef, j.flag, j.a0 + (int)blockIdx.y,
+                     cfg, j.counts + blockIdx.y, base);
 }
 
 struct ConeIn {
@@ -218,6 +233,10 @@ struct ConeModelT {
     void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, Coef7* coef, int32_t* flag) const {
         hipLaunchKernelGGL(k_cone_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, c.nx, c.ny,
                            c.nz, tab, A, cfg.amin, cfg.amax, coef, flag);
+    }
+    static constexpr int kCountSpan = 1024;
+    void launch_count_multi(hipStream_t s, const CountJob<Coef7>* jobs, int nj, int bx, int nh) const {
+        hipLaunchKernelGGL(k_cone_count_multi, dim3((unsigned)bx, (unsigned)nh, (unsigned)nj), dim3(256), 0, s, jobs, cfg);
     }
     void launch_count(hipStream_t s, const PrimCloud& c, const Coef7* coef, const int32_t* flag, int a0, int nh,
                       int32_t* cnt) const {

@@ -103,20 +103,17 @@ __device__ __forceinline__ bool cyl_valid(const CylCoef& m, double rmin, double 
     return !((rmin != -DBL_MAX && m.c[6] < rmin) || (rmax != DBL_MAX && m.c[6] > rmax));
 }
 
-__global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, const float* __restrict__ Y,
-                                                   const float* __restrict__ Z, const float* __restrict__ NX,
-                                                   const float* __restrict__ NY, const float* __restrict__ NZ,
-                                                   int64_t n, const CylCoef* __restrict__ coef,
-                                                   const int32_t* __restrict__ flag, int a0, double w, double th,
-                                                   int eigen33, double rmin, double rmax,
-                                                   int32_t* __restrict__ counts) {
-    const int a = a0 + blockIdx.y;
+__device__ __forceinline__ void cyl_count_block(const float* __restrict__ X, const float* __restrict__ Y,
+                                                const float* __restrict__ Z, const float* __restrict__ NX,
+                                                const float* __restrict__ NY, const float* __restrict__ NZ, int64_t n,
+                                                const CylCoef* __restrict__ coef, const int32_t* __restrict__ flag,
+                                                int a, double w, double th, int eigen33, double rmin, double rmax,
+                                                int32_t* __restrict__ count, int64_t base) {
     if (flag[a] != 1) return;
     const CylCoef m = coef[a];
     if (!cyl_valid(m, rmin, rmax)) return;
     __shared__ int part[4];
     int cnt = 0;
-    const int64_t base = (int64_t)blockIdx.x * 1024;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
@@ -125,7 +122,26 @@ __global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, 
     }
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(counts + blockIdx.y, part[0] + part[1] + part[2] + part[3]);
+    if (threadIdx.x == 0) atomicAdd(count, part[0] + part[1] + part[2] + part[3]);
+}
+__global__ __launch_bounds__(256) void k_cyl_count(const float* __restrict__ X, const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, const float* __restrict__ NX,
+                                                   const float* __restrict__ NY, const float* __restrict__ NZ,
+                                                   int64_t n, const CylCoef* __restrict__ coef,
+                                                   const int32_t* __restrict__ flag, int a0, double w, double th,
+                                                   int eigen33, double rmin, double rmax,
+                                                   int32_t* __restrict__ counts) {
+    cyl_count_block(X, Y, Z, NX, NY, NZ, n, coef, flag, a0 + (int)blockIdx.y, w, th, eigen33, rmin, rmax,
+                    counts + blockIdx.y, (int64_t)blockIdx.x * 1024);
+}
+// Several clouds' chunks in one launch: blockIdx.z = the job, blocks past its cloud or its attempts exit.
+__global__ __launch_bounds__(256) void k_cyl_count_multi(const CountJob<CylCoef>* __restrict__ jobs, double w,
+                                                         double th, int eigen33, double rmin, double rmax) {
+    const CountJob<CylCoef>& j = jobs[blockIdx.z];
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+    if ((int)blockIdx.y >= j.nh || base >= j.cl.n) return;
+    cyl_count_block(j.cl.x, j.cl.y, j.cl.z, j.cl.nx, j.cl.ny, j.cl.nz, j.cl.n, j.coef, j.flag, j.a0 + (int)blockIdx.y,
+                    w, th, eigen33, rmin, rmax, j.counts + blockIdx.y, base);
 }
 
 struct CylIn {
@@ -165,6 +181,11 @@ struct CylModel {
     void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, CylCoef* coef, int32_t* flag) const {
         hipLaunchKernelGGL(k_cyl_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, c.nx, c.ny,
                            c.nz, tab, A, rmin, rmax, coef, flag);
+    }
+    static constexpr int kCountSpan = 1024;
+    void launch_count_multi(hipStream_t s, const CountJob<CylCoef>* jobs, int nj, int bx, int nh) const {
+        hipLaunchKernelGGL(k_cyl_count_multi, dim3((unsigned)bx, (unsigned)nh, (unsigned)nj), dim3(256), 0, s, jobs, w, th,
+                           eigen33, rmin, rmax);
     }
     void launch_count(hipStream_t s, const PrimCloud& c, const CylCoef* coef, const int32_t* flag, int a0, int nh,
                       int32_t* cnt) const {

@@ -291,6 +291,7 @@ struct ElmShared {
     Pre pre[N + 1];                 // the Jacobian's N perturbed models, then the trial model
     float x[N], diag[N], wa1[N], wa2[N], wa3[N], qtf[N], colnorm[N], hstep[N], hc[N], sq[N];
     float R[N][N];                  // R(r, c) = R[c][r]: the QR's top n x n block (column-major)
+    float lmS[N][N];                // lmpar's working copy of R for qrsolv (thread 0; in LDS rather than scratch)
     int perm[N], transp[N];
     float maxpivot;
     int nonzero_pivots;
@@ -665,7 +666,7 @@ __device__ void elm_lmpar(ElmShared<F>& s, const float* qtb, float delta, float&
     par = elm_max(par, parl);
     par = elm_min(par, paru);
     if (par == 0.0f) par = gnorm / dxnorm;
-    float S[N][N];
+    float(&S)[N][N] = s.lmS;
     for (int c = 0; c < N; ++c)
         for (int r = 0; r < N; ++r) S[c][r] = s.R[c][r];
     float sdiag[N];

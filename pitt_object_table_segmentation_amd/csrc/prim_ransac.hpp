@@ -51,6 +51,16 @@ struct PrimCloud {
     int32_t* inliers;  // device, capacity n: the final inliers, ascending
 };
 
+// One cloud's counting launch of a chunk (the multi-cloud count kernels take an array, blockIdx.z).
+template <class Coef>
+struct CountJob {
+    PrimCloud cl;
+    const Coef* coef;
+    const int32_t* flag;
+    int a0, nh;
+    int32_t* counts;
+};
+
 struct PrimResult {
     int status;        // PITT_OK (a model), PITT_NO_MODEL, or an error code
     int hypotheses;    // computeModel iterations
@@ -225,6 +235,27 @@ struct PrimRun final : PrimRunBase {
         if (!*any) return PITT_OK;
         // one zeroed [nc][256] count block per chunk, read back whole
         PITT_HIP_TRY(hipMemsetAsync(dcnt, 0, (size_t)nc * 256 * 4, s));
+        if (!ctx->prof) {  // every running cloud's counts in one launch (profiling runs keep one per cloud)
+            using Job = CountJob<Coef>;
+            Job* hj = (Job*)ctx->pinned(nm + "_cjobs_h", (size_t)nc * sizeof(Job));
+            Job* dj = (Job*)ctx->buf(nm + "_cjobs", (size_t)nc * sizeof(Job));
+            if (!hj || !dj) return ctx->fail(PITT_E_NOMEM, nm + " count jobs");
+            int k = 0, nh_max = 0;
+            int64_t bx_max = 0;
+            for (int c = 0; c < nc; ++c) {
+                St& q = st[(size_t)c];
+                if (!q.run) continue;
+                const int nh = (int)(std::min<int64_t>(A, q.a + chunk) - q.a);
+                hj[k++] = Job{cl[c], dcoef + (size_t)c * A, dflag + (size_t)c * A, (int)q.a, nh, dcnt + (size_t)c * 256};
+                nh_max = std::max(nh_max, nh);
+                bx_max = std::max<int64_t>(bx_max, (cl[c].n + M::kCountSpan - 1) / M::kCountSpan);
+            }
+            PITT_HIP_TRY(hipMemcpyAsync(dj, hj, (size_t)k * sizeof(Job), hipMemcpyHostToDevice, s));
+            m.launch_count_multi(s, dj, k, (int)std::max<int64_t>(bx_max, 1), nh_max);
+            PITT_HIP_TRY(hipGetLastError());
+            PITT_HIP_TRY(hipMemcpyAsync(hcnt, dcnt, (size_t)nc * 256 * 4, hipMemcpyDeviceToHost, s));
+            return PITT_OK;
+        }
         for (int c = 0; c < nc; ++c) {
             St& q = st[(size_t)c];
             if (!q.run) continue;

@@ -92,16 +92,14 @@ __device__ __forceinline__ bool sph_in(float x, float y, float z, float4 c, floa
 }
 
 // counts[a - a0] for attempts [a0, a0 + gridDim.y): blockIdx.x = 2048-point tile
-__global__ __launch_bounds__(256) void k_sph_count(const float* __restrict__ X, const float* __restrict__ Y,
-                                                   const float* __restrict__ Z, int64_t n,
-                                                   const float4* __restrict__ coef, const int32_t* __restrict__ flag,
-                                                   int a0, float t, int32_t* __restrict__ counts) {
-    const int a = a0 + blockIdx.y;
+__device__ __forceinline__ void sph_count_block(const float* __restrict__ X, const float* __restrict__ Y,
+                                                const float* __restrict__ Z, int64_t n, const float4* __restrict__ coef,
+                                                const int32_t* __restrict__ flag, int a, float t,
+                                                int32_t* __restrict__ count, int64_t base) {
     if (flag[a] != 1) return;
     const float4 c = coef[a];
     __shared__ int part[4];
     int cnt = 0;
-    const int64_t base = (int64_t)blockIdx.x * 2048;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
@@ -110,7 +108,20 @@ __global__ __launch_bounds__(256) void k_sph_count(const float* __restrict__ X, 
     }
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(counts + blockIdx.y, part[0] + part[1] + part[2] + part[3]);
+    if (threadIdx.x == 0) atomicAdd(count, part[0] + part[1] + part[2] + part[3]);
+}
+__global__ __launch_bounds__(256) void k_sph_count(const float* __restrict__ X, const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, int64_t n,
+                                                   const float4* __restrict__ coef, const int32_t* __restrict__ flag,
+                                                   int a0, float t, int32_t* __restrict__ counts) {
+    sph_count_block(X, Y, Z, n, coef, flag, a0 + (int)blockIdx.y, t, counts + blockIdx.y, (int64_t)blockIdx.x * 2048);
+}
+// Several clouds' chunks in one launch: blockIdx.z = the job, blocks past its cloud or its attempts exit.
+__global__ __launch_bounds__(256) void k_sph_count_multi(const CountJob<float4>* __restrict__ jobs, float t) {
+    const CountJob<float4>& j = jobs[blockIdx.z];
+    const int64_t base = (int64_t)blockIdx.x * 2048;
+    if ((int)blockIdx.y >= j.nh || base >= j.cl.n) return;
+    sph_count_block(j.cl.x, j.cl.y, j.cl.z, j.cl.n, j.coef, j.flag, j.a0 + (int)blockIdx.y, t, j.counts + blockIdx.y, base);
 }
 
 struct SphIn {
@@ -147,6 +158,10 @@ struct SphModel {
     void launch_model(hipStream_t s, const PrimCloud& c, const int32_t* tab, int A, float4* coef, int32_t* flag) const {
         hipLaunchKernelGGL(k_sph_model, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, s, c.x, c.y, c.z, tab, A, rmin,
                            rmax, coef, flag);
+    }
+    static constexpr int kCountSpan = 2048;
+    void launch_count_multi(hipStream_t s, const CountJob<float4>* jobs, int nj, int bx, int nh) const {
+        hipLaunchKernelGGL(k_sph_count_multi, dim3((unsigned)bx, (unsigned)nh, (unsigned)nj), dim3(256), 0, s, jobs, t);
     }
     void launch_count(hipStream_t s, const PrimCloud& c, const float4* coef, const int32_t* flag, int a0, int nh,
                       int32_t* cnt) const {
