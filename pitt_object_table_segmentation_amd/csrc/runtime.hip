@@ -14,7 +14,55 @@
 
 #include "ctx.hpp"
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
+
 namespace pitt {
+#if !defined(__HIP_DEVICE_COMPILE__)
+// PointXYZ (x, y, z, pad) -> x[], y[], z[] for m points.  AVX-512 where the host has it (16 points per
+// step: four loads, six two-source permutes, three stores), else one point at a time.
+__attribute__((target("avx512f"))) static void deinterleave4_avx512(const float* src, int64_t m, float* x, float* y,
+                                                                    float* z) {
+    const __m512i ixy = _mm512_setr_epi32(0, 4, 8, 12, 16, 20, 24, 28, 1, 5, 9, 13, 17, 21, 25, 29);
+    const __m512i iz = _mm512_setr_epi32(2, 6, 10, 14, 18, 22, 26, 30, 2, 6, 10, 14, 18, 22, 26, 30);
+    const __m512i lo = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 20, 21, 22, 23);
+    const __m512i hi = _mm512_setr_epi32(8, 9, 10, 11, 12, 13, 14, 15, 24, 25, 26, 27, 28, 29, 30, 31);
+    int64_t i = 0;
+    for (; i + 16 <= m; i += 16) {
+        const float* p = src + 4 * i;
+        const __m512 a0 = _mm512_loadu_ps(p), a1 = _mm512_loadu_ps(p + 16), a2 = _mm512_loadu_ps(p + 32),
+                     a3 = _mm512_loadu_ps(p + 48);
+        const __m512 xy01 = _mm512_permutex2var_ps(a0, ixy, a1), xy23 = _mm512_permutex2var_ps(a2, ixy, a3);
+        const __m512 z01 = _mm512_permutex2var_ps(a0, iz, a1), z23 = _mm512_permutex2var_ps(a2, iz, a3);
+        _mm512_storeu_ps(x + i, _mm512_permutex2var_ps(xy01, lo, xy23));
+        _mm512_storeu_ps(y + i, _mm512_permutex2var_ps(xy01, hi, xy23));
+        _mm512_storeu_ps(z + i, _mm512_permutex2var_ps(z01, lo, z23));
+    }
+    for (; i < m; ++i) {
+        x[i] = src[4 * i];
+        y[i] = src[4 * i + 1];
+        z[i] = src[4 * i + 2];
+    }
+}
+#endif
+static void deinterleave4(const float* src, int64_t m, float* x, float* y, float* z) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    static const bool avx512 = __builtin_cpu_supports("avx512f");
+    if (avx512) {
+        deinterleave4_avx512(src, m, x, y, z);
+        return;
+    }
+#endif
+    for (int64_t i = 0; i < m; ++i) {
+        float q[4];
+        std::memcpy(q, src + 4 * i, sizeof q);
+        x[i] = q[0];
+        y[i] = q[1];
+        z[i] = q[2];
+    }
+}
+
 int plane_segment_batch_impl(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_params* p,
                              pitt_plane_result* results, int32_t* inliers_dev);
 int finish_batch(pitt_ctx* ctx);
@@ -68,6 +116,15 @@ __global__ __launch_bounds__(256) void k_single_planes(const float* __restrict__
         d[i] = stage[b];
         d[cap + i] = stage[b + m];
         d[2 * cap + i] = stage[b + 2 * m];
+    }
+}
+// The caller's AoS cloud (sf floats per point, copied up as it is) -> the frame's planes.
+__global__ __launch_bounds__(256) void k_single_aos(const float* __restrict__ aos, int64_t n, int sf, int64_t cap,
+                                                    float* __restrict__ d) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        d[i] = aos[i * sf];
+        d[cap + i] = aos[i * sf + 1];
+        d[2 * cap + i] = aos[i * sf + 2];
     }
 }
 }  // namespace pitt
@@ -403,19 +460,22 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     const bool timing = ctx->host_timing;
     const double t0 = timing ? pitt::wall_ms() : 0.0;
     const int sf = stride_bytes / 4;
-    for (int64_t b = 0; b < n; b += C) {
+    static const int mode = pitt_env_int("PITT_SINGLE_MODE", 0, 0, 1);  // A/B: 1 = the AoS bytes up as they are
+    if (mode == 1 && n > 0) {
+        float* da = (float*)ctx->buf("single_aos", (size_t)n * stride_bytes);
+        if (!da) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+        PITT_HIP_TRY(hipMemcpyAsync(da, xyz, (size_t)n * stride_bytes, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(pitt::k_single_aos, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0,
+                           ctx->stream, da, n, sf, cap, d);
+        PITT_HIP_TRY(hipGetLastError());
+    }
+    for (int64_t b = 0; mode == 0 && b < n; b += C) {
         const int64_t m = std::min(C, n - b);
         float* hx = h + 3 * b;  // chunk b / C starts at 3 b (every earlier chunk is full)
         float *hy = hx + m, *hz = hx + 2 * m;
         const float* src = xyz + b * sf;
         if (sf == 4) {
-            for (int64_t i = 0; i < m; ++i) {
-                float q[4];
-                std::memcpy(q, src + 4 * i, sizeof q);
-                hx[i] = q[0];
-                hy[i] = q[1];
-                hz[i] = q[2];
-            }
+            pitt::deinterleave4(src, m, hx, hy, hz);
         } else {
             for (int64_t i = 0; i < m; ++i) {
                 hx[i] = src[3 * i];
@@ -426,7 +486,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
         PITT_HIP_TRY(hipMemcpyAsync(ds + 3 * b, hx, (size_t)(3 * m) * sizeof(float), hipMemcpyHostToDevice,
                                     ctx->stream));
     }
-    if (n > 0) {
+    if (mode == 0 && n > 0) {
         hipLaunchKernelGGL(pitt::k_single_planes, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256),
                            0, ctx->stream, ds, n, C, cap, d);
         PITT_HIP_TRY(hipGetLastError());
