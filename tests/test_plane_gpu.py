@@ -107,6 +107,18 @@ def test_single_cloud_api_stride16(ctx):
     assert np.array_equal(m12.inliers, o.inliers)
 
 
+@pytest.mark.parametrize("n", [3, 15, 17, 2049, 65536 + 33, 131072 + 5])
+def test_single_cloud_api_ragged_sizes(ctx, n):
+    """pitt_plane_segment's staging: chunks of 64k points, the deinterleave's 16-point steps and their
+    tails, both strides, against the oracle on the same points."""
+    x, y, z = pitt.synth_frame(0, 4321)
+    x, y, z = x[:n].copy(), y[:n].copy(), z[:n].copy()
+    o = orc.plane_segment(x, y, z)
+    for cloud in (np.stack([x, y, z, np.ones_like(x)], 1), np.stack([x, y, z], 1)):
+        m = ctx.plane_segment(np.ascontiguousarray(cloud, np.float32))
+        assert np.array_equal(m.inliers, o.inliers) and np.array_equal(m.coefficients, o.coefficients), n
+
+
 def _threads():
     return max(1, min(16, len(os.sched_getaffinity(0))))
 
