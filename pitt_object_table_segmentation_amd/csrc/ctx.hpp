@@ -149,6 +149,8 @@ struct pitt_ctx {
     // pitt_plane_segment: points converted (AoS -> SoA) per staged H2D copy; 0 = one copy of the cloud.
     // $PITT_HOST_TIMING=1 prints its host phases to stderr.
     int64_t single_chunk = pitt_env_int("PITT_SINGLE_CHUNK", 1 << 16, 0, 1 << 30);
+    // $PITT_SINGLE_MODE=1: the caller's AoS bytes go up in one pageable copy and the device deinterleaves them
+    int single_mode = pitt_env_int("PITT_SINGLE_MODE", 0, 0, 1);
     bool host_timing = pitt_env_flag("PITT_HOST_TIMING", false);
     struct ChunkHint {
         std::array<uint64_t, 4> key;  // frame planes, frames, hypothesis cap, tiles

@@ -460,7 +460,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     const bool timing = ctx->host_timing;
     const double t0 = timing ? pitt::wall_ms() : 0.0;
     const int sf = stride_bytes / 4;
-    static const int mode = pitt_env_int("PITT_SINGLE_MODE", 0, 0, 1);  // A/B: 1 = the AoS bytes up as they are
+    const int mode = ctx->single_mode;  // 1: the caller's AoS bytes go up as they are (A/B)
     if (mode == 1 && n > 0) {
         float* da = (float*)ctx->buf("single_aos", (size_t)n * stride_bytes);
         if (!da) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
