@@ -149,8 +149,10 @@ struct pitt_ctx {
     // pitt_plane_segment: points converted (AoS -> SoA) per staged H2D copy; 0 = one copy of the cloud.
     // $PITT_HOST_TIMING=1 prints its host phases to stderr.
     int64_t single_chunk = pitt_env_int("PITT_SINGLE_CHUNK", 1 << 16, 0, 1 << 30);
-    // $PITT_SINGLE_MODE=1: the caller's AoS bytes go up in one pageable copy and the device deinterleaves them
-    int single_mode = pitt_env_int("PITT_SINGLE_MODE", 0, 0, 1);
+    // $PITT_SINGLE_MODE bit 0: the caller's AoS bytes go up in one pageable copy and the device deinterleaves
+    // them (else the host deinterleaves into pinned chunks); bit 1: the inliers come down straight into the
+    // caller's memory (else through a pinned copy behind the batch)
+    int single_mode = pitt_env_int("PITT_SINGLE_MODE", 3, 0, 3);
     bool host_timing = pitt_env_flag("PITT_HOST_TIMING", false);
     struct ChunkHint {
         std::array<uint64_t, 4> key;  // frame planes, frames, hypothesis cap, tiles

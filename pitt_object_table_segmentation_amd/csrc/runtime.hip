@@ -461,7 +461,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     const double t0 = timing ? pitt::wall_ms() : 0.0;
     const int sf = stride_bytes / 4;
     const int mode = ctx->single_mode;  // 1: the caller's AoS bytes go up as they are (A/B)
-    if (mode == 1 && n > 0) {
+    if ((mode & 1) && n > 0) {
         float* da = (float*)ctx->buf("single_aos", (size_t)n * stride_bytes);
         if (!da) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
         PITT_HIP_TRY(hipMemcpyAsync(da, xyz, (size_t)n * stride_bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -469,7 +469,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
                            ctx->stream, da, n, sf, cap, d);
         PITT_HIP_TRY(hipGetLastError());
     }
-    for (int64_t b = 0; mode == 0 && b < n; b += C) {
+    for (int64_t b = 0; !(mode & 1) && b < n; b += C) {
         const int64_t m = std::min(C, n - b);
         float* hx = h + 3 * b;  // chunk b / C starts at 3 b (every earlier chunk is full)
         float *hy = hx + m, *hz = hx + 2 * m;
@@ -486,7 +486,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
         PITT_HIP_TRY(hipMemcpyAsync(ds + 3 * b, hx, (size_t)(3 * m) * sizeof(float), hipMemcpyHostToDevice,
                                     ctx->stream));
     }
-    if (mode == 0 && n > 0) {
+    if (!(mode & 1) && n > 0) {
         hipLaunchKernelGGL(pitt::k_single_planes, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256),
                            0, ctx->stream, ds, n, C, cap, d);
         PITT_HIP_TRY(hipGetLastError());
@@ -507,16 +507,22 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     // the inlier list comes back with the batch: a copy of the whole list buffer into pinned memory
     // enqueued behind it (a continuation would enqueue more work after this copy: then copy again)
     const int64_t cont0 = ctx->continuations;
-    if (inliers_out && n > 0) PITT_HIP_TRY(hipMemcpyAsync(hi, di, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    const bool out_staged = !(mode & 2);  // bit 1: the inliers come down straight into the caller's memory
+    if (out_staged && inliers_out && n > 0)
+        PITT_HIP_TRY(hipMemcpyAsync(hi, di, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     rc = pitt_wait(ctx);
     if (rc < 0) return rc;
     const double t2 = timing ? pitt::wall_ms() : 0.0;
     if (r.status < 0) return ctx->fail(r.status, "plane segmentation failed");
     if (r.n_coeff == 0) return PITT_NO_MODEL;
     if (inliers_out && r.n_inliers > 0) {
-        if (ctx->continuations != cont0)
-            PITT_HIP_TRY(hipMemcpy(hi, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
-        std::memcpy(inliers_out, hi, (size_t)r.n_inliers * sizeof(int32_t));
+        if (!out_staged) {
+            PITT_HIP_TRY(hipMemcpy(inliers_out, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
+        } else {
+            if (ctx->continuations != cont0)
+                PITT_HIP_TRY(hipMemcpy(hi, di, (size_t)r.n_inliers * sizeof(int32_t), hipMemcpyDeviceToHost));
+            std::memcpy(inliers_out, hi, (size_t)r.n_inliers * sizeof(int32_t));
+        }
     }
     if (timing)
         std::fprintf(stderr, "pitt_plane_segment n=%lld: convert+enqueue %.3f ms, batch+inliers D2H %.3f ms, copy out %.3f ms\n",
