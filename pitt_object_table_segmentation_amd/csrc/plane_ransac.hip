@@ -9,9 +9,9 @@
 //                   the next chunk's active-frame list on the device (no host round trip)
 //   k_decide        model / refinement decision per frame
 //   k_refine        per frame: winning model's inliers streamed in order into the nine exact-order
-//                   float accumulators + eigen33 (A6, A7) (small batches: the exact walk, xsum.hpp)
-//   k_sel_mark /    the final model's ascending inlier list over the chip, and each frame's
-//   k_sel_write     pitt_plane_result record (back with the chunk stats in one copy)
+//                   float accumulators + eigen33 (A6, A7), then the refined model's ascending
+//                   inlier list (one 2-wave block per frame)
+//   k_finalize      per-frame pitt_plane_result
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2201,35 +2201,23 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     }
 }
 
-__device__ __forceinline__ void write_result(const FrameState& s, const int32_t* __restrict__ hyp_attempt,
-                                             const float4* __restrict__ final_coef, int32_t n_inliers, int hcap, int f,
-                                             pitt_plane_result* __restrict__ res);
-
 __global__ __launch_bounds__(kBlock) void k_sel_write(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, int n_frames, int tiles_max,
     const uint32_t* __restrict__ sel_bits, const int32_t* __restrict__ sel_cnt, int32_t* __restrict__ inliers,
-    int32_t* __restrict__ n_final, uint32_t* __restrict__ acct_tile, const int32_t* __restrict__ hyp_attempt,
-    const float4* __restrict__ final_coef, int hcap, pitt_plane_result* __restrict__ res) {
+    int32_t* __restrict__ n_final, uint32_t* __restrict__ acct_tile) {
     PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
     if (f >= n_frames) return;
     const FrameMeta m = meta[f];
-    if (!st[f].has_model) {  // the record of a frame without a model: its first item writes it
-        if (t == 0 && lane == 0) write_result(st[f], hyp_attempt, final_coef, 0, hcap, f, res);
-        return;
-    }
-    if (t >= m.tiles) return;
+    if (t >= m.tiles || !st[f].has_model) return;
     const int32_t* cnt = sel_cnt + (int64_t)f * tiles_max;
     int pre = 0;
     for (int j = lane; j < t; j += 64) pre += cnt[j];
     pre = __builtin_amdgcn_readfirstlane(wave_sum(pre));
     const int mine = cnt[t];
-    if (t == m.tiles - 1 && lane == 0) {
-        n_final[f] = pre + mine;
-        write_result(st[f], hyp_attempt, final_coef, pre + mine, hcap, f, res);
-    }
+    if (t == m.tiles - 1 && lane == 0) n_final[f] = pre + mine;
     // the earlier tiles' counts, then the tile's bits and its indices
     if (lane == 0 && acct_tile)
         acct_tile[(int64_t)f * tiles_max + t] = 4u * (uint32_t)(t + 1) + (inliers && mine ? 256u + 4u * (uint32_t)mine : 0u);
@@ -2246,10 +2234,13 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
     }
 }
 
-// The frame's result record (k_sel_write's last item of the frame, or its first when it has no model).
-__device__ __forceinline__ void write_result(const FrameState& s, const int32_t* __restrict__ hyp_attempt,
-                                             const float4* __restrict__ final_coef, int32_t n_inliers, int hcap, int f,
-                                             pitt_plane_result* __restrict__ res) {
+__global__ void k_finalize(const FrameState* __restrict__ st, const int32_t* __restrict__ hyp_attempt,
+                           const float4* __restrict__ final_coef, const int32_t* __restrict__ n_final,
+                           int hcap, int n_frames, pitt_plane_result* __restrict__ res) {
+    PITT_DBG_GUARD();
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    const FrameState s = st[f];
     pitt_plane_result r;
     r.status = s.status;
     r.hypotheses = s.it;
@@ -2268,7 +2259,7 @@ __device__ __forceinline__ void write_result(const FrameState& s, const int32_t*
         r.coefficients[2] = c.z;
         r.coefficients[3] = c.w;
         r.n_coeff = 4;
-        r.n_inliers = n_inliers;
+        r.n_inliers = n_final[f];
     } else {
         r.coefficients[0] = r.coefficients[1] = r.coefficients[2] = r.coefficients[3] = 0.0f;
         r.n_coeff = 0;
@@ -2546,11 +2537,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     const size_t acct_off = stat_off + (size_t)(nchunks + 1) * sizeof(ChunkStat);
     const size_t acct_bytes = (size_t)kAcKernels * kAcShards * sizeof(unsigned long long);
     const size_t zero_bytes = acct_off + acct_bytes;
-    // ... and the per-frame result records after it: the counters, chunk stats and records come back in
-    // one copy into the pinned mirror (zblock_h)
-    const size_t res_off = (zero_bytes + 63) & ~(size_t)63;
-    const size_t zall = res_off + (size_t)nf * sizeof(pitt_plane_result);
-    char* zblock = as<char>(ctx->buf("zblock", zall));
+    char* zblock = as<char>(ctx->buf("zblock", zero_bytes));
     int32_t* counters = as<int32_t>(zblock);
     ChunkStat* cstat = as<ChunkStat>(zblock + stat_off);
     // per-kernel byte accounting, only while profiling (the kernels skip the atomics otherwise)
@@ -2570,9 +2557,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float* group_box = as<float>(ctx->buf("group_box", (size_t)nf * tiles_max * (kTile / kGrp) * 8 * sizeof(float)));
     uint32_t* sel_bits = as<uint32_t>(ctx->buf("sel_bits", (size_t)nf * tiles_max * 64 * 4));
     int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
-    if (!zblock) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
-    pitt_plane_result* dres = reinterpret_cast<pitt_plane_result*>(zblock + res_off);
-    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
+    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
     int32_t* xfallback = ctx->xrefine ? as<int32_t>(ctx->buf("xfallback", (size_t)nf * 4)) : nullptr;
     if (ctx->xrefine && !xfallback) return ctx->fail(PITT_E_NOMEM, "refinement flags");
     CovPart* part = nullptr;
@@ -2580,11 +2566,10 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         part = as<CovPart>(ctx->buf("cov_part", (size_t)nf * tiles_max * sizeof(CovPart)));
         if (!part) return ctx->fail(PITT_E_NOMEM, "covariance partials");
     }
-    char* zh = as<char>(ctx->pinned("zblock_h", zall));
-    if (!zh) return ctx->fail(PITT_E_NOMEM, "pinned results");
-    pitt_plane_result* hres = reinterpret_cast<pitt_plane_result*>(zh + res_off);
-    ChunkStat* hstat = reinterpret_cast<ChunkStat*>(zh + stat_off);
-    int32_t* hxfb = reinterpret_cast<int32_t*>(zh) + nchunks + 1;
+    pitt_plane_result* hres = as<pitt_plane_result>(ctx->pinned("results_h", (size_t)nf * sizeof(pitt_plane_result)));
+    ChunkStat* hstat = as<ChunkStat>(ctx->pinned("cstat_h", (size_t)(nchunks + 1) * sizeof(ChunkStat)));
+    int32_t* hxfb = as<int32_t>(ctx->pinned("xfb_h", 16));
+    if (!hxfb) return ctx->fail(PITT_E_NOMEM, "pinned results");
     void* hacct = acct ? ctx->pinned("acct_h", acct_bytes + tile_words * 2 * 4) : nullptr;
     if (!hres || !hstat || (acct && !hacct)) return ctx->fail(PITT_E_NOMEM, "pinned results");
     // $PITT_REFINE_DEBUG: k_refine's per-role cycles and spin counts, summarised on stderr by pitt_wait
@@ -2768,14 +2753,17 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     ctx->prof_end(rec);
     rec = ctx->prof_begin("k_sel_write", 0.0);
     acct_recs[kAcSelWrite] = rec;
-    // (k_sel_write also writes each frame's result record: k_finalize's work, folded in)
     hipLaunchKernelGGL(k_sel_write, dim3(sel_blocks), dim3(kBlock), 0, sm, meta, st, nf, tiles_max, sel_bits, sel_cnt,
-                       inliers_dev, n_final, acct_tiles ? acct_tiles + tile_words : nullptr, hyp_attempt, final_coef,
-                       hcap, dres);
+                       inliers_dev, n_final, acct_tiles ? acct_tiles + tile_words : nullptr);
     PITT_CHECK_LAUNCH("k_sel_write", -1, phase);
     ctx->prof_end(rec);
+    hipLaunchKernelGGL(k_finalize, dim3((nf + 255) / 256), dim3(256), 0, sm, st, hyp_attempt, final_coef, n_final,
+                       hcap, nf, dres);
+    PITT_CHECK_LAUNCH("k_finalize", -1, phase);
     PITT_HIP_TRY(hipGetLastError());
-    PITT_HIP_TRY(hipMemcpyAsync(zh, zblock, zall, hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipMemcpyAsync(hres, dres, (size_t)nf * sizeof(pitt_plane_result), hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipMemcpyAsync(hstat, cstat, (size_t)(nchunks + 1) * sizeof(ChunkStat), hipMemcpyDeviceToHost, sm));
+    PITT_HIP_TRY(hipMemcpyAsync(hxfb, counters + nchunks + 1, 4, hipMemcpyDeviceToHost, sm));
     if (rdbg) PITT_HIP_TRY(hipMemcpyAsync(ctx->refine_dbg_h, rdbg, (size_t)nf * 16 * 8, hipMemcpyDeviceToHost, sm));
     if (acct) {
         PITT_HIP_TRY(hipMemcpyAsync(hacct, acct, acct_bytes, hipMemcpyDeviceToHost, sm));
