@@ -366,7 +366,7 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
             "note": "a step = a device-to-device copy of new frames into the context's buffers, then its batch"}
 
 
-def config2_pass(pitt, ctx, frame, reps=10):
+def config2_pass(pitt, ctx, frame, reps=40):
     """BASELINE config 2: one 640x480 cloud through the single-cloud ABI (pitt_plane_segment: PointXYZ
     host array in, inliers and coefficients back on the host -- the service handler's path, PCIe
     included), median latency of `reps` after 1 warm-up, checked against the oracle."""
