@@ -366,6 +366,9 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
             "note": "a step = a device-to-device copy of new frames into the context's buffers, then its batch"}
 
 
+ORIG_HW_QUEUES = None  # the caller's GPU_MAX_HW_QUEUES, before main() raises it for the pipelined pass
+
+
 def config2_pass(pitt, ctx, frame, reps=40):
     """BASELINE config 2: one 640x480 cloud through the single-cloud ABI (pitt_plane_segment: PointXYZ
     host array in, inliers and coefficients back on the host -- the service handler's path, PCIe
@@ -401,11 +404,33 @@ def config2_pass(pitt, ctx, frame, reps=40):
         if n:
             kern[k] = round(ms / reps * 1e3, 1)
     ctx.profile(False)
-    return {"ms_per_frame": round(float(np.median(ts)), 3), "statistic": f"median of {reps} after 1 warm-up",
-            "inliers": int(len(r.inliers)), "matches_oracle": bool(np.array_equal(r.inliers, o.inliers) and
-                                                                 np.array_equal(r.coefficients, o.coefficients)),
-            "device_resident_ms_per_frame": round(float(np.median(td)), 3),
-            "device_kernels_us": kern}
+    res = {"ms_per_frame_in_bench_process": round(float(np.median(ts)), 3),
+           "statistic": f"median of {reps} after 1 warm-up",
+           "inliers": int(len(r.inliers)), "matches_oracle": bool(np.array_equal(r.inliers, o.inliers) and
+                                                                np.array_equal(r.coefficients, o.coefficients)),
+           "device_resident_ms_per_frame": round(float(np.median(td)), 3),
+           "device_kernels_us": kern}
+    # The service's own process: the same call in a child process with the caller's environment (this
+    # process runs the headline with 8 hardware queues and four contexts' arenas, which cost the one-cloud
+    # call ~10 and ~7 us, tools/gpu_c2c.sh); its result must equal the oracle-checked one above.
+    env = dict(os.environ)
+    if ORIG_HW_QUEUES is None:
+        env.pop("GPU_MAX_HW_QUEUES", None)
+    else:
+        env["GPU_MAX_HW_QUEUES"] = ORIG_HW_QUEUES
+    try:
+        cp = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "config2_run.py"), str(reps), "--json"],
+                            env=env, capture_output=True, text=True, timeout=300)
+        c = json.loads(cp.stdout.strip().splitlines()[-1])
+        same = (c["inliers"] == len(r.inliers) and c["inliers_sum"] == int(np.asarray(r.inliers, np.int64).sum())
+                and np.array_equal(np.asarray(c["coefficients"], np.float32), r.coefficients))
+        res["ms_per_frame"] = c["host_ms"] if same else None
+        res["service_process"] = {"ms_per_frame": c["host_ms"], "device_resident_ms_per_frame": c["device_ms"],
+                                  "same_result": bool(same), "how": "tools/config2_run.py in a child process"}
+    except Exception as e:  # noqa: BLE001 -- reported, the in-process figure stands
+        res["ms_per_frame"] = res["ms_per_frame_in_bench_process"]
+        res["service_process"] = {"error": repr(e)[:200]}
+    return res
 
 
 def config5_pass(pitt, ctx, threads, reps=5):
@@ -590,6 +615,8 @@ def main():
     args = ap.parse_args()
     # $PITT_GRAPHS=1 (opt-in HIP graphs) needs the runtime's graph packet capture off, before HIP starts
     os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+    global ORIG_HW_QUEUES
+    ORIG_HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
     if args.hw_queues > 0:  # hardware queues per process (one per in-flight context's stream); before HIP init
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
