@@ -292,6 +292,10 @@ struct ElmShared {
     float x[N], diag[N], wa1[N], wa2[N], wa3[N], qtf[N], colnorm[N], hstep[N], hc[N], sq[N];
     float R[N][N];                  // R(r, c) = R[c][r]: the QR's top n x n block (column-major)
     float lmS[N][N];                // lmpar's working copy of R for qrsolv (thread 0; in LDS rather than scratch)
+#ifdef PITT_ELM_PROF
+    unsigned long long prof_qrsolv;
+    int prof_lmpar_iter;
+#endif
     int perm[N], transp[N];
     float maxpivot;
     int nonzero_pivots;
@@ -577,30 +581,49 @@ template <int N>
 __device__ void elm_qrsolv(float (&S)[N][N], const int* ipvt, const float* diag, const float* qtb, float* x,
                            float* sdiag) {
     float wa[N];
+#pragma unroll
     for (int j = 0; j < N; ++j) wa[j] = qtb[j];
+#pragma unroll
     for (int j = 0; j < N; ++j) x[j] = S[j][j];
+    // the Givens eliminations on a register copy of S (every index below is a compile-time constant once
+    // the loops are unrolled, so S, sdiag and wa stay in VGPRs instead of one LDS round trip per access)
+    float Sr[N][N], sd[N];
+#pragma unroll
     for (int c = 0; c < N; ++c)
-        for (int r = c + 1; r < N; ++r) S[c][r] = S[r][c];  // strictly lower = upper^T
+#pragma unroll
+        for (int r = 0; r < N; ++r) Sr[c][r] = r > c ? S[r][c] : S[c][r];  // strictly lower = upper^T
+#pragma unroll
+    for (int k = 0; k < N; ++k) sd[k] = sdiag[k];
+#pragma unroll
     for (int j = 0; j < N; ++j) {
         const int l = ipvt[j];
         if (diag[l] == 0.0f) break;
-        for (int k = j; k < N; ++k) sdiag[k] = 0.0f;
-        sdiag[j] = diag[l];
+#pragma unroll
+        for (int k = j; k < N; ++k) sd[k] = 0.0f;
+        sd[j] = diag[l];
         float qtbpj = 0.0f;
+#pragma unroll
         for (int k = j; k < N; ++k) {
             float gc, gs;
-            elm_givens(-S[k][k], sdiag[k], &gc, &gs);
-            S[k][k] = gc * S[k][k] + gs * sdiag[k];
+            elm_givens(-Sr[k][k], sd[k], &gc, &gs);
+            Sr[k][k] = gc * Sr[k][k] + gs * sd[k];
             const float temp = gc * wa[k] + gs * qtbpj;
             qtbpj = -gs * wa[k] + gc * qtbpj;
             wa[k] = temp;
+#pragma unroll
             for (int i = k + 1; i < N; ++i) {
-                const float t2 = gc * S[k][i] + gs * sdiag[i];
-                sdiag[i] = -gs * S[k][i] + gc * sdiag[i];
-                S[k][i] = t2;
+                const float t2 = gc * Sr[k][i] + gs * sd[i];
+                sd[i] = -gs * Sr[k][i] + gc * sd[i];
+                Sr[k][i] = t2;
             }
         }
     }
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+#pragma unroll
+        for (int r = 0; r < N; ++r) S[c][r] = Sr[c][r];
+#pragma unroll
+    for (int k = 0; k < N; ++k) sdiag[k] = sd[k];
     int nsing = 0;
     while (nsing < N && sdiag[nsing] != 0.0f) ++nsing;
     for (int j = nsing; j < N; ++j) wa[j] = 0.0f;
@@ -675,7 +698,14 @@ __device__ void elm_lmpar(ElmShared<F>& s, const float* qtb, float delta, float&
         if (par == 0.0f) par = elm_max(dwarf, 0.001f * paru);
         const float sp = sqrtf(par);
         for (int j = 0; j < N; ++j) wa1[j] = sp * s.diag[j];
+#ifdef PITT_ELM_PROF
+        const unsigned long long tq0 = clock64();
+#endif
         elm_qrsolv<N>(S, s.perm, wa1, qtb, x, sdiag);
+#ifdef PITT_ELM_PROF
+        s.prof_qrsolv += clock64() - tq0;
+        ++s.prof_lmpar_iter;
+#endif
         for (int j = 0; j < N; ++j) wa2[j] = s.diag[j] * x[j];
         dxnorm = elm_blue1(wa2, N);
         float temp = fp;
@@ -741,6 +771,10 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
     constexpr int maxfev = 400;
     const float neps = sqrtf(elm_max(0.0f, FLT_EPSILON));  // NumericalDiff: sqrt(max(epsfcn, eps))
     if (tid == 0) {
+#ifdef PITT_ELM_PROF
+        s.prof_qrsolv = 0;
+        s.prof_lmpar_iter = 0;
+#endif
         for (int k = 0; k < N; ++k) s.x[k] = j.start[k];
         F::prep(s.x, s.pre[N]);
         s.cur = 0;
@@ -964,10 +998,10 @@ __global__ __launch_bounds__(kElmThreads) void k_elm(const ElmJob* __restrict__ 
 #ifdef PITT_ELM_PROF
     if (tid == 0)
         printf("PITT_ELM_PROF N %d m %lld outer %d inner %d nfev %d status %d cycles: jacobian %llu qr %llu post %llu "
-               "lmpar %llu eval %llu stable %llu logic %llu | qr: norms %llu pivnorm %llu swap %llu gemv %llu update %llu "
-               "downdate %llu\n",
-               N, (long long)m, n_outer, n_inner, s.nfev, s.status, pc[0], pc[2], pc[3], pc[5], pc[6], pc[7], pc[4],
-               qprof[0], qprof[1], qprof[2], qprof[3], qprof[4], qprof[5]);
+               "lmpar %llu (qrsolv %llu in %d iterations) eval %llu stable %llu logic %llu | qr: norms %llu pivnorm %llu "
+               "swap %llu gemv %llu update %llu downdate %llu\n",
+               N, (long long)m, n_outer, n_inner, s.nfev, s.status, pc[0], pc[2], pc[3], pc[5], s.prof_qrsolv,
+               s.prof_lmpar_iter, pc[6], pc[7], pc[4], qprof[0], qprof[1], qprof[2], qprof[3], qprof[4], qprof[5]);
 #endif
 #undef PITT_ELM_T
     if (tid == 0) {
