@@ -2280,6 +2280,14 @@ __device__ __forceinline__ bool xr_eligible(const FrameState& s, int phase) {
 }
 
 // per (frame, tile) wave: the tile's inliers of the winning model
+// The walk's producers take each tile in kXrSplit parts, one wave each (a one-frame batch has only ~150
+// tiles: whole-tile waves left the chip nearly idle and each wave walked 32 dependent groups).
+#ifndef PITT_XR_SPLIT
+#define PITT_XR_SPLIT 8
+#endif
+constexpr int kXrSplit = PITT_XR_SPLIT;
+constexpr int kXrGroups = kTile / 64 / kXrSplit;  // 64-point groups per part
+
 template <int ORDER>
 __global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X, const float* __restrict__ Y,
                                                      const float* __restrict__ Z, const FrameMeta* __restrict__ meta,
@@ -2289,7 +2297,8 @@ __global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X
     PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    const int f = it / tiles_max, t = it - f * tiles_max;
+    const int ts = tiles_max * kXrSplit;  // items per frame: kXrSplit parts of each tile
+    const int f = it / ts, q = it - f * ts, t = q / kXrSplit, part = q - t * kXrSplit;
     if (f >= n_frames) return;
     const FrameMeta m = meta[f];
     int cnt = 0;
@@ -2297,13 +2306,13 @@ __global__ __launch_bounds__(kBlock) void k_xr_count(const float* __restrict__ X
         const float4 c = best_coef[f];
         float tv;
         asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
-        for (int g = 0; g < kTile / 64; ++g) {
+        for (int g = part * kXrGroups; g < (part + 1) * kXrGroups; ++g) {
             const int64_t i = (int64_t)t * kTile + 64 * g + lane;
             const bool in = i < m.n && fabsf(plane_dot<ORDER>(c, X[m.off + i], Y[m.off + i], Z[m.off + i])) < tv;
             cnt += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in));
         }
     }
-    if (lane == 0) tcnt[(int64_t)f * tiles_max + t] = cnt;
+    if (lane == 0) tcnt[(int64_t)f * ts + q] = cnt;
 }
 
 // one block per frame: the tiles' inlier offsets, the frame's segment (first block: the previous frames'
@@ -2321,9 +2330,10 @@ __global__ __launch_bounds__(256) void k_xr_scan(const FrameMeta* __restrict__ m
         for (int g = 0; g < f; ++g) b += (meta[g].n + kXsBlk - 1) / kXsBlk;
         base = b;
     }
-    int32_t* c = tcnt + (int64_t)f * tiles_max;
-    const int per = (m.tiles + 255) / 256;
-    const int a = (int)threadIdx.x * per, e = min(a + per, m.tiles);
+    int32_t* c = tcnt + (int64_t)f * tiles_max * kXrSplit;
+    const int parts = m.tiles * kXrSplit;
+    const int per = (parts + 255) / 256;
+    const int a = (int)threadIdx.x * per, e = min(a + per, parts);
     int acc = 0;
     for (int i = a; i < e; ++i) acc += c[i];
     part[threadIdx.x] = acc;
@@ -2359,15 +2369,16 @@ __global__ __launch_bounds__(kBlock) void k_xr_write(const float* __restrict__ X
     PITT_DBG_GUARD();
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    const int f = it / tiles_max, t = it - f * tiles_max;
+    const int ts = tiles_max * kXrSplit;
+    const int f = it / ts, q = it - f * ts, t = q / kXrSplit, part = q - t * kXrSplit;
     if (f >= n_frames) return;
     const FrameMeta m = meta[f];
     if (t >= m.tiles || !xr_eligible(st[f], phase)) return;
     const float4 c = best_coef[f];
     float tv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
-    int64_t pos = seg[f].blk0 * kXsBlk + toff[(int64_t)f * tiles_max + t];
-    for (int g = 0; g < kTile / 64; ++g) {
+    int64_t pos = seg[f].blk0 * kXsBlk + toff[(int64_t)f * ts + q];
+    for (int g = part * kXrGroups; g < (part + 1) * kXrGroups; ++g) {
         const int64_t i = (int64_t)t * kTile + 64 * g + lane;
         float x = 0.0f, y = 0.0f, z = 0.0f;
         bool in = false;
@@ -2596,7 +2607,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     XsScratch xr_scr;
     if (xs) {
         xr_v = as<float>(ctx->buf("xr_v", (size_t)9 * xs_T * 4));
-        xr_tcnt = as<int32_t>(ctx->buf("xr_tcnt", (size_t)nf * tiles_max * 4));
+        xr_tcnt = as<int32_t>(ctx->buf("xr_tcnt", (size_t)nf * tiles_max * kXrSplit * 4));
         xr_bseg = as<int32_t>(ctx->buf("xr_bseg", (size_t)(xs_T / kXsBlk) * 4));
         xr_seg = as<XsSeg>(ctx->buf("xr_seg", (size_t)nf * sizeof(XsSeg)));
         xr_sums = as<float>(ctx->buf("xr_sums", (size_t)nf * 9 * 4));
@@ -2688,12 +2699,13 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         ctx->prof_end(rec);
     } else if (xs) {  // small batch: the nine sums by the exact walk over the chip
         rec = ctx->prof_begin("k_refine:xsum", 0.0);
-        hipLaunchKernelGGL((k_xr_count<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
+        const int xr_blocks = (int)(((int64_t)nf * tiles_max * kXrSplit + kWaves - 1) / kWaves);
+        hipLaunchKernelGGL((k_xr_count<ORDER>), dim3(xr_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
                            thf, nf, tiles_max, xr_tcnt, phase);
     PITT_CHECK_LAUNCH("k_xr_count", -1, phase);
         hipLaunchKernelGGL(k_xr_scan, dim3(nf), dim3(256), 0, sm, meta, tiles_max, xr_tcnt, xr_seg, xr_bseg);
     PITT_CHECK_LAUNCH("k_xr_scan", -1, phase);
-        hipLaunchKernelGGL((k_xr_write<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
+        hipLaunchKernelGGL((k_xr_write<ORDER>), dim3(xr_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st, best_coef,
                            thf, nf, tiles_max, xr_tcnt, xr_seg, xr_v, xs_T, phase);
     PITT_CHECK_LAUNCH("k_xr_write", -1, phase);
         xs_enqueue(sm, xr_v, xs_T, 9, nf, xr_seg, xr_bseg, xr_sums, xr_scr);

@@ -40,10 +40,17 @@ with pitt.Context(0) as ctx:
         ctx.plane_segment_batch(b, pitt.sac_params(), out)
         td.append((time.perf_counter() - t) * 1e3)
     m = ctx.plane_segment(cloud)
+    ctx.profile(True)
+    ctx.profile_reset()
+    for _ in range(reps):
+        ctx.plane_segment_batch(b, pitt.sac_params(), out)
+    kern = {k: round(ctx.profile_get(k)[1] / reps * 1e3, 1) for k in ("k_score", "k_refine:xsum", "k_sel_mark")}
+    ctx.profile(False)
 if "--json" in sys.argv:  # for bench.py, which runs this in a child process
     import json
     print(json.dumps({"host_ms": round(float(np.median(ts)), 3), "device_ms": round(float(np.median(td)), 3),
                       "inliers": int(len(m.inliers)), "inliers_sum": int(np.asarray(m.inliers, np.int64).sum()),
                       "coefficients": [float(c) for c in m.coefficients]}))
 else:
-    print(f"config2 host ABI {np.median(ts):.3f} ms, device-resident batch {np.median(td):.3f} ms (medians of {reps})")
+    print(f"config2 host ABI {np.median(ts):.3f} ms, device-resident batch {np.median(td):.3f} ms (medians of {reps}); "
+          f"kernels us {kern}")
