@@ -369,7 +369,7 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
 ORIG_HW_QUEUES = None  # the caller's GPU_MAX_HW_QUEUES, before main() raises it for the pipelined pass
 
 
-def config2_pass(pitt, ctx, frame, reps=40):
+def config2_pass(pitt, ctx, frame, reps=200):
     """BASELINE config 2: one 640x480 cloud through the single-cloud ABI (pitt_plane_segment: PointXYZ
     host array in, inliers and coefficients back on the host -- the service handler's path, PCIe
     included), median latency of `reps` after 1 warm-up, checked against the oracle."""
