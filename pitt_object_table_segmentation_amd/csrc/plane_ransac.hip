@@ -276,6 +276,9 @@ constexpr int kWaves = kBlock / 64;
 #define PITT_SCORE_WAVES 2
 #endif
 constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score block
+#ifndef PITT_SCORE_DEPTH
+#define PITT_SCORE_DEPTH 2  // register sets of points in flight in k_score (3: an A/B variant)
+#endif
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 #ifndef PITT_SCORE_GRID_CAP
 #define PITT_SCORE_GRID_CAP (256 * 32)
@@ -763,6 +766,25 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
         store_lane_counts(cnt, Hf, lane, tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0);
         (void)rounds;
     } else {
+#if PITT_SCORE_DEPTH == 3
+    // three register sets: sub-steps s + 1 and s + 2 are in flight while s is scored
+    static_assert(kSubs == 8, "the 3-deep rotation below is written for 8 sub-steps");
+    SubPts P2;
+    load_sub(X, Y, Z, cur.base + kSub, lane, P[1]);
+    for (int s = 0; s < 6; s += 3) {
+        load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P2);
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
+                              gsrc + 128u * s);
+        load_sub(X, Y, Z, cur.base + (s + 3) * kSub, lane, P[0]);
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
+                              gsrc + 128u * (s + 1));
+        load_sub(X, Y, Z, cur.base + (s + 4) * kSub, lane, P[1]);
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P2, cur.rem - (s + 2) * kSub, tv, lane, wc, tb, gb + (s + 2) * kGPS * 8,
+                              gsrc + 128u * (s + 2));
+    }
+    score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - 6 * kSub, tv, lane, wc, tb, gb + 6 * kGPS * 8, gsrc + 128u * 6);
+    score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - 7 * kSub, tv, lane, wc, tb, gb + 7 * kGPS * 8, gsrc + 128u * 7);
+#else
     // sub-steps in pairs: the next sub-step loads into the other register set while this one is
     // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
     for (int s = 0; s < kSubs; s += 2) {
@@ -773,6 +795,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
         score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
                               gsrc + 128u * (s + 1));
     }
+#endif
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
     asm volatile("" ::: "memory");
     int32_t* out = tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0;
