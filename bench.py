@@ -601,6 +601,8 @@ def main():
     # frames/s against 355.2k at 3 in flight on the box's default 4 queues; 4 in flight sharing 4
     # queues measured 287.4k)
     ap.add_argument("--pipeline", type=int, default=4, help="contexts/streams with batches in flight")
+    ap.add_argument("--settle-steps", type=int, default=300,
+                    help="untimed pipelined steps before the warm-up steps (GPU clocks settle; DESIGN.md s6)")
     ap.add_argument("--parts", type=int, default=1,
                     help="world 1: each step's batch split over this many contexts (the same frames and work per "
                          "step, several steps in flight); the roofline and extra passes keep whole batches")
@@ -752,10 +754,9 @@ def main():
     for i in range(len(ctxs)):
         for _ in range(2):
             ctxs[i].plane_segment_batch(batches[i], params, outs[i])
-    for _ in range(args.warmup):
-        timed_step()
-    timed_drain()
-    # parity spot check outside the timed region (first frame of this rank vs the oracle)
+    # parity spot check outside the timed region (first frame of this rank vs the oracle), before the
+    # warm-up steps: the oracle's CPU time leaves the GPU idle, and the timed region should start on
+    # the clocks the warm-up steps brought up, not on an idle GPU's
     if rank == 0:
         res0 = ctx.plane_segment_batch(batches[0], params, outs[0])
         o = oracle().plane_segment(*frames0[0])
@@ -763,6 +764,18 @@ def main():
               and res0[0]["hypotheses"] == o.hypotheses)
         log(f"[rank 0] parity frame 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'} "
             f"(T={int(res0[0]['hypotheses'])}, inliers={int(res0[0]['n_inliers'])})")
+    if world > 1:
+        dist.barrier()
+    # settle, then warm up: --settle-steps pipelined untimed steps before the W warm-up steps.  After
+    # the setup's serial batches and the oracle's CPU time the GPU has been idle or lightly loaded, and
+    # the first tens of milliseconds of pipelined work run slower per step (clocks and power settling):
+    # 20 timed steps measured 358-362k frames/s after 5 warm-up steps, 382-391k after 50 and 394-396k
+    # after 300 (tools/gpu_warm.sh).  The timed steps are unchanged.
+    for _ in range(args.settle_steps):
+        timed_step()
+    for _ in range(args.warmup):
+        timed_step()
+    timed_drain()
 
     # ---- timed throughput pass: K steps, batches overlapped on the contexts' streams ----
     if world > 1:
@@ -833,6 +846,7 @@ def main():
                 "points_per_frame": W * H,
                 "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU"
                                + (f", each split over {parts} contexts" if parts > 1 else ""),
+                "untimed_before_timed": {"settle_steps": args.settle_steps, "warmup_steps": args.warmup},
                 "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
                 "world_size_seen": world,
                 "collective": (f"{backend} all_gather_into_tensor of per-frame records, async (collected one "

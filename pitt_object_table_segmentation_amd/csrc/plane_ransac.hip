@@ -279,6 +279,11 @@ constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score bloc
 #ifndef PITT_SCORE_DEPTH
 #define PITT_SCORE_DEPTH 2  // register sets of points in flight in k_score (3: an A/B variant)
 #endif
+#ifndef PITT_SCORE_MERGE
+#define PITT_SCORE_MERGE 0  // 1: two 16-hypothesis rounds per pass, 32-entry survivor lists (A/B variant)
+#endif
+constexpr bool kScoreMerge = PITT_SCORE_MERGE != 0;
+constexpr int kListRows = kScoreMerge ? 32 : 16;  // LDS rows of one group's survivor list
 constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST <= 4)
 #ifndef PITT_SCORE_GRID_CAP
 #define PITT_SCORE_GRID_CAP (256 * 32)
@@ -497,6 +502,29 @@ __device__ __forceinline__ void score_list(uint32_t lb, int c, float x, float y,
 #undef PITT_LIST_OPERANDS
 }
 
+// PITT_SCORE_MERGE: the same over a 32-entry list (two rounds' survivors of group GR, lb + 512 GR);
+// entry k's count lands in lane 16 GR + k of vc (k < 16) or lane 16 GR + k - 16 of vc2.
+template <int ORDER, int GR>
+__device__ __forceinline__ void score_list32(uint32_t lb, int c, float x, float y, float z, float tv, int& vc,
+                                             int& vc2) {
+    if (c == 0) return;
+    uint32_t base;
+    asm("v_mov_b32 %0, %1" : "=v"(base) : "s"(lb + 512u * GR));
+    float d0, t0, d1, t1;
+    uint64_t m0, m1;
+    uint32_t n0, n1;
+#define PITT_LIST_OPERANDS                                                                              \
+    : [d0] "=&v"(d0), [t0] "=&v"(t0), [d1] "=&v"(d1), [t1] "=&v"(t1), [m0] "=&s"(m0), [m1] "=&s"(m1),  \
+      [n0] "=&s"(n0), [n1] "=&s"(n1), [vc] "+v"(vc), [vc2] "+v"(vc2)                                    \
+    : [base] "v"(base), [c] "s"(c), [x] "v"(x), [y] "v"(y), [z] "v"(z), [tv] "v"(tv), [L] "n"(16 * GR) \
+    : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69",  \
+      "v70", "v71", "scc", "memory"
+    if constexpr (ORDER == 0) asm volatile(PITT_SCORE_LIST32_ASM_0 PITT_LIST_OPERANDS);
+    else if constexpr (ORDER == 1) asm volatile(PITT_SCORE_LIST32_ASM_1 PITT_LIST_OPERANDS);
+    else asm volatile(PITT_SCORE_LIST32_ASM_2 PITT_LIST_OPERANDS);
+#undef PITT_LIST_OPERANDS
+}
+
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
 // INS: a pair whose box lies certainly inside the slab (box_inside) is not scored point by point;
 // it counts the group's points with no NaN coordinate (gcnt, one ballot per group and sub-step).
@@ -555,7 +583,48 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
     }
     const RowGeo G = row_geo(B);
     const int rounds = (Hf + kRnd - 1) / kRnd;
-    const uint32_t lrow = (uint32_t)(uintptr_t)wl + 256u * (uint32_t)(lane >> 4);  // this lane's group list
+    const uint32_t lrow = (uint32_t)(uintptr_t)wl + 16u * kListRows * (uint32_t)(lane >> 4);  // this lane's group list
+    if constexpr (kScoreMerge && !INS) {
+        // rounds r, r + 1 in one pass: round r's survivors of group g take list slots 0.. in ascending
+        // order, round r + 1's follow them (slot = round r's survivor count of the row + rank)
+        const uint32_t lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)wl);
+        for (int r = 0; r < rounds; r += 2) {
+            const int hl = kRnd * r + (lane & (kRnd - 1));
+            const float4 c0 = cl[min(hl, Hf - 1)];
+            const float4 c1 = cl[min(hl + kRnd, Hf - 1)];
+            const int nb0 = min(kRnd, Hf - kRnd * r);
+            const int nb1 = max(0, min(kRnd, Hf - kRnd * (r + 1)));
+            const uint64_t valid0 = (((uint64_t)1 << nb0) - 1) * 0x0001000100010001ull;
+            const uint64_t valid1 = (((uint64_t)1 << nb1) - 1) * 0x0001000100010001ull;
+            const uint64_t need0 = __builtin_amdgcn_ballot_w64(!box_clear(G, c0, tv)) & valid0;
+            const uint64_t need1 = __builtin_amdgcn_ballot_w64(!box_clear(G, c1, tv)) & valid1;
+            if ((need0 | need1) == 0) continue;
+            const uint32_t below = (1u << (lane & 15)) - 1u;
+            const uint32_t row0 = (uint32_t)(need0 >> (lane & 48)) & 0xFFFFu;
+            const uint32_t row1 = (uint32_t)(need1 >> (lane & 48)) & 0xFFFFu;
+            const bool mine0 = (row0 >> (lane & 15)) & 1u, mine1 = (row1 >> (lane & 15)) & 1u;
+            const int k0 = __builtin_popcount(row0 & below);
+            const int k1 = __builtin_popcount(row0) + __builtin_popcount(row1 & below);
+            if (mine0) *(__attribute__((address_space(3))) f4v*)(uintptr_t)(lrow + 16u * (uint32_t)k0) = f4v{c0.x, c0.y, c0.z, c0.w};
+            if (mine1) *(__attribute__((address_space(3))) f4v*)(uintptr_t)(lrow + 16u * (uint32_t)k1) = f4v{c1.x, c1.y, c1.z, c1.w};
+            int vc = 0, vc2 = 0;
+#define PITT_ROWC(g) (__builtin_popcount((uint32_t)(need0 >> (16 * (g))) & 0xFFFFu) + \
+                      __builtin_popcount((uint32_t)(need1 >> (16 * (g))) & 0xFFFFu))
+            score_list32<ORDER, 0>(lb, PITT_ROWC(0), P.x[0], P.y[0], P.z[0], tv, vc, vc2);
+            score_list32<ORDER, 1>(lb, PITT_ROWC(1), P.x[1], P.y[1], P.z[1], tv, vc, vc2);
+            score_list32<ORDER, 2>(lb, PITT_ROWC(2), P.x[2], P.y[2], P.z[2], tv, vc, vc2);
+            score_list32<ORDER, 3>(lb, PITT_ROWC(3), P.x[3], P.y[3], P.z[3], tv, vc, vc2);
+#undef PITT_ROWC
+            // back to the hypothesis lanes: round r's count from slot k0 (< 16, in vc), round r + 1's
+            // from slot k1 (vc below 16, vc2 from 16)
+            const int got0 = __builtin_amdgcn_ds_bpermute(4 * ((lane & 48) + k0), vc);
+            const int ga = __builtin_amdgcn_ds_bpermute(4 * ((lane & 48) + (k1 & 15)), vc);
+            const int gb = __builtin_amdgcn_ds_bpermute(4 * ((lane & 48) + (k1 & 15)), vc2);
+            wc[64 * r + lane] += mine0 ? got0 : 0;
+            if (r + 1 < rounds) wc[64 * (r + 1) + lane] += mine1 ? (k1 < 16 ? ga : gb) : 0;
+        }
+        return;
+    }
     for (int r = 0; r < rounds; ++r) {
         const int hl = kRnd * r + (lane & (kRnd - 1));
         const float4 cr = cl[min(hl, Hf - 1)];
@@ -725,7 +794,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void k_score(
     float* __restrict__ group_box) {
     PITT_DBG_GUARD();
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
-    __shared__ float4 wlist[kScoreWaves][64];  // four 16-entry survivor lists, one per group
+    __shared__ float4 wlist[kScoreWaves][4 * kListRows];  // four survivor lists, one per group
     __shared__ float4 wbox[kScoreWaves][BOX ? 1 : 64];  // later chunks: the item's 32 group boxes
     __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;

@@ -195,7 +195,7 @@ def test_config4_sharded_hip_path_equals_single_batch(ctx):
 def _run_bench(world, frames_per_gpu, dump, port, steps=4, pipeline=2, extra=()):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    common = ["--steps", str(steps), "--warmup", "1", "--pipeline", str(pipeline), "--frames-per-gpu",
+    common = ["--steps", str(steps), "--warmup", "1", "--settle-steps", "0", "--pipeline", str(pipeline), "--frames-per-gpu",
               str(frames_per_gpu), "--no-extras", "--no-cpu-baseline", "--dump-records", dump] + list(extra)
     if world == 1:
         cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "1"] + common
