@@ -280,7 +280,7 @@ constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score bloc
 #define PITT_SCORE_DEPTH 2  // register sets of points in flight in k_score (3: an A/B variant)
 #endif
 #ifndef PITT_SCORE_MERGE
-#define PITT_SCORE_MERGE 0  // 1: two 16-hypothesis rounds per pass, 32-entry survivor lists (A/B variant)
+#define PITT_SCORE_MERGE 1  // two 16-hypothesis rounds per pass, 32-entry survivor lists (0: one round per pass)
 #endif
 constexpr bool kScoreMerge = PITT_SCORE_MERGE != 0;
 constexpr int kListRows = kScoreMerge ? 32 : 16;  // LDS rows of one group's survivor list
@@ -477,7 +477,7 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 // The surviving hypotheses of group GR, compacted in ascending order into its 16-entry LDS list
-// (lb + 256 GR): entry k is scored in PCL's float order and its count written to lane 16 GR + k of
+// (lb + 16 kListRows GR): entry k is scored in PCL's float order and its count written to lane 16 GR + k of
 // vc (PCL order A3, no FMA).  Hand-scheduled (tools/gen_score_asm.py -> score_list_asm.inc): two
 // entries per step as two interleaved chains, the next two rows already in flight, an odd list's
 // first entry alone; the lane of every count is an immediate (no m0), so the scalar work per entry
@@ -486,7 +486,7 @@ template <int ORDER, int GR>
 __device__ __forceinline__ void score_list(uint32_t lb, int c, float x, float y, float z, float tv, int& vc) {
     if (c == 0) return;
     uint32_t base;  // ds_read's address operand lives in a VGPR
-    asm("v_mov_b32 %0, %1" : "=v"(base) : "s"(lb + 256u * GR));
+    asm("v_mov_b32 %0, %1" : "=v"(base) : "s"(lb + 16u * kListRows * GR));
     float d0, t0, d1, t1;
     uint64_t m0, m1;
     uint32_t n0, n1;

@@ -9,7 +9,7 @@ STEPS=${2:-5}
 cd /tmp && export TMPDIR=/tmp
 OUT="$ROOTDIR/gpurun_out"
 mkdir -p "$OUT"
-BENCH="$ROOTDIR/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-extras"
+BENCH="$ROOTDIR/bench.py --steps $STEPS --warmup 1 --settle-steps 0 --no-cpu-baseline --no-extras"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${TAG}_trace" -o trace -f csv -- python3 $BENCH \
     > "$OUT/prof_${TAG}_trace.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_score' -d "$OUT/prof_${TAG}_fetch" -o fetch -f csv \
