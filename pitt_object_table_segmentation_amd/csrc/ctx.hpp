@@ -146,6 +146,12 @@ struct pitt_ctx {
     // batches of up to this many frames refine through the chip-wide exact walk (xsum.hpp) instead of
     // k_refine's per-frame chain (same sums, lower latency); $PITT_XS_MAX_FRAMES=0 keeps the chain always
     int xs_max_frames = pitt_env_int("PITT_XS_MAX_FRAMES", 8, 0, 1 << 30);
+    // Early refinement ($PITT_EARLY_REFINE=1, off by default): when a batch launches two or more scoring
+    // chunks, the frames that finished in the first are decided and refined on side[0] while the later
+    // chunks score the rest (direct launches only; graph captures and profiled runs keep one stream).
+    // Bit-exact, but measured slower on the pipelined headline.
+    bool early_refine = pitt_env_flag("PITT_EARLY_REFINE", false);
+    hipEvent_t er_ev[2] = {nullptr, nullptr};  // first-chunk decisions made | early refinement done
     // pitt_plane_segment: points converted (AoS -> SoA) per staged H2D copy; 0 = one copy of the cloud.
     // $PITT_HOST_TIMING=1 prints its host phases to stderr.
     int64_t single_chunk = pitt_env_int("PITT_SINGLE_CHUNK", 1 << 16, 0, 1 << 30);

@@ -2724,11 +2724,25 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     // everything the launches use, by value: a continuation runs after this call has returned
     const float *fx = fr->x, *fy = fr->y, *fz = fr->z;
     const int optimize = p->optimize ? 1 : 0, cov_mode = p->cov_mode;
+    // early refinement (ctx.hpp): the first chunk's finished frames refine on side[0] during the later chunks
+#ifdef PITT_AB_VARIANTS
+    const bool er_refine_default = ctx->refine_producers == 1 && ctx->refine_frames == 1 && !ctx->xrefine && !rdbg;
+#else
+    const bool er_refine_default = true;
+#endif
+    const bool er_base = ctx->early_refine && er_refine_default && !ctx->prof && K >= 2 && optimize &&
+                         cov_mode != PITT_COV_FAST && !xs;
+    if (er_base) {
+        if (!ctx->side[0]) PITT_HIP_TRY(hipStreamCreateWithFlags(&ctx->side[0], hipStreamNonBlocking));
+        for (hipEvent_t& e : ctx->er_ev)
+            if (!e) PITT_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     // chunks [c0, c1) with their replays (front: the state reset and first hypotheses before them), then
     // phase `phase`'s decisions, refinements, the final selection and the result copies
     auto enqueue = [=](int c0, int c1, int phase, bool front, std::vector<int>& acct_recs,
-                       std::vector<int>& score_recs) -> int {
+                       std::vector<int>& score_recs, bool er = false) -> int {
     int rec;
+    bool er_launched = false;
     if (front) {
     PITT_HIP_TRY(hipMemsetAsync(zblock, 0, zero_bytes, sm));
     rec = ctx->prof_begin("k_hypothesize", 0.0);
@@ -2776,6 +2790,24 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
                            hyp_attempt, acct);
     PITT_CHECK_LAUNCH("k_replay", c, phase);
         ctx->prof_end(rec);
+        if (er && c == 0 && c1 >= 2) {
+            // the frames done after the first chunk (the ones with the most inliers: they need the fewest
+            // hypotheses) are decided now, as phase 3, and refined on the side stream while the later
+            // chunks score the rest.  Nothing later on this stream touches them: k_replay and k_score
+            // skip done frames, k_decide skips decided ones, k_refine below takes phase 1 only; the
+            // selection waits for the side stream.
+            hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
+                               optimize, best_coef, final_coef, 3);
+            PITT_CHECK_LAUNCH("k_decide", -1, 3);
+            PITT_HIP_TRY(hipEventRecord(ctx->er_ev[0], sm));
+            PITT_HIP_TRY(hipStreamWaitEvent(ctx->side[0], ctx->er_ev[0], 0));
+            hipLaunchKernelGGL((k_refine<ORDER, DIV, 1>), dim3(nf), dim3(64 * 3), 0, ctx->side[0], fx, fy, fz, meta,
+                               st, best_coef, thf, tile_counts, hstride, tiles_max, final_coef, acct,
+                               (unsigned long long*)nullptr, 2, (const int32_t*)nullptr, 3);
+            PITT_CHECK_LAUNCH("k_refine", -1, 3);
+            PITT_HIP_TRY(hipEventRecord(ctx->er_ev[1], ctx->side[0]));
+            er_launched = true;
+        }
     }
     hipLaunchKernelGGL(k_decide, dim3((nf + 255) / 256), dim3(256), 0, sm, meta, st, hyp_coef, hcap, nf,
                        optimize, best_coef, final_coef, phase);
@@ -2849,6 +2881,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         }
 #endif
     }
+    if (er_launched) PITT_HIP_TRY(hipStreamWaitEvent(sm, ctx->er_ev[1], 0));  // the early refinements
     rec = ctx->prof_begin("k_sel_mark", 0.0);
     acct_recs[kAcSelMark] = rec;
     hipLaunchKernelGGL((k_sel_mark<ORDER>), dim3(sel_blocks), dim3(kBlock), 0, sm, fx, fy, fz, meta, st,
@@ -2875,7 +2908,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     }
     return PITT_OK;
     };
-    auto enqueue_front = [&]() -> int { return enqueue(0, K, 1, true, acct_recs, score_recs); };
+    auto enqueue_front = [&](bool er) -> int { return enqueue(0, K, 1, true, acct_recs, score_recs, er); };
 #ifdef PITT_SYNC_CHECK
     *(volatile unsigned int*)dbg_seq = seq;
 #endif
@@ -2907,7 +2940,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
             } else {
                 hipGraph_t graph = nullptr;
                 PITT_HIP_TRY(hipStreamBeginCapture(sm, hipStreamCaptureModeRelaxed));
-                const int erc = enqueue_front();
+                const int erc = enqueue_front(false);  // a graph keeps one stream
                 const hipError_t ce = hipStreamEndCapture(sm, &graph);
                 if (erc) {
                     if (graph) (void)hipGraphDestroy(graph);
@@ -2957,11 +2990,11 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
 #endif
             ++ctx->graph_replays;
         } else {
-            const int erc = enqueue_front();
+            const int erc = enqueue_front(er_base);
             if (erc) return erc;
         }
     } else {
-        const int erc = enqueue_front();
+        const int erc = enqueue_front(er_base);
         if (erc) return erc;
     }
 #ifdef PITT_SYNC_CHECK

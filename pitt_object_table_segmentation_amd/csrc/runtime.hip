@@ -333,6 +333,8 @@ void pitt_destroy(pitt_ctx* ctx) {
         (void)hipEventDestroy(r.b);
     }
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->er_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipStream_t& sd : ctx->side)
         if (sd) {
             (void)hipStreamSynchronize(sd);
