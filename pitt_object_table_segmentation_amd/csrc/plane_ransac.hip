@@ -785,8 +785,16 @@ __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__
 
 // BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
 // -- for k_refine's tile skipping.
+#ifndef PITT_SCORE_WPE
+#define PITT_SCORE_WPE 0  // > 0: k_score's register budget set for this many waves per SIMD (an A/B variant)
+#endif
+#if PITT_SCORE_WPE > 0
+#define PITT_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(PITT_SCORE_WPE, PITT_SCORE_WPE)))
+#else
+#define PITT_SCORE_ATTR
+#endif
 template <int ORDER, int NST, bool BOX, bool LANE = false, bool INS = false>
-__global__ __launch_bounds__(64 * kScoreWaves) void k_score(
+__global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
