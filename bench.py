@@ -6,8 +6,13 @@ the final ascending inlier list, results on the host; with N > 1 ranks the per-f
 records are gathered over RCCL (config 4).  Inputs are resident in HBM before the timed region;
 each in-flight context segments its own batch (distinct frames, no cross-batch cache reuse).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B] [--settle-steps S]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Before the W warm-up steps every rank runs S untimed pipelined settle steps (default 300, ~0.2 s): the
+oracle's spot check and the setup leave the GPU idle, and the first tens of milliseconds of pipelined
+work after that run ~10 % slower per step.  The K timed steps are bracketed by a barrier
+and torch.cuda.synchronize() on both sides and timed as the max over ranks.
 
 Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, N = 1):
   roofline      k_score, the inlier-scoring kernel: algorithmic bytes (12 B per point of every
