@@ -123,3 +123,30 @@ def test_single_cloud_continuation_copies_the_finished_inliers():
     finally:
         ctx.close()
         full.close()
+
+
+def test_early_refinement_matches_one_stream():
+    """$PITT_EARLY_REFINE=1 (off by default): the frames done after the first
+    chunk are refined on the side stream while the later chunks run.  Same records and inlier lists as
+    the one-stream context, and the oracle's."""
+    w, h = 320, 240
+    frames = [pitt.synth_frame(pitt.SCENE_TABLE if i % 3 else pitt.SCENE_TABLE_NAN, 8300 + i, w, h) for i in range(12)]
+    b = pitt.FrameBatch.from_host(frames, device="cuda:0")
+    inl_a = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+    inl_b = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
+    er = _ctx(PITT_EARLY_REFINE=1, PITT_XS_MAX_FRAMES=0)  # the chain refinement, as large batches
+    one = _ctx(PITT_EARLY_REFINE=0, PITT_XS_MAX_FRAMES=0)
+    try:
+        hyps = None
+        for _ in range(3):  # first sight, then the learnt short schedule
+            ra = er.plane_segment_batch(b, pitt.sac_params(), inl_a)
+            rb = one.plane_segment_batch(b, pitt.sac_params(), inl_b)
+            assert ra.tobytes() == rb.tobytes()
+            la, lb = _lists(b, ra, inl_a), _lists(b, rb, inl_b)
+            assert all(np.array_equal(x, y) for x, y in zip(la, lb))
+            hyps = ra["hypotheses"]
+        assert (hyps <= 32).any() and (hyps > 32).any(), hyps  # both phases present
+        P._check(er, frames, ra, la)
+    finally:
+        er.close()
+        one.close()
