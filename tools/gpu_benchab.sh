@@ -1,5 +1,6 @@
 #!/bin/bash
-# bench.py against bench_prev.py (a copy of the previous version), alternating, at the driver's 20 steps.
+# bench.py against bench_prev.py, alternating, at the driver's 20 steps.  bench_prev.py is a copy of the earlier
+# bench.py made before the call (e.g. `git show <rev>:bench.py > bench_prev.py`; not kept in the tree).
 set -o pipefail
 mkdir -p gpurun_out
 for r in 1 2 3; do
