@@ -28,6 +28,7 @@ Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, 
   config5       find_supports + euclidean_clusters on the 1.2M-point fused scene, GPU vs oracle
   cpu_baseline  the oracle (CPU restatement of PCL's path) on the host: frame-parallel on the
                 host's CPU share, and single-core per-frame medians (config 1)
+  steady_state  (K < 200) the same pipelined step over 200 timed steps right after the headline's
 """
 import argparse
 import concurrent.futures as cf
@@ -801,6 +802,21 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # the same pipelined step over 200 timed steps right after the headline's (1 GPU, default extras, when
+    # fewer steps were asked): the steady state beside the short window's fill and drain; never `value`
+    steady = None
+    if world == 1 and not args.no_extras and args.steps < 200:
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(200):
+            timed_step()
+        timed_drain()
+        torch.cuda.synchronize()
+        dts = time.perf_counter() - ts
+        steady = {"steps": 200, "frames_per_s": round(total * 200 / dts, 1), "ms_per_step": round(dts / 200 * 1e3, 4),
+                  "note": "the headline's pipelined step timed over 200 steps right after it (fill and drain "
+                          "amortised); reported beside `value`, not instead of it"}
+        log(f"[rank 0] steady state: {steady}")
 
     # ---- roofline pass: one batch at a time, HIP events around every launch on the launch stream
     # (a concurrent batch would share HBM and stretch the kernel's duration) ----
@@ -883,6 +899,8 @@ def main():
             "hip_graphs": dict(zip(("captures", "replays"), ctxs[0].graph_stats())),
             "library_sha16": lib_sha,
         }
+        if steady is not None:
+            line["steady_state"] = steady
     if rank == 0 and world == 1 and not args.no_extras:
         line["cov_fast"] = cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, args.steps, B)
         log(f"[rank 0] cov_fast: {line['cov_fast']}")
