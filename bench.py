@@ -9,10 +9,12 @@ each in-flight context segments its own batch (distinct frames, no cross-batch c
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B] [--settle-steps S]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Before the W warm-up steps every rank runs S untimed pipelined settle steps (default 300, ~0.2 s): the
-oracle's spot check and the setup leave the GPU idle, and the first tens of milliseconds of pipelined
-work after that run ~10 % slower per step.  The K timed steps are bracketed by a barrier
-and torch.cuda.synchronize() on both sides and timed as the max over ranks.
+The K timed steps are bracketed by a barrier and torch.cuda.synchronize() on both sides and timed as
+the max over ranks.  The same K-step window is timed twice: first after only the W warm-up steps (the
+GPU from idle: `value_without_settle`), then after S untimed pipelined settle steps (default 300,
+~0.2 s) and the W warm-up steps again (`value`): the first tens of milliseconds of pipelined work after
+an idle GPU run ~10 % slower per step.  `untimed_steps` counts every pipelined step
+run before the timed window.
 
 Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, N = 1):
   roofline      k_score, the inlier-scoring kernel: algorithmic bytes (12 B per point of every
@@ -23,7 +25,7 @@ Prints ONE JSON line on rank 0.  Besides the headline value it carries (rank 0, 
   clutter       a clutter-scene batch (T = 1001 hypotheses per frame) against the VALU roof
   pcie_fed      frames/s when every batch starts in pinned host memory (H2D copy in the step)
   streaming     every step's buffers receive new frames (a clutter-bearing batch among them): frames/s,
-                continuations and graph captures per 100 batches
+                continuations per 100 batches
   config2       one cloud through the single-cloud ABI (host in, host out), median latency
   config5       find_supports + euclidean_clusters on the 1.2M-point fused scene, GPU vs oracle
   cpu_baseline  the oracle (CPU restatement of PCL's path) on the host: frame-parallel on the
@@ -209,8 +211,8 @@ def cov_fast_pass(pitt, ctx, batches, outs, params, step, drain, steps, frames_p
     against the exact mode.  Exact order stays the default and the parity path."""
     import torch
     fast = pitt.sac_params(cov_mode=pitt.COV_FAST)
-    # every context sees the fast layout twice before timing (its graph is captured on the second
-    # sight), as the main pass primes its contexts
+    # every context sees the fast layout twice before timing (arena and chunk hint settle), as the
+    # main pass primes its contexts
     for _ in range(2 * len(batches)):
         step(fast)
     drain()
@@ -289,7 +291,7 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
     `pool_n` needs the whole chunk schedule.  Step i copies pool batch i % pool_n into the buffers of
     context i % len(ctxs) (a device-to-device copy on that context's stream, ahead of its batch), so a
     context's buffers hold new content at every use.  Reported: frames/s with the copies inside the
-    steps, the copies' own time (a copy-only pass), continuations and graph captures per 100 batches."""
+    steps, the copies' own time (a copy-only pass), continuations per 100 batches."""
     import torch
     B = batches[0].n_frames
     rng = np.random.default_rng(77)
@@ -330,18 +332,16 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
                 pending[j] = False
         torch.cuda.synchronize()
 
-    for i in range(2 * len(ctxs) * pool_n):  # every context sees every pool batch (hint and graph settle)
+    for i in range(2 * len(ctxs) * pool_n):  # every context sees every pool batch (the chunk hint settles)
         step(i)
     drain()
     cont0 = sum(c.schedule_stats()[0] for c in ctxs)
-    cap0 = sum(c.graph_stats()[0] for c in ctxs)
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
     drain()
     dt = time.perf_counter() - t0
     cont = sum(c.schedule_stats()[0] for c in ctxs) - cont0
-    caps = sum(c.graph_stats()[0] for c in ctxs) - cap0
     t1 = time.perf_counter()
     for i in range(steps):
         step(i, run=False)
@@ -367,7 +367,6 @@ def streaming_pass(pitt, ctxs, batches, dev, threads, params, steps, clutter_per
             "frames_per_s_copies_excluded": round(B * steps / max(1e-9, dt - dc), 1),
             "clutter_frames": f"{clutter_per_batch} of {B} in 1 of {pool_n} pool batches",
             "continuations_per_100_batches": round(100.0 * cont / steps, 2),
-            "graph_captures_per_100_batches": round(100.0 * caps / steps, 2),
             "spot_check_vs_oracle": ok,
             "note": "a step = a device-to-device copy of new frames into the context's buffers, then its batch"}
 
@@ -443,15 +442,39 @@ def config5_pass(pitt, ctx, threads, reps=5):
     """BASELINE config 5: find_supports (th 0.02f, 10 iterations) on the 1.2M-point fused scene, then
     euclidean_clusters (0.03 m, 1 % / 99 %) on every support's on-support cloud
     (obj_segmentation.cpp:261-312).  Timed through pitt_segment_objects_dev with the scene resident
-    in HBM (nothing read back but sizes, coefficients and sums), median of `reps` after 1 warm-up;
-    the host-array service path (H2D / D2H per call) is timed beside it.  Results vs the oracle once."""
+    in HBM (nothing read back but sizes, coefficients and sums), median of `reps` after 1 warm-up.
+    Beside it, the host-array path a C++ caller of the drop-in ABI takes (pitt_find_supports, then
+    pitt_euclidean_clusters on each support's on-support cloud straight from the pointers it returned:
+    H2D of the scene, D2H of every output into the library's pinned blocks), and the same through the
+    Python wrappers (which copy every output into fresh numpy arrays).  Results vs the oracle once."""
+    import ctypes
     import torch
+    from pitt_object_table_segmentation_amd import _lib as L
     orc = oracle()
     x, y, z = pitt.synth_fused(1000, 4)
     dx, dy, dz = (torch.from_numpy(a).cuda() for a in (x, y, z))
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+    sp = pitt.support_params()
 
     def dev_once():
         return ctx.segment_objects_dev(dx, dy, dz, copy=False)
+
+    def host_abi_once():
+        out, cout = L.SupportList(), L.ClusterList()
+        assert L.lib.pitt_find_supports(ctx.h, fp(x), fp(y), fp(z), len(x), ctypes.byref(sp), ctypes.byref(out)) == 0
+        shape = []
+        for i in range(out.n_supports):
+            s = out.supports[i]
+            m = s.n_on_support
+            if m < 30:
+                shape.append((int(s.n_support), m, []))
+                continue
+            a = ctypes.cast(s.on_support_xyz, ctypes.c_void_p).value
+            pl = [ctypes.cast(a + 4 * m * k, ctypes.POINTER(ctypes.c_float)) for k in range(3)]
+            assert L.lib.pitt_euclidean_clusters(ctx.h, pl[0], pl[1], pl[2], m, 0.03, int(np.floor(m * 0.01 + 0.5)),
+                                                 int(np.floor(m * 0.99 + 0.5)), ctypes.byref(cout)) == 0
+            shape.append((int(s.n_support), m, [int(cout.clusters[c].size) for c in range(cout.n_clusters)]))
+        return shape
 
     def host_once():
         sups = ctx.find_supports(x, y, z)
@@ -474,8 +497,16 @@ def config5_pass(pitt, ctx, threads, reps=5):
         return round(float(np.median(ts)), 2)
 
     dev_ms = median_ms(dev_once)
-    host_ms = median_ms(host_once)
+    host_ms = median_ms(host_abi_once)
+    py_ms = median_ms(host_once)
     sups, objs = ctx.segment_objects_dev(dx, dy, dz)
+    # the host paths found the same supports and clusters as the device path
+    hsups, hcl = host_once()
+    host_same = (host_abi_once() == [(int(s["support_cloud"].shape[0]), int(s["on_support_cloud"].shape[0]),
+                                      [int(o[1].numel()) for o in objs if o[0] == k]) for k, s in enumerate(sups)]
+                 and len(hsups) == len(sups)
+                 and all(np.array_equal(a.idx_map, b["idx_map"].cpu().numpy()) for a, b in zip(hsups, sups))
+                 and [len(c.indices) for cl in hcl for c in cl] == [int(o[1].numel()) for o in objs])
     t = time.perf_counter()
     rs = orc.find_supports(x, y, z)
     rcl = [(k, c) for k, s in enumerate(rs) if len(s["on_support_cloud"]) >= 30
@@ -489,6 +520,10 @@ def config5_pass(pitt, ctx, threads, reps=5):
             "gpu_ms_per_scene": dev_ms, "gpu_statistic": f"median of {reps} after 1 warm-up",
             "gpu_path": "pitt_segment_objects_dev (device-resident: scene in HBM, sizes/coefficients/sums back)",
             "host_api_ms_per_scene": host_ms,
+            "host_api": "C ABI from host arrays: pitt_find_supports + pitt_euclidean_clusters per support on the "
+                        "returned on-support planes (every output copied to the library's pinned host blocks)",
+            "python_api_ms_per_scene": py_ms,
+            "host_paths_match_device_path": bool(host_same),
             "cpu_ms_per_scene": round(cpu_ms, 1), "cpu": "oracle, one thread, O(N) restatement of the loop",
             "matches_oracle": bool(same)}
 
@@ -621,8 +656,6 @@ def main():
     ap.add_argument("--dump-records", default="",
                     help="rank 0 writes the (gathered) records of batch slot 0's last step to this .npy")
     args = ap.parse_args()
-    # $PITT_GRAPHS=1 (opt-in HIP graphs) needs the runtime's graph packet capture off, before HIP starts
-    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     global ORIG_HW_QUEUES
     ORIG_HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
     if args.hw_queues > 0:  # hardware queues per process (one per in-flight context's stream); before HIP init
@@ -755,8 +788,8 @@ def main():
 
     ctx = ctxs[0]
     # setup, not steps: every context runs its batch twice, so that its scratch arena is allocated
-    # and its HIP graph captured (on the second sight of a batch layout) before any timed step;
-    # otherwise contexts the warm-up steps never reach pay both inside the timed region
+    # and its chunk hint learnt before any timed step; otherwise contexts the warm-up steps never
+    # reach pay for that inside the timed region
     for i in range(len(ctxs)):
         for _ in range(2):
             ctxs[i].plane_segment_batch(batches[i], params, outs[i])
@@ -772,11 +805,39 @@ def main():
             f"(T={int(res0[0]['hypotheses'])}, inliers={int(res0[0]['n_inliers'])})")
     if world > 1:
         dist.barrier()
+
+    def timed_window(steps):
+        """K pipelined steps bracketed by a barrier + synchronize on both sides; the max over ranks."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            timed_step()
+        r = timed_drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        d = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([d], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d = float(t.item())
+        return d, r
+
+    # ---- the same K-step window with only the W warm-up steps before it (no settle steps): the GPU
+    # comes from the setup's serial batches and the oracle's CPU time, as a bench without settling
+    # would time it.  Reported beside `value` as `value_without_settle`, never instead of it. ----
+    for _ in range(args.warmup):
+        timed_step()
+    timed_drain()
+    dt_cold, _ = timed_window(args.steps)
     # settle, then warm up: --settle-steps pipelined untimed steps before the W warm-up steps.  After
     # the setup's serial batches and the oracle's CPU time the GPU has been idle or lightly loaded, and
     # the first tens of milliseconds of pipelined work run slower per step (clocks and power settling):
     # 20 timed steps measured 358-362k frames/s after 5 warm-up steps, 382-391k after 50 and 394-396k
-    # after 300 (tools/gpu_warm.sh).  The timed steps are unchanged.
+    # after 300 (DESIGN.md s6).  The timed steps are unchanged; every untimed pipelined step before them
+    # is counted in the line's `untimed_steps`.
     for _ in range(args.settle_steps):
         timed_step()
     for _ in range(args.warmup):
@@ -784,24 +845,10 @@ def main():
     timed_drain()
 
     # ---- timed throughput pass: K steps, batches overlapped on the contexts' streams ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     if gather is not None:
         gather.seconds, gather.posted = 0.0, 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        timed_step()
-    res = timed_drain()
+    dt, res = timed_window(args.steps)
     rec_dump = None if records[0] is None else records[0].copy()  # before the extra passes reuse the slots
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     # the same pipelined step over 200 timed steps right after the headline's (1 GPU, default extras, when
     # fewer steps were asked): the steady state beside the short window's fill and drain; never `value`
     steady = None
@@ -852,6 +899,10 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            # every pipelined step run before the timed K (untimed): the W warm-up steps before the
+            # no-settle window, that window's K steps, the settle steps and the W warm-up steps again
+            "untimed_steps": 2 * args.warmup + args.steps + args.settle_steps,
+            "value_without_settle": round(total * args.steps / dt_cold, 2),
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -867,7 +918,11 @@ def main():
                 "points_per_frame": W * H,
                 "parallelism": f"frame-sharded x{world}, {args.pipeline} batches in flight per GPU"
                                + (f", each split over {parts} contexts" if parts > 1 else ""),
-                "untimed_before_timed": {"settle_steps": args.settle_steps, "warmup_steps": args.warmup},
+                "untimed_before_timed": {"warmup_steps": args.warmup, "no_settle_window_steps": args.steps,
+                                         "settle_steps": args.settle_steps, "warmup_steps_again": args.warmup,
+                                         "note": "value_without_settle = the same K-step window timed after only "
+                                                 "the W warm-up steps (the GPU from idle); value = the K-step "
+                                                 "window after the settle steps"},
                 "hypotheses_per_frame_mean": round(float(np.mean(hyps)), 2),
                 "world_size_seen": world,
                 "collective": (f"{backend} all_gather_into_tensor of per-frame records, async (collected one "
@@ -896,7 +951,6 @@ def main():
                 "algorithmic_bytes_per_launch": round(nbytes / max(1, launches), 1),
             },
             "kernels": kernels,
-            "hip_graphs": dict(zip(("captures", "replays"), ctxs[0].graph_stats())),
             "library_sha16": lib_sha,
         }
         if steady is not None:

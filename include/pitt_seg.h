@@ -48,9 +48,12 @@ extern "C" {
 #endif
 
 /* 3: pitt_sac_params.cov_mode (A6), pitt_cylinder_params / pitt_cone_params.eigen33, pitt_build_flags.
+ * 4: pitt_graph_stats removed (the plane pipeline launches directly; HIP graphs measured no gain);
+ *    pitt_multi_* (frame-sharded plane batches over several devices from one host process);
+ *    pitt_find_supports_aos, pitt_euclidean_clusters_aos (host AoS clouds uploaded as they lie).
  * Callers check pitt_abi_version() == PITT_ABI_VERSION when they load the library: the structs passed
  * by pointer are read in this ABI's layout. */
-#define PITT_ABI_VERSION 3
+#define PITT_ABI_VERSION 4
 /* Points per scoring tile; frames are scored in tiles of this many points. */
 #define PITT_TILE_POINTS 2048
 
@@ -133,8 +136,6 @@ int  pitt_set_stream(pitt_ctx* ctx, void* hip_stream);
 /* Copy bytes between any host / device addresses on the context's stream (synchronous): for FFI
  * callers without HIP bindings reading the device-resident outputs (pitt_*_dev). */
 int  pitt_memcpy(pitt_ctx* ctx, void* dst, const void* src, int64_t bytes);
-/* Plane batches captured into HIP graphs / replayed from them on this context ($PITT_GRAPHS=0 off). */
-int  pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays);
 /* The adaptive chunk schedule on this context: batches that ran past the scoring chunks the hint
  * scheduled (a continuation finished them), and the chunks the last batch launched up front
  * ($PITT_ADAPTIVE_CHUNKS=0 always launches every chunk). */
@@ -174,6 +175,25 @@ int pitt_plane_segment_batch(pitt_ctx* ctx, const pitt_frames* frames, const pit
 int pitt_plane_segment_batch_async(pitt_ctx* ctx, const pitt_frames* frames, const pitt_sac_params* p,
                                    pitt_plane_result* results, int32_t* inliers_dev);
 int pitt_wait(pitt_ctx* ctx);
+
+/* --- several devices from one host process (frames shard, one gather) ---------
+ * The reference's C++ host (obj_segmentation.cpp:381, ransac_segmentation.cpp) is one process; a
+ * pitt_multi holds one context per listed device (a device may be listed twice: two contexts on it).
+ * pitt_plane_segment_batch_multi takes a batch in HOST memory (pitt_frames with host planes; frames
+ * ascending and non-overlapping), gives device g the contiguous frames [g F / G, (g + 1) F / G), uploads
+ * each shard, segments it on its device (one host thread per device) and gathers on the host: results
+ * [n_frames] in frame order, and (optional) frame f's ascending inliers at inliers_out + offsets[f]
+ * (host int32 [capacity]; entries between a frame's inliers and the next frame are unspecified).
+ * Byte-equal to one pitt_plane_segment_batch over all the frames. */
+typedef struct pitt_multi pitt_multi;
+int  pitt_multi_create(pitt_multi** out, const int32_t* hip_devices, int32_t n_devices);
+void pitt_multi_destroy(pitt_multi* m);
+int32_t pitt_multi_devices(const pitt_multi* m);
+/* Device g's context (owned by m): its device-resident entry points, stream and profiler. */
+pitt_ctx* pitt_multi_context(pitt_multi* m, int32_t g);
+const char* pitt_multi_last_error(const pitt_multi* m);
+int pitt_plane_segment_batch_multi(pitt_multi* m, const pitt_frames* host_frames, const pitt_sac_params* p,
+                                   pitt_plane_result* results, int32_t* inliers_out);
 
 /* Debug / parity hooks: per-hypothesis inlier counts of the last batch (host [n_frames*cap]),
  * hypotheses beyond a frame's T are unspecified. */
@@ -216,9 +236,15 @@ typedef struct {
     int32_t            iterations;  /* RANSAC rounds run by the loop            */
 } pitt_support_list;
 
-/* xyz: host SoA (x[n], y[n], z[n]). */
+/* xyz: host SoA (x[n], y[n], z[n]).  The outputs (idx maps, support and on-support SoA clouds) are
+ * in the context's pinned host memory, valid until the next support call on the context. */
 int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                        const pitt_support_params* p, pitt_support_list* out);
+/* The same from the cloud as it lies in the request (supports_segmentation_srv.cpp:246-247: PCL
+ * PointXYZ, stride_bytes 16; or packed xyz, 12): one upload of the caller's bytes, deinterleaved on the
+ * device.  The service handlers' path. */
+int pitt_find_supports_aos(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                           const pitt_support_params* p, pitt_support_list* out);
 
 /* Device-resident form (the cloud a device preprocessing chain left in HBM: pitt_voxel_grid ->
  * pitt_deep_filter -> pitt_transform_cloud, obj_segmentation.cpp:238-248): x/y/z device SoA; every
@@ -260,6 +286,10 @@ typedef struct {
 int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const float* y, const float* z,
                             int64_t n, double tolerance, int32_t min_size, int32_t max_size,
                             pitt_cluster_list* out);
+/* The same from a host AoS cloud (cluster_segmentation_srv.cpp:57-58: PointXYZ, stride_bytes 16; or
+ * packed xyz, 12), uploaded as it lies and deinterleaved on the device. */
+int pitt_euclidean_clusters_aos(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                                double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list* out);
 
 /* Device-resident form: x/y/z device SoA; each cluster's members (ascending) stay on the device at
  * indices[offset, offset + size); the sums come back to the host. */

@@ -233,6 +233,12 @@ public:
     bool findSupports(pitt_msgs::SupportSegmentation::Request& req, pitt_msgs::SupportSegmentation::Response& res);
     // cluster_segmentation_srv.cpp:38
     bool clusterize(pitt_msgs::ClusterSegmentation::Request& req, pitt_msgs::ClusterSegmentation::Response& res);
+    // the two handlers on a cloud given as PointXYZ bytes (4 floats per point) rather than inside the
+    // request (the flat C ABI and the ROS nodes pass their converted message this way: no copy of the
+    // cloud into a request); the request's cloud fields are not read
+    bool findSupports(const float* xyz16, size_t n, size_t n_normals, const pitt_msgs::SupportSegmentation::Request& req,
+                      pitt_msgs::SupportSegmentation::Response& res);
+    bool clusterize(const float* xyz16, size_t n, pitt_msgs::ClusterSegmentation::Response& res);
 
     // ransac_segmentation.cpp:175-199: accept iff the response holds > 0 inliers (local minInliers = 0, Q2)
     bool callRansacPlaneSegmentation(const pitt_msgs::PointCloud& cloud, const pitt_msgs::NormalCloud& norm,

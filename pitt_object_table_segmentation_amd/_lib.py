@@ -12,23 +12,6 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _graph_packet_capture_off() -> None:
-    """HIP graphs of the plane path (opt-in, $PITT_GRAPHS=1) need the runtime's graph packet capture off
-    (DESIGN.md s3d): ask for it before the HIP runtime starts.  When torch has already started HIP the
-    variable would no longer reach the runtime, so it is left unset and the library keeps graphs off."""
-    import sys
-    if "DEBUG_CLR_GRAPH_PACKET_CAPTURE" in os.environ:
-        return
-    torch = sys.modules.get("torch")
-    try:
-        started = torch is not None and torch.cuda.is_initialized()
-    except AttributeError:
-        started = False
-    if not started:
-        os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"
-
-
-_graph_packet_capture_off()
 # PITT_LIB_PATH: an alternative build of the same library (A/B experiments, tools/ only)
 LIB_PATH = os.environ.get("PITT_LIB_PATH") or os.path.join(_HERE, "libpitt_seg.so")
 
@@ -235,7 +218,7 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 
 # name -> (restype, argtypes); every symbol declared in include/pitt_seg.h
-PITT_ABI_VERSION = 3  # include/pitt_seg.h
+PITT_ABI_VERSION = 4  # include/pitt_seg.h
 
 SIGNATURES = {
     "pitt_abi_version": (_i32, []),
@@ -254,6 +237,13 @@ SIGNATURES = {
     "pitt_plane_segment_batch_async": (_i32, [_vp, ctypes.POINTER(Frames), ctypes.POINTER(SacParams),
                                               ctypes.POINTER(PlaneResult), _vp]),
     "pitt_wait": (_i32, [_vp]),
+    "pitt_multi_create": (_i32, [ctypes.POINTER(_vp), _i32p, _i32]),
+    "pitt_multi_destroy": (None, [_vp]),
+    "pitt_multi_devices": (_i32, [_vp]),
+    "pitt_multi_context": (_vp, [_vp, _i32]),
+    "pitt_multi_last_error": (ctypes.c_char_p, [_vp]),
+    "pitt_plane_segment_batch_multi": (_i32, [_vp, ctypes.POINTER(Frames), ctypes.POINTER(SacParams),
+                                              ctypes.POINTER(PlaneResult), _i32p]),
     "pitt_last_hypothesis_counts": (_i32, [_vp, _i32, _i32p, _i32]),
     "pitt_extract_indices": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _i64p]),
     "pitt_deep_filter": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, _i64p, _vp, _vp, _vp,
@@ -273,13 +263,16 @@ SIGNATURES = {
                                   ctypes.POINTER(SupportList)]),
     "pitt_euclidean_clusters": (_i32, [_vp, _f32p, _f32p, _f32p, _i64, ctypes.c_double, _i32, _i32,
                                        ctypes.POINTER(ClusterList)]),
+    "pitt_find_supports_aos": (_i32, [_vp, _f32p, _i64, _i32, ctypes.POINTER(SupportParams),
+                                      ctypes.POINTER(SupportList)]),
+    "pitt_euclidean_clusters_aos": (_i32, [_vp, _f32p, _i64, _i32, ctypes.c_double, _i32, _i32,
+                                           ctypes.POINTER(ClusterList)]),
     "pitt_find_supports_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SupportParams),
                                       ctypes.POINTER(SupportListDev)]),
     "pitt_euclidean_clusters_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.c_double, _i32, _i32,
                                            ctypes.POINTER(ClusterListDev)]),
     "pitt_cluster_params_default": (None, [ctypes.POINTER(ClusterParams)]),
     "pitt_memcpy": (_i32, [_vp, _vp, _vp, _i64]),
-    "pitt_graph_stats": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "pitt_refine_stats": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "pitt_segment_objects_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, ctypes.POINTER(SupportParams),
                                         ctypes.POINTER(ClusterParams), ctypes.POINTER(Scene)]),

@@ -27,6 +27,15 @@ def _ip(a: np.ndarray):
     return a.ctypes.data_as(_i32p)
 
 
+def _host_copy(ptr, shape, dtype) -> np.ndarray:
+    """A numpy copy of `shape` elements at a host address the library returned (one memmove:
+    np.ctypeslib.as_array builds a ctypes array type per call, which costs milliseconds here)."""
+    out = np.empty(shape, dtype)
+    if out.size:
+        ctypes.memmove(out.ctypes.data, ctypes.cast(ptr, ctypes.c_void_p).value, out.nbytes)
+    return out
+
+
 class PittError(RuntimeError):
     def __init__(self, code: int, msg: str = ""):
         super().__init__(f"pitt error {code}: {msg}")
@@ -453,10 +462,11 @@ class Context:
         res = []
         for i in range(out.n_supports):
             s = out.supports[i]
-            ns, no = s.n_support, s.n_on_support
-            sup = np.ctypeslib.as_array(s.support_xyz, (3 * ns,)).reshape(3, ns).T.copy() if ns else np.zeros((0, 3), np.float32)
-            on = np.ctypeslib.as_array(s.on_support_xyz, (3 * no,)).reshape(3, no).T.copy() if no else np.zeros((0, 3), np.float32)
-            res.append(SupportResult(np.ctypeslib.as_array(s.idx_map, (s.n_points,)).copy(),
+            # the clouds come back as SoA planes: an (m, 3) view of a (3, m) copy (its .T rows are the
+            # contiguous x, y, z planes the other entry points take)
+            sup = _host_copy(s.support_xyz, (3, s.n_support), np.float32).T
+            on = _host_copy(s.on_support_xyz, (3, s.n_on_support), np.float32).T
+            res.append(SupportResult(_host_copy(s.idx_map, (s.n_points,), np.int32),
                                      np.array(list(s.coefficients), np.float32), sup, on))
         return res
 
@@ -467,18 +477,17 @@ class Context:
         out = L.ClusterList()
         self._check(lib.pitt_euclidean_clusters(self.h, _fp(x), _fp(y), _fp(z), len(x), tolerance, min_size,
                                                 max_size, ctypes.byref(out)), "pitt_euclidean_clusters")
-        res = []
-        for i in range(out.n_clusters):
-            c = out.clusters[i]
-            idx = np.ctypeslib.as_array(c.indices, (c.size,)).copy() if c.size else np.zeros(0, np.int32)
-            res.append(ClusterResult(idx, np.array(list(c.sum_xyz), np.float32)))
+        if out.n_clusters == 0:
+            return []
+        # the members of every cluster are one contiguous block (size-descending order): one copy
+        cl = [out.clusters[i] for i in range(out.n_clusters)]
+        total = sum(c.size for c in cl)
+        allm = _host_copy(cl[0].indices, (total,), np.int32)
+        res, o = [], 0
+        for c in cl:
+            res.append(ClusterResult(allm[o:o + c.size], np.array(list(c.sum_xyz), np.float32)))
+            o += c.size
         return res
-
-    def graph_stats(self):
-        """(captures, replays) of the plane pipeline's HIP graphs on this context."""
-        c, r = ctypes.c_int64(), ctypes.c_int64()
-        self._check(lib.pitt_graph_stats(self.h, ctypes.byref(c), ctypes.byref(r)), "pitt_graph_stats")
-        return c.value, r.value
 
     def schedule_stats(self):
         """(batches finished by a continuation past their scheduled chunks, chunks the last batch launched
@@ -630,6 +639,59 @@ def _cloud16(xyz: np.ndarray) -> np.ndarray:
     out = np.ones((xyz.shape[0], 4), np.float32)
     out[:, :3] = xyz
     return out
+
+
+class MultiContext:
+    """pitt_multi: one context per listed device, frame-sharded plane batches from host memory
+    (include/pitt_seg.h; the in-process multi-device path of a C++ host).  A device may be listed
+    more than once (several contexts on it: how the path is exercised on a one-GPU box)."""
+
+    def __init__(self, devices: Sequence[int]):
+        devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+        h = ctypes.c_void_p()
+        rc = lib.pitt_multi_create(ctypes.byref(h), devs, len(devices))
+        if rc != L.PITT_OK:
+            raise PittError(rc, "pitt_multi_create (needs gfx950 devices)")
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if self.h:
+            lib.pitt_multi_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def plane_segment_batch(self, frames: Sequence[tuple], params: Optional[L.SacParams] = None):
+        """frames: host (x, y, z) float32 arrays.  Returns (RESULT_DTYPE records, [ascending inliers])
+        gathered in frame order from the devices' shards."""
+        counts = np.array([len(f[0]) for f in frames], np.int64)
+        offs, cap = padded_offsets(counts)
+        planes = [np.zeros(max(cap, 1), np.float32) for _ in range(3)]
+        for o, n, f in zip(offs, counts, frames):
+            for k in range(3):
+                planes[k][o:o + n] = f[k]
+        inl = np.empty(max(cap, 1), np.int32)
+        res = np.zeros(len(frames), RESULT_DTYPE)
+        fr = L.Frames(planes[0].ctypes.data, planes[1].ctypes.data, planes[2].ctypes.data,
+                      offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                      counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(frames), cap)
+        p = params or sac_params()
+        rc = lib.pitt_plane_segment_batch_multi(self.h, ctypes.byref(fr), ctypes.byref(p),
+                                                res.ctypes.data_as(ctypes.POINTER(L.PlaneResult)), _ip(inl))
+        if rc < 0:
+            raise PittError(rc, f"pitt_plane_segment_batch_multi: {lib.pitt_multi_last_error(self.h).decode()}")
+        return res, [inl[o:o + r["n_inliers"]].copy() for o, r in zip(offs, res)]
 
 
 class Services:

@@ -201,7 +201,6 @@ extern "C" int pitt_classify_clusters(pitt_ctx* ctx, const float* x, const float
     //     (the staged clusters are ready once this stream's work so far has run: an event orders it) ---
     if (!ctx->aux) {
         if (pitt_create(&ctx->aux, ctx->device) != PITT_OK || !ctx->aux) return ctx->fail(PITT_E_HIP, "auxiliary context");
-        ctx->aux->use_graphs = false;
     }
     {
         hipEvent_t staged = nullptr;

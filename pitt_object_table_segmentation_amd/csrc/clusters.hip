@@ -560,11 +560,10 @@ static int compact(pitt_ctx* ctx, int64_t n, Pred pred, Act act, int64_t* total)
 // either way.
 int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t n,
                             double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list* out,
-                            pitt_cluster_list_dev* dout, bool dev_in) {
+                            pitt_cluster_list_dev* dout, bool dev_in, int aos_stride) {
     hipStream_t s = ctx->stream;
     ctx->keep_clusters.clear();
     ctx->keep_clusters_dev.clear();
-    ctx->keep_i32.clear();
     if (out) {
         out->n_clusters = 0;
         out->clusters = nullptr;
@@ -575,6 +574,9 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
         dout->indices = nullptr;
     }
     if (n == 0) return PITT_OK;  // extract(): empty input => no clusters
+    const bool timing = ctx->host_timing && !dev_in;  // $PITT_HOST_TIMING=1: host phases on stderr
+    const double tm0 = timing ? wall_ms() : 0.0;
+    double tm_in = 0.0, tm_roots = 0.0;
     // KdTreeFLANN::radiusSearch: r^2 = (float)(radius * radius) with radius = (double)(float)tol
     const float tol_f = (float)tolerance;
     const float r2 = (float)((double)tol_f * (double)tol_f);
@@ -611,10 +613,17 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
     int32_t* CSTART = (int32_t*)ctx->buf("cl_cstart", (N + 1) * 4);
     if (!CSTART) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
     float *Y = X + N, *Z = X + 2 * N;
-    const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    PITT_HIP_TRY(hipMemcpyAsync(X, hx, N * 4, kin, s));
-    PITT_HIP_TRY(hipMemcpyAsync(Y, hy, N * 4, kin, s));
-    PITT_HIP_TRY(hipMemcpyAsync(Z, hz, N * 4, kin, s));
+    if (aos_stride) {  // the caller's host AoS cloud as it lies: one upload, deinterleaved on the device
+        void* scr = ctx->buf("cl_aos", N * aos_stride);
+        if (!scr) return ctx->fail(PITT_E_NOMEM, "cluster scratch");
+        PITT_HIP_TRY(upload_aos(s, scr, hx, n, aos_stride, X, Y, Z));
+    } else {
+        const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        PITT_HIP_TRY(hipMemcpyAsync(X, hx, N * 4, kin, s));
+        PITT_HIP_TRY(hipMemcpyAsync(Y, hy, N * 4, kin, s));
+        PITT_HIP_TRY(hipMemcpyAsync(Z, hz, N * 4, kin, s));
+    }
+    if (timing) tm_in = wall_ms();
     PITT_HIP_TRY(hipMemsetAsync(KEYS, 0xFF, (size_t)hsize * 8, s));
     PITT_HIP_TRY(hipMemsetAsync(CELLS, 0, (N * 7 + 16) * 4, s));
     PITT_HIP_TRY(hipMemsetAsync(CMIN, 0x7F, N * 4, s));   // INT_MAX-ish: atomicMin seeds
@@ -660,6 +669,7 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
         std::memcpy(roots.data(), h, (size_t)K * 4);
         std::memcpy(sizes.data(), h + K, (size_t)K * 4);
     }
+    if (timing) tm_roots = wall_ms();
     struct RS {
         int32_t root, size;
     };
@@ -747,10 +757,15 @@ int euclidean_clusters_impl(pitt_ctx* ctx, const float* hx, const float* hy, con
         dout->indices = MIDX;
         return PITT_OK;
     }
-    ctx->keep_i32.emplace_back((size_t)M);
-    PITT_HIP_TRY(hipMemcpyAsync(ctx->keep_i32.back().data(), MIDX, (size_t)M * 4, hipMemcpyDeviceToHost, s));
+    // members into the context's pinned output block (reused across calls; valid until the next call)
+    int32_t* base = (int32_t*)ctx->pinned("cl_out_h", (size_t)std::max<int64_t>(M, 1) * 4);
+    if (!base) return ctx->fail(PITT_E_NOMEM, "cluster members (pinned)");
+    PITT_HIP_TRY(hipMemcpyAsync(base, MIDX, (size_t)M * 4, hipMemcpyDeviceToHost, s));
     PITT_HIP_TRY(hipStreamSynchronize(s));
-    const int32_t* base = ctx->keep_i32.back().data();
+    if (timing)
+        std::fprintf(stderr, "pitt_euclidean_clusters n=%lld: input %.3f ms, components + roots %.3f ms, members + sums + "
+                     "D2H %.3f ms (%lld clusters, %lld members)\n", (long long)n, tm_in - tm0, tm_roots - tm_in,
+                     wall_ms() - tm_roots, (long long)K, (long long)M);
     for (int64_t t = 0; t < K; ++t) {
         pitt_cluster c;
         c.size = coff[(size_t)t + 1] - coff[(size_t)t];
@@ -773,7 +788,18 @@ extern "C" int pitt_euclidean_clusters(pitt_ctx* ctx, const float* x, const floa
     if (!out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, out, nullptr, false);
+    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, out, nullptr, false, 0);
+}
+
+extern "C" int pitt_euclidean_clusters_aos(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                                           double tolerance, int32_t min_size, int32_t max_size, pitt_cluster_list* out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!out || n < 0 || (n > 0 && !xyz)) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (stride_bytes != 12 && stride_bytes != 16) return ctx->fail(PITT_E_INVALID, "stride must be 12 or 16");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::euclidean_clusters_impl(ctx, xyz, nullptr, nullptr, n, tolerance, min_size, max_size, out, nullptr,
+                                         false, stride_bytes);
 }
 
 extern "C" int pitt_euclidean_clusters_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
@@ -783,13 +809,13 @@ extern "C" int pitt_euclidean_clusters_dev(pitt_ctx* ctx, const float* x, const 
     if (!out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, nullptr, out, true);
+    return pitt::euclidean_clusters_impl(ctx, x, y, z, n, tolerance, min_size, max_size, nullptr, out, true, 0);
 }
 
 namespace pitt {
 int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t N,
                        const pitt_support_params* sp, pitt_support_list* out, pitt_support_list_dev* dout,
-                       bool dev_in);
+                       bool dev_in, int aos_stride);
 
 __global__ void k_offset_indices(const int32_t* __restrict__ src, int64_t m, int32_t* __restrict__ dst) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
@@ -822,7 +848,7 @@ extern "C" int pitt_segment_objects_dev(pitt_ctx* ctx, const float* x, const flo
     out->n_objects = 0;
     out->objects = nullptr;
     out->indices = nullptr;
-    int rc = find_supports_impl(ctx, x, y, z, n, sp, nullptr, &out->supports, true);
+    int rc = find_supports_impl(ctx, x, y, z, n, sp, nullptr, &out->supports, true, 0);
     if (rc) return rc;
     const std::vector<pitt_support_dev> sups = ctx->keep_supports_dev;  // cluster calls clear the keep lists
     std::vector<pitt_object> objs;
@@ -839,7 +865,7 @@ extern "C" int pitt_segment_objects_dev(pitt_ctx* ctx, const float* x, const flo
         const int32_t mx = (int32_t)std::round((double)m * cp->max_rate);
         pitt_cluster_list_dev L;
         rc = euclidean_clusters_impl(ctx, su.on_support_xyz, su.on_support_xyz + su.stride,
-                                     su.on_support_xyz + 2 * su.stride, m, cp->tolerance, mn, mx, nullptr, &L, true);
+                                     su.on_support_xyz + 2 * su.stride, m, cp->tolerance, mn, mx, nullptr, &L, true, 0);
         if (rc) return rc;
         int64_t members = 0;
         for (int c = 0; c < L.n_clusters; ++c) {

@@ -17,6 +17,31 @@ constexpr int kCTile = 2048;
 
 __host__ __device__ inline int64_t ctiles(int64_t n) { return (n + kCTile - 1) / kCTile; }
 
+// A host cloud uploaded as it lies (SF floats per point: PCL PointXYZ 4, packed xyz 3) -> SoA planes
+// (the *_aos entry points: one H2D copy of the caller's bytes, no host-side deinterleave).
+template <int SF>
+__global__ __launch_bounds__(256) void k_aos_planes(const float* __restrict__ aos, int64_t n, float* __restrict__ x,
+                                                    float* __restrict__ y, float* __restrict__ z) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        x[i] = aos[i * SF];
+        y[i] = aos[i * SF + 1];
+        z[i] = aos[i * SF + 2];
+    }
+}
+// hx: a host AoS cloud of `stride_bytes` (12 or 16) per point -> planes x/y/z on the context's stream.
+inline hipError_t upload_aos(hipStream_t s, void* scratch, const float* hx, int64_t n, int stride_bytes, float* x,
+                             float* y, float* z) {
+    if (n <= 0) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(scratch, hx, (size_t)n * stride_bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    if (stride_bytes == 16)
+        hipLaunchKernelGGL(k_aos_planes<4>, dim3(g), dim3(256), 0, s, (const float*)scratch, n, x, y, z);
+    else
+        hipLaunchKernelGGL(k_aos_planes<3>, dim3(g), dim3(256), 0, s, (const float*)scratch, n, x, y, z);
+    return hipGetLastError();
+}
+
 // Pred: __device__ bool operator()(int64_t i) const  (i < n guaranteed by the caller)
 template <class Pred>
 __global__ __launch_bounds__(kBlock) void k_pred_count(Pred pred, int64_t n, int32_t* __restrict__ tile_counts) {

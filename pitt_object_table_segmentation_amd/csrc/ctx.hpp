@@ -60,12 +60,6 @@ inline bool pitt_env_flag(const char* name, bool dflt) {
     return v && *v ? (v[0] != '0') : dflt;
 }
 // A small integer knob from the environment, clamped to [lo, hi].
-// The HIP runtime's graph packet capture is off only when DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 was in the
-// environment when the runtime started (the Python package and bench.py set it before torch starts HIP).
-inline bool graph_packet_capture_off() {
-    const char* v = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
-    return v && v[0] == '0' && v[1] == 0;
-}
 inline int pitt_env_int(const char* name, int dflt, int lo, int hi) {
     const char* v = std::getenv(name);
     const int x = v && *v ? std::atoi(v) : dflt;
@@ -130,15 +124,6 @@ struct pitt_ctx {
     int64_t xrefine_batches = 0, xrefine_fallbacks = 0;  // frames k_xrefine handed back to k_refine
     void* refine_dbg_h = nullptr;
 
-    // HIP graphs of the plane pipeline (opt-in, $PITT_GRAPHS=1): a batch's ~20 launches captured once per
-    // (layout, parameters, arena) and replayed with one hipGraphLaunch.  Only with the HIP runtime's graph
-    // packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before the runtime starts):
-    // replays through the packet-capture path faulted whenever a replay's kernels met work-list entries
-    // their producers had not yet written -- the path does not keep the captured kernels in stream order
-    // (DESIGN.md s3d).  Direct launches measured the same throughput (profiles/r05_graph_ab.json), so
-    // they are the default.
-    bool use_graphs = pitt_env_flag("PITT_GRAPHS", false) && graph_packet_capture_off();
-    int graph_min_frames = pitt_env_int("PITT_GRAPH_MIN_FRAMES", 1, 1, 1 << 30);  // smaller batches launch directly
     // Adaptive chunk schedule (plane_ransac.hip): a batch launches the scoring chunks that the last
     // batches of its layout needed; a frame still running after them is finished by a continuation.
     // Exact either way; $PITT_ADAPTIVE_CHUNKS=0 always launches the whole schedule.
@@ -148,7 +133,7 @@ struct pitt_ctx {
     int xs_max_frames = pitt_env_int("PITT_XS_MAX_FRAMES", 8, 0, 1 << 30);
     // Early refinement ($PITT_EARLY_REFINE=1, off by default): when a batch launches two or more scoring
     // chunks, the frames that finished in the first are decided and refined on side[0] while the later
-    // chunks score the rest (direct launches only; graph captures and profiled runs keep one stream).
+    // chunks score the rest (profiled runs keep one stream).
     // Bit-exact, but measured slower on the pipelined headline.
     bool early_refine = pitt_env_flag("PITT_EARLY_REFINE", false);
     hipEvent_t er_ev[2] = {nullptr, nullptr};  // first-chunk decisions made | early refinement done
@@ -201,29 +186,18 @@ struct pitt_ctx {
         h->need[h->pos] = need;
         h->pos = (h->pos + 1) & 15;
     }
-    uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (cached graphs hold its pointers)
+    uint64_t arena_gen = 0;  // bumped whenever an arena buffer moves (memoised device tables hold its pointers)
     // prim_ransac.hpp: which sampler table each cloud slot of a model's device table buffer holds (the
-    // buffer's address and arena generation when they were uploaded), so a repeat skips the upload
+    // buffer's address, arena generation and slot stride when they were uploaded), so a repeat skips
+    // the upload
     struct PrimTableMemo {
         const void* dev = nullptr;
         uint64_t gen = 0;
+        int64_t stride = -1;  // attempts per slot (A): slot c starts at c * A * kSample
         std::vector<std::tuple<int64_t, uint32_t, int64_t>> keys;
     };
     std::unordered_map<std::string, PrimTableMemo> prim_tables;
-    struct GraphEntry {
-        std::vector<uint64_t> key;
-        hipGraphExec_t exec = nullptr;
-        uint64_t last_use = 0;
-    };
     uint32_t call_seq = 0;  // plane batches enqueued; stamped into each frame's metadata (FrameMeta.pad)
-#ifdef PITT_SYNC_CHECK
-    // debug knob of the graph-ordering investigation
-    bool dbg_sync_before_graph = pitt_env_flag("PITT_DBG_SYNC_BEFORE_GRAPH", false);
-#endif
-    std::vector<GraphEntry> graphs;
-    std::vector<std::vector<uint64_t>> graph_seen;  // keys launched once (captured on a repeat)
-    uint64_t graph_clock = 0;
-    int64_t graph_captures = 0, graph_replays = 0;
 
     // profiling
     bool prof = false;
@@ -256,8 +230,6 @@ struct pitt_ctx {
     int32_t last_frames = 0;
 
     // results kept alive for list-returning calls
-    std::vector<std::vector<int32_t>> keep_i32;
-    std::vector<std::vector<float>> keep_f32;
     std::vector<pitt_support> keep_supports;
     std::vector<pitt_support_dev> keep_supports_dev;
     std::vector<pitt_cluster> keep_clusters;
@@ -276,10 +248,9 @@ struct pitt_ctx {
     void check_canaries(const char* where);
     void* sentinel = nullptr;
     // Device scratch buffer `name` of at least `bytes` (grows, never shrinks).  A block that moves
-    // is freed only after drain(), and bumps arena_gen so that no cached graph replays it.
+    // is freed only after drain(), and bumps arena_gen (memoised device contents are then stale).
     void* buf(const std::string& name, size_t bytes);
-    // Pinned host buffer (the same rules: drain() before a free, arena_gen bumped on a move -- graph
-    // copy nodes hold these addresses too; DESIGN.md s3d, the round-3 graph fault).
+    // Pinned host buffer (the same rules: drain() before a free, arena_gen bumped on a move).
     void* pinned(const std::string& name, size_t bytes);
 
     // Profiler hooks around a launch.

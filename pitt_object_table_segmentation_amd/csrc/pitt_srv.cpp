@@ -46,20 +46,6 @@ bool ParamServer::get(const std::string& k, std::vector<float>& out) const {
     return true;
 }
 
-namespace {
-void to_soa(const pitt_msgs::PointCloud& c, std::vector<float>& x, std::vector<float>& y, std::vector<float>& z) {
-    const size_t n = c.size();
-    x.resize(n);
-    y.resize(n);
-    z.resize(n);
-    for (size_t i = 0; i < n; ++i) {
-        x[i] = c.data[4 * i];
-        y[i] = c.data[4 * i + 1];
-        z[i] = c.data[4 * i + 2];
-    }
-}
-}  // namespace
-
 // The parameter reads of the four primitive handlers (each service reads its own on every call).
 // plane_segmentation_srv.cpp:27-74 (the normal weight, eps and opening angles do not reach
 // SACMODEL_PLANE, A1)
@@ -330,6 +316,26 @@ pitt_support_params SegmentationServices::resolveSupport(const pitt_msgs::Suppor
 // supports_segmentation_srv.cpp:241-361 (+ initializeInputParameters :70-86)
 bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request& req,
                                         pitt_msgs::SupportSegmentation::Response& res) {
+    return findSupports(req.input_cloud.data.data(), req.input_cloud.size(), req.input_norm.size(), req, res);
+}
+
+namespace {
+// SoA planes (n apart) -> a PointXYZ message cloud (x, y, z, 1), sized once
+void planes_to_cloud(const float* p, int64_t n, pitt_msgs::PointCloud& c) {
+    c.data.resize((size_t)n * 4);
+    float* d = c.data.data();
+    for (int64_t i = 0; i < n; ++i) {
+        d[4 * i] = p[i];
+        d[4 * i + 1] = p[n + i];
+        d[4 * i + 2] = p[2 * n + i];
+        d[4 * i + 3] = 1.0f;
+    }
+}
+}  // namespace
+
+bool SegmentationServices::findSupports(const float* xyz16, size_t n, size_t n_normals,
+                                        const pitt_msgs::SupportSegmentation::Request& req,
+                                        pitt_msgs::SupportSegmentation::Response& res) {
     const pitt_support_params sp = resolveSupport(req);
     const float ndw = srvm::getServiceFloatParameter(req.ransac_model_normal_distance_weigth, 0.9f);
 
@@ -337,22 +343,18 @@ bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request&
     status_ = PITT_OK;
     // The first RANSAC call runs with the request's normals: a size mismatch fails it (A1) and the
     // loop exits before any support is found.  Later rounds re-estimate normals of matching size.
-    if (req.input_norm.size() == req.input_cloud.size()) {
-        std::vector<float> x, y, z;
-        to_soa(req.input_cloud, x, y, z);
+    if (n_normals == n) {
+        // the request's PointXYZ bytes go up as they lie (one copy, deinterleaved on the device)
         pitt_support_list L;
-        status_ = pitt_find_supports(ctx_, x.data(), y.data(), z.data(), (int64_t)x.size(), &sp, &L);
+        status_ = pitt_find_supports_aos(ctx_, xyz16, (int64_t)n, 16, &sp, &L);
         if (status_ == PITT_OK) {
+            res.supports_description.reserve((size_t)L.n_supports);
             for (int s = 0; s < L.n_supports; ++s) {
                 const pitt_support& su = L.supports[s];
                 pitt_msgs::Support m;
                 m.inliers.assign(su.idx_map, su.idx_map + su.n_points);
-                for (int64_t i = 0; i < su.n_support; ++i)
-                    m.support_cloud.push_back(su.support_xyz[i], su.support_xyz[su.n_support + i],
-                                              su.support_xyz[2 * su.n_support + i]);
-                for (int64_t i = 0; i < su.n_on_support; ++i)
-                    m.on_support_cloud.push_back(su.on_support_xyz[i], su.on_support_xyz[su.n_on_support + i],
-                                                 su.on_support_xyz[2 * su.n_on_support + i]);
+                planes_to_cloud(su.support_xyz, su.n_support, m.support_cloud);
+                planes_to_cloud(su.on_support_xyz, su.n_on_support, m.on_support_cloud);
                 m.support_coefficient_a = su.coefficients[0];
                 m.support_coefficient_b = su.coefficients[1];
                 m.support_coefficient_c = su.coefficients[2];
@@ -376,25 +378,32 @@ bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request&
 // cluster_segmentation_srv.cpp:38-108
 bool SegmentationServices::clusterize(pitt_msgs::ClusterSegmentation::Request& req,
                                       pitt_msgs::ClusterSegmentation::Response& res) {
+    return clusterize(req.cloud.data.data(), req.cloud.size(), res);
+}
+
+bool SegmentationServices::clusterize(const float* xyz16, size_t n, pitt_msgs::ClusterSegmentation::Response& res) {
     const pitt_cluster_params cp = clusterParams();
     res.cluster_objs.clear();
     status_ = PITT_OK;
-    const size_t n = req.cloud.size();
     if (n >= (size_t)(int64_t)cp.min_input_size) {
         const int mn = (int)std::round((double)n * cp.min_rate);
         const int mx = (int)std::round((double)n * cp.max_rate);
-        std::vector<float> x, y, z;
-        to_soa(req.cloud, x, y, z);
         pitt_cluster_list L;
-        status_ = pitt_euclidean_clusters(ctx_, x.data(), y.data(), z.data(), (int64_t)n, cp.tolerance, mn, mx, &L);
+        status_ = pitt_euclidean_clusters_aos(ctx_, xyz16, (int64_t)n, 16, cp.tolerance, mn, mx, &L);
         if (status_ == PITT_OK) {
+            res.cluster_objs.reserve((size_t)L.n_clusters);
             for (int c = 0; c < L.n_clusters; ++c) {
                 const pitt_cluster& cl = L.clusters[c];
                 pitt_msgs::InliersCluster m;
                 m.inliers.assign(cl.indices, cl.indices + cl.size);
+                m.cloud.data.resize((size_t)cl.size * 4);  // the members' points in index order (:85-95)
                 for (int64_t k = 0; k < cl.size; ++k) {
-                    const int32_t i = cl.indices[k];
-                    m.cloud.push_back(x[(size_t)i], y[(size_t)i], z[(size_t)i]);
+                    const float* p = xyz16 + 4 * (size_t)cl.indices[k];
+                    float* d = m.cloud.data.data() + 4 * k;
+                    d[0] = p[0];
+                    d[1] = p[1];
+                    d[2] = p[2];
+                    d[3] = 1.0f;
                 }
                 const int cnt = (int)cl.size + 1;  // Q7: the counter starts at 1
                 m.x_centroid = cl.sum_xyz[0] / cnt;
@@ -688,9 +697,7 @@ int pitt_srv_arbitrate(int64_t sphere_inliers, int64_t cylinder_inliers, int64_t
 int pitt_srv_find_supports(pitt_srv* s, const float* xyz16, int64_t n, int64_t n_normals,
                            const pitt_srv_support_request* r, int32_t* n_supports, float used_out[13]) {
     if (!s || (n > 0 && !xyz16) || n < 0 || !r || !n_supports) return PITT_E_INVALID;
-    pitt_msgs::SupportSegmentation srv;
-    srv.request.input_cloud = cloud_from(xyz16, n);
-    srv.request.input_norm.n = (size_t)n_normals;
+    pitt_msgs::SupportSegmentation srv;  // the cloud stays in the caller's array (findSupports(xyz16, ...))
     srv.request.min_iterative_cloud_percentual_size = r->min_iterative_cloud_percentual_size;
     srv.request.min_iterative_plane_percentual_size = r->min_iterative_plane_percentual_size;
     srv.request.variance_threshold_for_horizontal = r->variance_threshold_for_horizontal;
@@ -700,7 +707,7 @@ int pitt_srv_find_supports(pitt_srv* s, const float* xyz16, int64_t n, int64_t n
     srv.request.horizontal_axis.assign(r->horizontal_axis, r->horizontal_axis + std::max(0, std::min(8, r->n_horizontal_axis)));
     srv.request.support_edge_remove_offset.assign(r->edge_remove_offset,
                                                   r->edge_remove_offset + std::max(0, std::min(8, r->n_edge_remove_offset)));
-    bool ok = s->svc.findSupports(srv.request, srv.response);
+    bool ok = s->svc.findSupports(xyz16, (size_t)n, (size_t)n_normals, srv.request, srv.response);
     if (s->svc.last_status() < 0) return s->svc.last_status();
     s->supports = std::move(srv.response);
     *n_supports = (int32_t)s->supports.supports_description.size();
@@ -747,9 +754,8 @@ int pitt_srv_support_cloud(pitt_srv* s, int32_t k, int32_t which, float* out) {
 
 int pitt_srv_clusterize(pitt_srv* s, const float* xyz16, int64_t n, int32_t* n_clusters) {
     if (!s || (n > 0 && !xyz16) || n < 0 || !n_clusters) return PITT_E_INVALID;
-    pitt_msgs::ClusterSegmentation srv;
-    srv.request.cloud = cloud_from(xyz16, n);
-    bool ok = s->svc.clusterize(srv.request, srv.response);
+    pitt_msgs::ClusterSegmentation srv;  // the cloud stays in the caller's array
+    bool ok = s->svc.clusterize(xyz16, (size_t)n, srv.response);
     if (s->svc.last_status() < 0) return s->svc.last_status();
     s->clusters = std::move(srv.response);
     *n_clusters = (int32_t)s->clusters.cluster_objs.size();

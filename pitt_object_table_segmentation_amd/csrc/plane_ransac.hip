@@ -584,6 +584,11 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
     const RowGeo G = row_geo(B);
     const int rounds = (Hf + kRnd - 1) / kRnd;
     const uint32_t lrow = (uint32_t)(uintptr_t)wl + 16u * kListRows * (uint32_t)(lane >> 4);  // this lane's group list
+#if defined(PITT_SCORE_EXPERIMENT) && PITT_SCORE_EXPERIMENT == 2
+    // measurement only (wrong counts): the box and nothing else
+    asm volatile("" ::"v"(G.c[0]), "v"(G.c[1]), "v"(G.c[2]), "v"(G.h[0]), "v"(G.h[1]), "v"(G.h[2]), "v"(G.m));
+    return;
+#endif
     if constexpr (kScoreMerge && !INS) {
         // rounds r, r + 1 in one pass: round r's survivors of group g take list slots 0.. in ascending
         // order, round r + 1's follow them (slot = round r's survivor count of the row + rank)
@@ -610,10 +615,15 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
             int vc = 0, vc2 = 0;
 #define PITT_ROWC(g) (__builtin_popcount((uint32_t)(need0 >> (16 * (g))) & 0xFFFFu) + \
                       __builtin_popcount((uint32_t)(need1 >> (16 * (g))) & 0xFFFFu))
+#if defined(PITT_SCORE_EXPERIMENT) && PITT_SCORE_EXPERIMENT == 1
+            // measurement only (wrong counts): the cull and compaction without the list walks
+            asm volatile("" : "+v"(vc), "+v"(vc2) : "s"(PITT_ROWC(0) + PITT_ROWC(1) + PITT_ROWC(2) + PITT_ROWC(3)), "v"(lb));
+#else
             score_list32<ORDER, 0>(lb, PITT_ROWC(0), P.x[0], P.y[0], P.z[0], tv, vc, vc2);
             score_list32<ORDER, 1>(lb, PITT_ROWC(1), P.x[1], P.y[1], P.z[1], tv, vc, vc2);
             score_list32<ORDER, 2>(lb, PITT_ROWC(2), P.x[2], P.y[2], P.z[2], tv, vc, vc2);
             score_list32<ORDER, 3>(lb, PITT_ROWC(3), P.x[3], P.y[3], P.z[3], tv, vc, vc2);
+#endif
 #undef PITT_ROWC
             // back to the hypothesis lanes: round r's count from slot k0 (< 16, in vc), round r + 1's
             // from slot k1 (vc below 16, vc2 from 16)
@@ -837,7 +847,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
         for (int s = 0; s < kSubs; s += 2) {
             load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
             score_sub_lane<ORDER>(cl, Hf, P[0], cur.rem - s * kSub, tv, lane, cnt, tb, gb + s * kGPS * 8);
-            if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
+            load_sub(X, Y, Z, cur.base + min(s + 2, kSubs - 1) * kSub, lane, P[0]);  // unconditional: see below
             score_sub_lane<ORDER>(cl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, cnt, tb, gb + (s + 1) * kGPS * 8);
         }
         store_lane_counts(cnt, Hf, lane, tile_counts + ((int64_t)cur.f * tiles_max + cur.t) * hstride + h0);
@@ -863,12 +873,16 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - 7 * kSub, tv, lane, wc, tb, gb + 7 * kGPS * 8, gsrc + 128u * 7);
 #else
     // sub-steps in pairs: the next sub-step loads into the other register set while this one is
-    // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache)
+    // scored (a runtime loop: unrolled 8 times the body would not fit the instruction cache).  The
+    // second load is unconditional (the last pair reloads sub-step 7, an L2 hit): guarded by
+    // s + 2 < kSubs, the compiler's vmcnt at the join had to assume it was not issued, so the
+    // second half-step waited for sub-step s + 2's loads before scoring s + 1 (one exposed HBM
+    // latency per pair of sub-steps).
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
         score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
                               gsrc + 128u * s);
-        if (s + 2 < kSubs) load_sub(X, Y, Z, cur.base + (s + 2) * kSub, lane, P[0]);
+        load_sub(X, Y, Z, cur.base + min(s + 2, kSubs - 1) * kSub, lane, P[0]);
         score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
                               gsrc + 128u * (s + 1));
     }
@@ -2533,7 +2547,7 @@ static auto refine_multi_kernel(int F) {
     return k_refine_multi<ORDER, DIV, 2>;
 }
 
-// Debug builds only (tools/build_variant.sh <name> -DPITT_SYNC_CHECK, with PITT_GRAPHS=0): synchronise
+// Debug builds only (tools/build_variant.sh <name> -DPITT_SYNC_CHECK): synchronise
 // after every launch of a batch so that a faulting kernel is named on stderr.
 #ifdef PITT_SYNC_CHECK
 #define PITT_CHECK_LAUNCH(what, c, phase)                                                                    \
@@ -2715,9 +2729,8 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         if (int rc = xs_scratch(ctx, xs_T / kXsBlk, 9, "xr", &xr_scr)) return rc;
     }
 
-    // Everything below is stream-ordered device work with device-built work lists.  Its launches
-    // depend only on the key below, so a repeated batch layout is captured into a HIP graph and
-    // replayed with one launch (profiling runs launch directly: their events time each kernel).
+    // Everything below is stream-ordered device work with device-built work lists: no host
+    // synchronisation until the results are copied back (pitt_wait / finish_batch).
     const int sel_blocks = (int)(((int64_t)nf * tiles_max + kWaves - 1) / kWaves);
     const double log_prob = std::log(1.0 - p->probability);
     std::vector<int> acct_recs((size_t)kAcKernels, -1);
@@ -2920,88 +2933,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
 #ifdef PITT_SYNC_CHECK
     *(volatile unsigned int*)dbg_seq = seq;
 #endif
-    // Graphs (opt-in, ctx.hpp: only with the runtime's graph packet capture off) from
-    // ctx->graph_min_frames frames up
-    if (ctx->use_graphs && !ctx->prof && sm != nullptr && nf >= ctx->graph_min_frames) {
-        const double log_prob_k = std::log(1.0 - p->probability);
-        uint64_t thb = 0, lpb = 0;
-        std::memcpy(&thb, &thf, sizeof thf);
-        std::memcpy(&lpb, &log_prob_k, sizeof lpb);
-        std::vector<uint64_t> key = {ctx->arena_gen, (uint64_t)(uintptr_t)sm, (uint64_t)nf, (uint64_t)tiles_max,
-                                     (uint64_t)(uintptr_t)fr->x, (uint64_t)(uintptr_t)fr->y, (uint64_t)(uintptr_t)fr->z,
-                                     (uint64_t)(uintptr_t)inliers_dev, (uint64_t)A, (uint64_t)hcap,
-                                     (uint64_t)(uint32_t)max_iter, thb, lpb, (uint64_t)p->optimize,
-                                     (uint64_t)p->cov_mode, (uint64_t)ctx->lane_score * 2 + (uint64_t)ctx->inside_cull, (uint64_t)(ORDER * 2 + DIV),
-                                     (uint64_t)ctx->refine_producers, (uint64_t)ctx->refine_mode,
-                                     (uint64_t)ctx->xrefine, (uint64_t)ctx->refine_frames, (uint64_t)K,
-                                     (uint64_t)(xs ? xs_T : 0)};  // the walk's stream stride and grids
-        pitt_ctx::GraphEntry* hit = nullptr;
-        for (auto& g : ctx->graphs)
-            if (g.key == key) hit = &g;
-        if (!hit) {
-            // capture on the second sight of a key (a one-off layout, e.g. a support-loop iteration,
-            // launches directly: capture and instantiation cost more than one enqueue)
-            auto seen = std::find(ctx->graph_seen.begin(), ctx->graph_seen.end(), key);
-            if (seen == ctx->graph_seen.end()) {
-                ctx->graph_seen.push_back(key);
-                if (ctx->graph_seen.size() > 16) ctx->graph_seen.erase(ctx->graph_seen.begin());
-            } else {
-                hipGraph_t graph = nullptr;
-                PITT_HIP_TRY(hipStreamBeginCapture(sm, hipStreamCaptureModeRelaxed));
-                const int erc = enqueue_front(false);  // a graph keeps one stream
-                const hipError_t ce = hipStreamEndCapture(sm, &graph);
-                if (erc) {
-                    if (graph) (void)hipGraphDestroy(graph);
-                    return erc;
-                }
-                PITT_HIP_TRY(ce);
-                hipGraphExec_t exec = nullptr;
-                const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-                (void)hipGraphDestroy(graph);
-                PITT_HIP_TRY(ie);
-                if (ctx->graphs.size() >= 8) {  // evict the least recently used
-                    auto lru = std::min_element(ctx->graphs.begin(), ctx->graphs.end(),
-                                                [](const pitt_ctx::GraphEntry& a, const pitt_ctx::GraphEntry& b) {
-                                                    return a.last_use < b.last_use;
-                                                });
-                    (void)hipGraphExecDestroy(lru->exec);
-                    ctx->graphs.erase(lru);
-                }
-                ctx->graphs.push_back({key, exec, 0});
-                hit = &ctx->graphs.back();
-                ++ctx->graph_captures;
-            }
-        }
-        if (hit) {
-            hit->last_use = ++ctx->graph_clock;
-#ifdef PITT_SYNC_CHECK
-            if (ctx->dbg_sync_before_graph) PITT_HIP_TRY(hipStreamSynchronize(sm));
-#endif
-            PITT_HIP_TRY(hipGraphLaunch(hit->exec, sm));
-#ifdef PITT_SYNC_CHECK
-            {
-                const hipError_t e0 = hipStreamSynchronize(sm);
-                std::fprintf(stderr, "PITT_SYNC_CHECK graph launch nf %d K %d: %s\n", nf, K, hipGetErrorString(e0));
-                if (e0 == hipSuccess) {
-                    std::vector<int32_t> hc((size_t)nchunks + 2), hl((size_t)(nchunks + 1) * nf);
-                    (void)hipMemcpy(hc.data(), counters, hc.size() * 4, hipMemcpyDeviceToHost);
-                    (void)hipMemcpy(hl.data(), lists, hl.size() * 4, hipMemcpyDeviceToHost);
-                    std::fprintf(stderr, "PITT_SYNC_CHECK   counters");
-                    for (int32_t v : hc) std::fprintf(stderr, " %d", v);
-                    std::fprintf(stderr, " | lists");
-                    for (size_t i = 0; i < hl.size() && i < 16; ++i) std::fprintf(stderr, " %d", hl[i]);
-                    std::fprintf(stderr, "\n");
-                    for (int c = 0; c <= nchunks; ++c)
-                        if (hc[(size_t)c] > nf) return ctx->fail(PITT_E_HIP, "sync check: stale chunk counters");
-                }
-            }
-#endif
-            ++ctx->graph_replays;
-        } else {
-            const int erc = enqueue_front(er_base);
-            if (erc) return erc;
-        }
-    } else {
+    {
         const int erc = enqueue_front(er_base);
         if (erc) return erc;
     }

@@ -188,18 +188,26 @@ struct PrimRun final : PrimRunBase {
     // 1. every cloud's hypotheses and their validity flags
     //    (the clouds' sampler tables go up in one copy and their flags come back in one)
     //    (a slot that already holds the cloud's table from an earlier call -- same buffer, same arena
-    //    generation, same (n, seed, attempts) -- is not uploaded again)
+    //    generation, same slot stride A, same (n, seed, attempts) -- is not uploaded again)
     int issue_hyp() override {
         pitt_ctx::PrimTableMemo& memo = ctx->prim_tables[nm];
-        if (memo.dev != (const void*)dtab || memo.gen != ctx->arena_gen) {
+        if (memo.dev != (const void*)dtab || memo.gen != ctx->arena_gen || memo.stride != A) {
+            // another buffer, or another slot layout: every slot's device region may hold anything
             memo.dev = dtab;
             memo.gen = ctx->arena_gen;
+            memo.stride = A;
             memo.keys.clear();
         }
-        if (memo.keys.size() < (size_t)nc) memo.keys.resize((size_t)nc, std::make_tuple((int64_t)-1, 0u, (int64_t)0));
+        const auto kNone = std::make_tuple((int64_t)-1, 0u, (int64_t)0);
+        if (memo.keys.size() < (size_t)nc) memo.keys.resize((size_t)nc, kNone);
         int c0 = nc, c1 = 0, u0 = nc, u1 = 0;  // the clouds that sample; those whose table goes up
         for (int c = 0; c < nc; ++c) {
-            if (cl[c].n < M::kSample) continue;
+            if (cl[c].n < M::kSample) {
+                // no table for this cloud: the range copy below may overwrite its slot with whatever the
+                // pinned staging holds there, so the slot no longer holds a known table
+                memo.keys[(size_t)c] = kNone;
+                continue;
+            }
             st[(size_t)c].run = true;
             c0 = std::min(c0, c);
             c1 = c + 1;

@@ -163,7 +163,7 @@ void* pitt_ctx::buf(const std::string& name, size_t bytes) {
         (void)hipMemset((char*)b.p + nb, 0xA5, kCanaryBytes);
 #endif
         b.bytes = nb;
-        ++arena_gen;  // captured graphs that hold the old pointer are stale
+        ++arena_gen;  // memoised device contents at the old pointer are stale
         if (name == "tables") pool_keys.clear();  // device table pool lost
     }
     return b.p;
@@ -205,8 +205,7 @@ void pitt_ctx::check_canaries(const char* where) {
 void* pitt_ctx::pinned(const std::string& name, size_t bytes) {
     auto& e = host_pinned[name];
     if (e.second < bytes || !e.first) {
-        // an async copy queued on the stream may still read or write the old block; cached graphs
-        // hold its address in their copy nodes
+        // an async copy queued on the stream may still read or write the old block
         if (e.first) {
             drain();
             (void)hipHostFree(e.first);
@@ -321,8 +320,6 @@ void pitt_destroy(pitt_ctx* ctx) {
     (void)pitt::finish_batch(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (auto& g : ctx->graphs)
-        if (g.exec) (void)hipGraphExecDestroy(g.exec);
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     if (ctx->sentinel) (void)hipFree(ctx->sentinel);
@@ -356,13 +353,6 @@ int pitt_set_stream(pitt_ctx* ctx, void* s) {
 }
 
 void* pitt_get_stream(pitt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
-
-int pitt_graph_stats(pitt_ctx* ctx, int64_t* captures, int64_t* replays) {
-    if (!ctx) return PITT_E_INVALID;
-    if (captures) *captures = ctx->graph_captures;
-    if (replays) *replays = ctx->graph_replays;
-    return PITT_OK;
-}
 
 int pitt_schedule_stats(pitt_ctx* ctx, int64_t* continuations, int32_t* last_chunks) {
     if (!ctx) return PITT_E_INVALID;
@@ -449,21 +439,25 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     if (int rc = pitt::finish_batch(ctx)) return rc;  // a batch in flight completes first
     const int64_t C = ctx->single_chunk > 0 ? std::min<int64_t>(ctx->single_chunk, std::max<int64_t>(n, 1))
                                             : std::max<int64_t>(n, 1);
-    float* h = (float*)ctx->pinned("single_h", (size_t)cap * 3 * sizeof(float));
-    int32_t* hi = (int32_t*)ctx->pinned("single_hinl", (size_t)cap * sizeof(int32_t));
-    if (!h || !hi) return ctx->fail(PITT_E_NOMEM, "pinned allocation failed");
+    // bit 0: the caller's AoS bytes go up as they are (no host staging); bit 1: the inliers come down
+    // straight into the caller's memory (no pinned staging).  The default (3) sets both, and only the
+    // buffers a mode uses are allocated: growing a pinned block drains the context and bumps arena_gen.
+    const int mode = ctx->single_mode;
+    const bool in_staged = !(mode & 1), out_staged = !(mode & 2);
+    float* h = in_staged ? (float*)ctx->pinned("single_h", (size_t)cap * 3 * sizeof(float)) : nullptr;
+    int32_t* hi = out_staged ? (int32_t*)ctx->pinned("single_hinl", (size_t)cap * sizeof(int32_t)) : nullptr;
+    if ((in_staged && !h) || (out_staged && !hi)) return ctx->fail(PITT_E_NOMEM, "pinned allocation failed");
     float* d = (float*)ctx->buf("single_xyz", (size_t)cap * 3 * sizeof(float));
-    float* ds = (float*)ctx->buf("single_stage", (size_t)cap * 3 * sizeof(float));
+    float* ds = in_staged ? (float*)ctx->buf("single_stage", (size_t)cap * 3 * sizeof(float)) : nullptr;
     int32_t* di = (int32_t*)ctx->buf("single_inl", (size_t)cap * sizeof(int32_t));
-    if (!d || !ds || !di) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
-    // The cloud goes up in chunks of C points, each deinterleaved on the host into [x y z] runs of the
-    // pinned staging buffer and sent by ONE copy as soon as it is ready, so the DMA of chunk k runs under
-    // the deinterleave of chunk k+1; k_single_planes then lays the chunks out as the frame's planes.
+    if (!d || (in_staged && !ds) || !di) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    // Staged input: the cloud goes up in chunks of C points, each deinterleaved on the host into [x y z]
+    // runs of the pinned staging buffer and sent by ONE copy as soon as it is ready, so the DMA of chunk k
+    // runs under the deinterleave of chunk k+1; k_single_planes then lays the chunks out as the planes.
     const bool timing = ctx->host_timing;
     const double t0 = timing ? pitt::wall_ms() : 0.0;
     const int sf = stride_bytes / 4;
-    const int mode = ctx->single_mode;  // 1: the caller's AoS bytes go up as they are (A/B)
-    if ((mode & 1) && n > 0) {
+    if (!in_staged && n > 0) {
         float* da = (float*)ctx->buf("single_aos", (size_t)n * stride_bytes);
         if (!da) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
         PITT_HIP_TRY(hipMemcpyAsync(da, xyz, (size_t)n * stride_bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -471,7 +465,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
                            ctx->stream, da, n, sf, cap, d);
         PITT_HIP_TRY(hipGetLastError());
     }
-    for (int64_t b = 0; !(mode & 1) && b < n; b += C) {
+    for (int64_t b = 0; in_staged && b < n; b += C) {
         const int64_t m = std::min(C, n - b);
         float* hx = h + 3 * b;  // chunk b / C starts at 3 b (every earlier chunk is full)
         float *hy = hx + m, *hz = hx + 2 * m;
@@ -488,7 +482,7 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
         PITT_HIP_TRY(hipMemcpyAsync(ds + 3 * b, hx, (size_t)(3 * m) * sizeof(float), hipMemcpyHostToDevice,
                                     ctx->stream));
     }
-    if (!(mode & 1) && n > 0) {
+    if (in_staged && n > 0) {
         hipLaunchKernelGGL(pitt::k_single_planes, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256),
                            0, ctx->stream, ds, n, C, cap, d);
         PITT_HIP_TRY(hipGetLastError());
@@ -509,9 +503,14 @@ int pitt_plane_segment(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t strid
     // the inlier list comes back with the batch: a copy of the whole list buffer into pinned memory
     // enqueued behind it (a continuation would enqueue more work after this copy: then copy again)
     const int64_t cont0 = ctx->continuations;
-    const bool out_staged = !(mode & 2);  // bit 1: the inliers come down straight into the caller's memory
-    if (out_staged && inliers_out && n > 0)
-        PITT_HIP_TRY(hipMemcpyAsync(hi, di, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (out_staged && inliers_out && n > 0) {
+        const hipError_t ce = hipMemcpyAsync(hi, di, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
+        if (ce != hipSuccess) {
+            // the batch is in flight with its results bound for r (this frame): complete it first
+            (void)pitt::finish_batch(ctx);
+            return ctx->fail(PITT_E_HIP, std::string("hipMemcpyAsync (inliers): ") + hipGetErrorString(ce));
+        }
+    }
     rc = pitt_wait(ctx);
     if (rc < 0) return rc;
     const double t2 = timing ? pitt::wall_ms() : 0.0;

@@ -391,10 +391,11 @@ static bool is_horizontal(const float c[4], const float axis[3], float var_th) {
 // the on-support bounds (k_onsupport_bounds) and the on-support compaction are stream-ordered.
 int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const float* hz, int64_t N,
                        const pitt_support_params* sp, pitt_support_list* out, pitt_support_list_dev* dout,
-                       bool dev_in) {
+                       bool dev_in, int aos_stride) {
     hipStream_t s = ctx->stream;
-    ctx->keep_i32.clear();
-    ctx->keep_f32.clear();
+    const bool timing = ctx->host_timing;  // $PITT_HOST_TIMING=1: host phases on stderr
+    const double tm0 = timing ? wall_ms() : 0.0;
+    double tm_ransac = 0.0;
     ctx->keep_supports.clear();
     ctx->keep_supports_dev.clear();
     if (out) {
@@ -426,11 +427,18 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
     if (!O || !IT[0] || !IT[1] || !INL || !MAP[0] || !MAP[1] || !MEM || !BT || !PRE || !BB || !NON)
         return ctx->fail(PITT_E_NOMEM, "support scratch");
     // the original cloud -- iterativeCloud starts as its copy
-    const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    PITT_HIP_TRY(hipMemcpyAsync(O, hx, (size_t)N * 4, kin, s));
-    PITT_HIP_TRY(hipMemcpyAsync(O + cap, hy, (size_t)N * 4, kin, s));
-    PITT_HIP_TRY(hipMemcpyAsync(O + 2 * cap, hz, (size_t)N * 4, kin, s));
+    if (aos_stride) {  // the caller's host AoS cloud as it lies: one upload, deinterleaved on the device
+        void* scr = ctx->buf("sup_aos", (size_t)std::max<int64_t>(N, 1) * aos_stride);
+        if (!scr) return ctx->fail(PITT_E_NOMEM, "support scratch");
+        PITT_HIP_TRY(upload_aos(s, scr, hx, N, aos_stride, O, O + cap, O + 2 * cap));
+    } else {
+        const hipMemcpyKind kin = dev_in ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        PITT_HIP_TRY(hipMemcpyAsync(O, hx, (size_t)N * 4, kin, s));
+        PITT_HIP_TRY(hipMemcpyAsync(O + cap, hy, (size_t)N * 4, kin, s));
+        PITT_HIP_TRY(hipMemcpyAsync(O + 2 * cap, hz, (size_t)N * 4, kin, s));
+    }
     PITT_HIP_TRY(hipMemcpyAsync(IT[0], O, (size_t)cap * 3 * 4, hipMemcpyDeviceToDevice, s));
+    const double tm1 = timing ? wall_ms() : 0.0;
 
     pitt_sac_params p;
     pitt_sac_params_default(&p);
@@ -461,7 +469,9 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
         fr.n_frames = 1;
         fr.capacity = cap;
         pitt_plane_result r;
+        const double tr0 = timing ? wall_ms() : 0.0;
         int rc = pitt_plane_segment_batch(ctx, &fr, &p, &r, INL);  // the loop's one host round trip
+        if (timing) tm_ransac += wall_ms() - tr0;
         if (rc < 0) return rc;
         if (r.status < 0) return ctx->fail(r.status, "RANSAC inside the support loop failed");
         ++iterations;
@@ -527,6 +537,7 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
         --level;
     }
     // sizes of the on-support clouds and the z-sum path taken, in one round trip
+    const double tm2 = timing ? wall_ms() : 0.0;
     const int nsup = (int)found.size();
     std::vector<int64_t> n_on((size_t)nsup, 0);
     if (nsup > 0) {
@@ -559,31 +570,46 @@ int find_supports_impl(pitt_ctx* ctx, const float* hx, const float* hy, const fl
         dout->iterations = iterations;
         return PITT_OK;
     }
-    // host results: one copy per output at the end
+    // host results: one copy per output at the end, into the context's pinned output block (reused
+    // across calls, so no page faults and full-rate DMA; valid until the next support call)
+    auto al16 = [](size_t b) { return (b + 15) / 16 * 16; };
+    size_t out_bytes = 16;
+    for (int k = 0; k < nsup; ++k)
+        out_bytes += al16((size_t)N * 4) + al16((size_t)found[(size_t)k].n_sup * 12) + al16((size_t)n_on[(size_t)k] * 12);
+    char* hout = (char*)ctx->pinned("sup_out_h", out_bytes);
+    if (!hout) return ctx->fail(PITT_E_NOMEM, "support outputs (pinned)");
+    std::vector<char*> hmap((size_t)nsup), hsup((size_t)nsup), hon((size_t)nsup);
+    size_t o = 0;
     for (int k = 0; k < nsup; ++k) {
         const Found& fd = found[(size_t)k];
         const int64_t ns = fd.n_sup, no = n_on[(size_t)k];
-        ctx->keep_i32.emplace_back((size_t)N);
-        ctx->keep_f32.emplace_back((size_t)ns * 3);
-        ctx->keep_f32.emplace_back((size_t)no * 3);
-        std::vector<float>& sup = ctx->keep_f32[ctx->keep_f32.size() - 2];
-        std::vector<float>& on = ctx->keep_f32.back();
-        PITT_HIP_TRY(hipMemcpyAsync(ctx->keep_i32.back().data(), fd.map, (size_t)N * 4, hipMemcpyDeviceToHost, s));
-        for (int c = 0; c < 3; ++c) {
-            if (ns) PITT_HIP_TRY(hipMemcpyAsync(sup.data() + c * ns, fd.sup + c * cap, (size_t)ns * 4, hipMemcpyDeviceToHost, s));
-            if (no) PITT_HIP_TRY(hipMemcpyAsync(on.data() + c * no, fd.on + c * cap, (size_t)no * 4, hipMemcpyDeviceToHost, s));
-        }
+        hmap[(size_t)k] = hout + o;
+        o += al16((size_t)N * 4);
+        hsup[(size_t)k] = hout + o;
+        o += al16((size_t)ns * 12);
+        hon[(size_t)k] = hout + o;
+        o += al16((size_t)no * 12);
+        PITT_HIP_TRY(hipMemcpyAsync(hmap[(size_t)k], fd.map, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+        // the support / on-support planes are cap apart on the device, packed (ns / no apart) on the host
+        if (ns) PITT_HIP_TRY(hipMemcpy2DAsync(hsup[(size_t)k], (size_t)ns * 4, fd.sup, (size_t)cap * 4, (size_t)ns * 4, 3,
+                                              hipMemcpyDeviceToHost, s));
+        if (no) PITT_HIP_TRY(hipMemcpy2DAsync(hon[(size_t)k], (size_t)no * 4, fd.on, (size_t)cap * 4, (size_t)no * 4, 3,
+                                              hipMemcpyDeviceToHost, s));
     }
     PITT_HIP_TRY(hipStreamSynchronize(s));
+    if (timing)
+        std::fprintf(stderr, "pitt_find_supports N=%lld: input %.3f ms, loop %.3f ms (%d iterations, RANSAC batches "
+                     "%.3f ms), sizes + outputs D2H %.3f ms\n", (long long)N, tm1 - tm0, tm2 - tm1, iterations,
+                     tm_ransac, wall_ms() - tm2);
     for (int k = 0; k < nsup; ++k) {
         const Found& fd = found[(size_t)k];
         pitt_support su;
         su.n_points = (int32_t)N;
-        su.idx_map = ctx->keep_i32[(size_t)k].data();
+        su.idx_map = (int32_t*)hmap[(size_t)k];
         std::memcpy(su.coefficients, fd.coef, sizeof su.coefficients);
-        su.support_xyz = ctx->keep_f32[(size_t)(2 * k)].data();
+        su.support_xyz = (float*)hsup[(size_t)k];
         su.n_support = fd.n_sup;
-        su.on_support_xyz = ctx->keep_f32[(size_t)(2 * k + 1)].data();
+        su.on_support_xyz = (float*)hon[(size_t)k];
         su.n_on_support = n_on[(size_t)k];
         ctx->keep_supports.push_back(su);
     }
@@ -631,7 +657,17 @@ int pitt_find_supports(pitt_ctx* ctx, const float* x, const float* y, const floa
     if (!p || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::find_supports_impl(ctx, x, y, z, n, p, out, nullptr, false);
+    return pitt::find_supports_impl(ctx, x, y, z, n, p, out, nullptr, false, 0);
+}
+
+int pitt_find_supports_aos(pitt_ctx* ctx, const float* xyz, int64_t n, int32_t stride_bytes,
+                           const pitt_support_params* p, pitt_support_list* out) {
+    if (!ctx) return PITT_E_INVALID;
+    if (!p || !out || n < 0 || (n > 0 && !xyz)) return ctx->fail(PITT_E_INVALID, "null argument");
+    if (stride_bytes != 12 && stride_bytes != 16) return ctx->fail(PITT_E_INVALID, "stride must be 12 or 16");
+    if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
+    if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
+    return pitt::find_supports_impl(ctx, xyz, nullptr, nullptr, n, p, out, nullptr, false, stride_bytes);
 }
 
 int pitt_find_supports_dev(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
@@ -640,7 +676,7 @@ int pitt_find_supports_dev(pitt_ctx* ctx, const float* x, const float* y, const 
     if (!p || !out || n < 0 || (n > 0 && (!x || !y || !z))) return ctx->fail(PITT_E_INVALID, "null argument");
     if (n > 0x7fffffff) return ctx->fail(PITT_E_INVALID, "cloud larger than 2^31 points");
     if (hipSetDevice(ctx->device) != hipSuccess) return ctx->fail(PITT_E_HIP, "hipSetDevice");
-    return pitt::find_supports_impl(ctx, x, y, z, n, p, nullptr, out, true);
+    return pitt::find_supports_impl(ctx, x, y, z, n, p, nullptr, out, true, 0);
 }
 
 }  // extern "C"

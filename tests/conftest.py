@@ -1,11 +1,7 @@
 import os
 import sys
 
-# before any test starts HIP: the opt-in graph tests need the runtime's graph packet capture off
-# (DESIGN.md s3d); the product default (direct launches) does not depend on it
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
-import pytest  # noqa: E402
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)

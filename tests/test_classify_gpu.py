@@ -168,31 +168,30 @@ def test_batch_time_per_frame(ctx):
     assert ms < 1000.0
 
 
-def test_batch_and_services_with_graphs():
-    """The round-4 graph fault's own test (tests/test_classify_gpu.py with one-frame graphs): the same
-    comparison on a context whose plane batches are graphed from one frame up ($PITT_GRAPHS=1,
-    $PITT_GRAPH_MIN_FRAMES=1; the runtime's graph packet capture off, tests/conftest.py)."""
-    import os
-    import torch
-    old = {k: os.environ.get(k) for k in ("PITT_GRAPHS", "PITT_GRAPH_MIN_FRAMES")}
-    os.environ.update({"PITT_GRAPHS": "1", "PITT_GRAPH_MIN_FRAMES": "1"})
+def test_sampler_table_memo_across_iteration_limits(ctx, srv):
+    """The sampler-table memo (prim_ransac.hpp): a batch at max_iterations X, then one at Y < X
+    whose first cloud is too small to sample (its slot is skipped while later slots are written at the
+    Y stride, over the X layout's slot 0), then the first batch again: the repeat must not reuse slot 0's
+    overwritten table.  Equal to the first call and to the per-cluster services at X."""
+    clusters = frame_clusters(4)[:3]
+    tiny = np.random.default_rng(9).normal(0, 0.01, (2, 3)).astype(np.float32)
+    names = ["/pitt/srv/sphere_segmentation/max_iter_limit", "/pitt/srv/cylinder_segmentation/max_iter_limit",
+             "/pitt/srv/cone_segmentation/max_iter_limit"]
+
+    def run(cl, iters):
+        for n in names:
+            srv.set_param(n, iters)
+        xyz, offs, cnt = _layout(cl, gap=11)
+        return srv.classify_clusters(xyz[:, 0], xyz[:, 1], xyz[:, 2], offs, cnt)
+
     try:
-        c = pitt.Context(0)
+        first = run(clusters, 300)
+        run([tiny] + clusters[1:], 40)
+        again = run(clusters, 300)
+        for a, b in zip(first, again):
+            assert a["inliers"] == b["inliers"] and a["tag"] == b["tag"]
+            assert all(np.array_equal(_bits(x), _bits(y)) for x, y in zip(a["coefficients"], b["coefficients"]))
+        _check_against_services(ctx, srv, clusters, again)
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    s = pitt.Services(c)
-    try:
-        clusters = frame_clusters(0)
-        xyz, offs, cnt = _layout(clusters)
-        d = [torch.from_numpy(np.ascontiguousarray(xyz[:, k])).cuda() for k in range(3)]
-        got = s.classify_clusters(*d, offs, cnt)
-        _check_against_services(c, s, clusters, got)
-        _check_against_services(c, s, clusters, got)  # the services' plane layouts now replay
-        assert c.graph_stats()[1] > 0, c.graph_stats()
-    finally:
-        s.close()
-        c.close()
+        for n in names:
+            srv.erase_param(n)

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(header):
 
 
 def test_abi_version():
-    assert _lib.lib.pitt_abi_version() == 3
+    assert _lib.lib.pitt_abi_version() == 4 == _lib.PITT_ABI_VERSION
 
 
 @pytest.mark.parametrize("n", [3, 5, 4800, 307200, 1228800])

@@ -36,8 +36,7 @@ def _lists(b, res, inl):
     return [h[o:o + r["n_inliers"]].copy() for o, r in zip(b.offsets, res)]
 
 
-@pytest.mark.parametrize("graphs", [1, 0])
-def test_continuation_after_a_learnt_short_schedule(graphs):
+def test_continuation_after_a_learnt_short_schedule():
     w, h = 320, 240
     table = [pitt.synth_frame(pitt.SCENE_TABLE, 8000 + i, w, h) for i in range(6)]
     mixed = [pitt.synth_frame(pitt.SCENE_CLUTTER if i % 2 else pitt.SCENE_TABLE_NAN, 8100 + i, w, h) for i in range(6)]
@@ -45,7 +44,7 @@ def test_continuation_after_a_learnt_short_schedule(graphs):
     bm = pitt.FrameBatch.from_host(mixed, device="cuda:0")
     assert b.capacity == bm.capacity and list(b.offsets) == list(bm.offsets)
     inl = torch.empty(b.capacity, dtype=torch.int32, device="cuda:0")
-    ctx = _ctx(PITT_GRAPHS=graphs, PITT_GRAPH_MIN_FRAMES=1)  # graphs (when on) for this 6-frame layout
+    ctx = _ctx()
     full = _ctx(PITT_ADAPTIVE_CHUNKS=0)
     try:
         for _ in range(3):  # the table layout: the hint learns the short schedule

@@ -49,6 +49,48 @@ def main(reps=5, dev_only=False):
         cl_ms = np.median([b for _, b in ts])
         print(f"config5 host path: {len(sups)} supports, {ncl} clusters; find_supports {sup_ms:.2f} ms, "
               f"clusters {cl_ms:.2f} ms (median of {reps})")
+        # the C entry point alone (no Python conversion of its outputs), and the service handler
+        import ctypes
+        from pitt_object_table_segmentation_amd import _lib as L
+        xs, ys, zs = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+        fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+        out, p = L.SupportList(), pitt.support_params()
+        raw = []
+        for r in range(reps + 1):
+            t = time.perf_counter()
+            assert L.lib.pitt_find_supports(ctx.h, fp(xs), fp(ys), fp(zs), len(xs), ctypes.byref(p),
+                                            ctypes.byref(out)) == 0
+            if r:
+                raw.append((time.perf_counter() - t) * 1e3)
+        print(f"config5 pitt_find_supports (C ABI call only): {np.median(raw):.2f} ms (median of {reps})")
+        ons = [np.ascontiguousarray(s.on_support_cloud.T) for s in sups]
+        craw = []
+        cout = L.ClusterList()
+        for r in range(reps + 1):
+            t = time.perf_counter()
+            for o in ons:
+                n = o.shape[1]
+                if n >= 30:
+                    assert L.lib.pitt_euclidean_clusters(ctx.h, fp(o[0]), fp(o[1]), fp(o[2]), n, 0.03,
+                                                         int(np.floor(n * 0.01 + 0.5)), int(np.floor(n * 0.99 + 0.5)),
+                                                         ctypes.byref(cout)) == 0
+            if r:
+                craw.append((time.perf_counter() - t) * 1e3)
+        print(f"config5 pitt_euclidean_clusters (C ABI calls only, {[o.shape[1] for o in ons]} points): "
+              f"{np.median(craw):.2f} ms (median of {reps})")
+        cloud = np.stack([xs, ys, zs], 1)
+        srv = pitt.Services(ctx)
+        try:
+            sv = []
+            for r in range(reps + 1):
+                t = time.perf_counter()
+                _, res, _ = srv.find_supports(cloud)
+                if r:
+                    sv.append((time.perf_counter() - t) * 1e3)
+            print(f"config5 findSupports service (pitt_srv_find_supports + Python): {np.median(sv):.2f} ms, "
+                  f"{len(res)} supports (median of {reps})")
+        finally:
+            srv.close()
 
 
 if __name__ == "__main__":

@@ -1,13 +1,32 @@
 #!/bin/bash
-# A/B of two builds of libpitt_seg.so on the same box: bench.py alternately with the in-tree library
-# (A) and exp_libs/<B>/libpitt_seg.so, ROUNDS times each.  Output: gpurun_out/ab_<tag>_{A,B}<i>.json
+# One parametrised A/B driver (replaces the per-experiment tools/gpu_*.sh scripts).
+#   bash tools/gpu_ab.sh [-t "<pytest files>"] [-r ROUNDS] [-b "<bench.py args>"] NAME...
+# NAME "cur" is the in-tree product library; any other NAME is abv/libpitt_seg_<NAME>.so (built by
+# tools/build_variant.sh).  With -t, the listed GPU tests run first under the in-tree library;
+# then ROUNDS alternating bench runs per library, each printing value, roofline frac and the
+# first scoring chunk's average launch.  Every GPU step has its own time limit; the script stops
+# at the first failure.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT" || exit 1
+TESTS=""; ROUNDS=2; BARGS="--no-extras --no-cpu-baseline"
+while getopts "t:r:b:" o; do case $o in t) TESTS=$OPTARG;; r) ROUNDS=$OPTARG;; b) BARGS=$OPTARG;; *) exit 2;; esac; done
+shift $((OPTIND - 1))
 mkdir -p gpurun_out
-TAG=$1; B=$2; ROUNDS=${3:-2}; shift 3
-for i in $(seq 1 $ROUNDS); do
-    timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras "$@" > gpurun_out/ab_${TAG}_A$i.json \
-        2> gpurun_out/ab_${TAG}_A$i.err || exit $?
-    PITT_LIB_PATH=$PWD/exp_libs/$B/libpitt_seg.so timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras "$@" \
-        > gpurun_out/ab_${TAG}_B$i.json 2> gpurun_out/ab_${TAG}_B$i.err || exit $?
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
+  tail -1 gpurun_out/ab_tests.log
+fi
+for r in $(seq 1 $ROUNDS); do
+  for lib in "$@"; do
+    if [ "$lib" = cur ]; then unset PITT_LIB_PATH; else export PITT_LIB_PATH=$PWD/abv/libpitt_seg_$lib.so; fi
+    timeout -k 10 300 python bench.py $BARGS > gpurun_out/ab_${lib}_$r.json 2> gpurun_out/ab_${lib}_$r.err || { tail -20 gpurun_out/ab_${lib}_$r.err; exit 1; }
+    python - "$lib" "gpurun_out/ab_${lib}_$r.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+k = d.get("kernels", {})
+f = k.get("k_score.first", {}).get("avg_launch_us")
+print(sys.argv[1], round(d["value"]), d["roofline"]["frac"], d["roofline"]["avg_launch_us"], f,
+      d.get("steady_state"), {n: round(v.get("us_per_batch", 0), 1) for n, v in k.items()})
+PY
+  done
 done
