@@ -451,13 +451,16 @@ __device__ __forceinline__ int count_group(float4 c, float x, float y, float z, 
 // never grows once a hypothesis has been scored (a larger best count means a smaller k), so past
 // the first chunk the frame needs at most ceil(k) - h0 of this chunk's hypotheses (and no more
 // than it has samples for).  The first chunk is scored whole: k is still the initial 1.0 there.
+// ident: the list holds every frame of the batch (the first chunk of a batch without degenerate
+// frames), so list slot li is scored as frame li -- the same items in another order, without the
+// dependent load of the list entry at every wave's start.
 __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const int32_t* __restrict__ list,
                                                   const FrameMeta* __restrict__ meta,
-                                                  const FrameState* __restrict__ st, int h0, int H) {
+                                                  const FrameState* __restrict__ st, int h0, int H, bool ident) {
     ScoreItem r;
     const int li = it / tiles_max;
     const int t = it - li * tiles_max;
-    const int f = __builtin_amdgcn_readfirstlane(list[li]);
+    const int f = ident ? li : __builtin_amdgcn_readfirstlane(list[li]);
     const FrameMeta m = meta[f];
     const bool ok = t < m.tiles;
     r.base = m.off + (ok ? (int64_t)t * kTile : 0);
@@ -528,10 +531,12 @@ __device__ __forceinline__ void score_list32(uint32_t lb, int c, float x, float 
 // One sub-step: box, cull, score.  wc: the wave's LDS count row, [round][16 g + h'].
 // INS: a pair whose box lies certainly inside the slab (box_inside) is not scored point by point;
 // it counts the group's points with no NaN coordinate (gcnt, one ballot per group and sub-step).
+// BOX, the last sub-step of an item (last): the item's staged boxes go to HBM here (gbox: its 32 group
+// boxes, tbox: its tile box), before the sub-step's scoring.
 template <int ORDER, bool BOX, bool INS>
 __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, SubPts& P, int rem, float tv, int lane,
                                           int32_t* __restrict__ wc, float& tb, float* __restrict__ gbox,
-                                          uint32_t gsrc) {
+                                          uint32_t gsrc, bool last = false, float* __restrict__ tbox = nullptr) {
     if (__builtin_expect(rem < kSub, 0)) {  // frame tail: points past it never count, never widen a box
 #pragma unroll
         for (int g = 0; g < kGPS; ++g)
@@ -557,7 +562,9 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
         row_reduce(B);
         // the four groups' boxes, for the later chunks and the final selection: lane 16 g + i (i < 6)
-        // holds value i of group g, stores it, and folds it into the tile box (min for lo, max for hi)
+        // holds value i of group g, stages it in the wave's LDS box rows (written to HBM once per item:
+        // a global store here would sit in vmcnt between the sub-steps' loads, and every later wait for
+        // a load would wait for its write acknowledgement too), and folds it into the tile box
         const int i = lane & 15;
         float v = B.lo[0];
         v = i == 1 ? B.lo[1] : v;
@@ -565,8 +572,28 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         v = i == 3 ? B.hi[0] : v;
         v = i == 4 ? B.hi[1] : v;
         v = i == 5 ? B.hi[2] : v;
-        if (i < 6) gbox[(lane >> 4) * 8 + i] = v;
-        tb = i < 3 ? vmin(tb, v) : vmax(tb, v);
+        if (i < 6) *(__attribute__((address_space(3))) float*)(uintptr_t)(gsrc + 32u * (uint32_t)(lane >> 4) + 4u * (uint32_t)i) = v;
+        (void)tb;
+#if defined(PITT_SCORE_EXPERIMENT) && PITT_SCORE_EXPERIMENT == 3
+        if (false) {  // measurement only: no box stores
+#else
+        if (last) {
+#endif
+            // the item's boxes are complete: write them now, before this sub-step's scoring, so the
+            // stores are acknowledged while the wave still scores (a store left at the wave's end holds
+            // its slot until the acknowledgement: ~10 % of the first chunk, tools/microbench/tile_stream)
+            const uint32_t base = gsrc - 128u * (kSubs - 1);  // the item's staged rows, 32 groups x 8 floats
+            const f4v q = *(const __attribute__((address_space(3))) f4v*)(uintptr_t)(base + 16u * (uint32_t)lane);
+            reinterpret_cast<f4v*>(gbox)[lane] = q;  // 32 group boxes, 1 KB
+            // the tile box: value i (< 6) folded over the 32 groups (NaN-free min / max, as the groups')
+            float t = *(const __attribute__((address_space(3))) float*)(uintptr_t)(base + 4u * (uint32_t)(i < 6 ? i : 0));
+#pragma unroll 8
+            for (int j = 1; j < kTile / kGrp; ++j) {
+                const float u = *(const __attribute__((address_space(3))) float*)(uintptr_t)(base + 32u * j + 4u * (uint32_t)(i < 6 ? i : 0));
+                t = i < 3 ? vmin(t, u) : vmax(t, u);
+            }
+            if (lane < 6) tbox[lane] = t;
+        }
     } else {
         // later chunks: the boxes the first chunk stored, staged in LDS at the item's start (row g of
         // the row layout = group g: a broadcast read per row, no reduction)
@@ -796,7 +823,9 @@ __device__ __forceinline__ void put_coefs(float4* cl, const float4* __restrict__
 // BOX (the first chunk only): also record each tile's bounding box -- NaN points never widen it
 // -- for k_refine's tile skipping.
 #ifndef PITT_SCORE_WPE
-#define PITT_SCORE_WPE 0  // > 0: k_score's register budget set for this many waves per SIMD (an A/B variant)
+// k_score's register budget: 5 waves per SIMD (<= 96 VGPRs; without the bound the first chunk's
+// in-loop box flush takes it to 98 and 4 waves)
+#define PITT_SCORE_WPE 5
 #endif
 #if PITT_SCORE_WPE > 0
 #define PITT_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(PITT_SCORE_WPE, PITT_SCORE_WPE)))
@@ -809,15 +838,21 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box,
-    float* __restrict__ group_box) {
+    float* __restrict__ group_box, int nf) {
     PITT_DBG_GUARD();
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
     __shared__ float4 wlist[kScoreWaves][4 * kListRows];  // four survivor lists, one per group
-    __shared__ float4 wbox[kScoreWaves][BOX ? 1 : 64];  // later chunks: the item's 32 group boxes
+    __shared__ float4 wbox[kScoreWaves][64];  // the item's 32 group boxes (first chunk: staged for one store)
     __shared__ int32_t wcnt[kScoreWaves][NST * 64 * (64 / kRnd)];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int items = __builtin_amdgcn_readfirstlane(*cnt) * tiles_max;  // < 2^31 (validated)
+    // The first chunk (BOX) scores every frame of the batch: its items are all nf x tiles_max (frame
+    // f = list slot f), with no wait for the active count or the list at the wave's start -- a frame
+    // that RANSAC cannot run (n < 3, no good sample) is scored too, and k_replay never reads its
+    // counts.  Later chunks score the frames k_replay listed.
+    const int nact = BOX ? nf : __builtin_amdgcn_readfirstlane(*cnt);
+    const int items = nact * tiles_max;  // < 2^31 (validated)
+    const bool ident = BOX;
     float4* cl = wcoef[w];
     float4* wl = wlist[w];
     int32_t* wc = wcnt[w];
@@ -826,18 +861,28 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     // items strided over the grid: the grid is sized for the whole batch but capped near the chip's
     // resident capacity, so a later chunk with few active frames (or none) retires quickly
     for (int it = blockIdx.x * kScoreWaves + w; it < items; it += gridDim.x * kScoreWaves) {
-    const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H);
+    const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H, ident);
     const int Hf = cur.h;
     if (Hf <= 0) continue;  // an empty item, or a frame that needs none of this chunk
     const int rounds = (Hf + kRnd - 1) / kRnd;
     SubPts P[2];
-    load_sub(X, Y, Z, cur.base, lane, P[0]);
-    put_coefs<NST>(cl, hyp_coef + (int64_t)cur.f * hcap + h0, Hf, lane);
-    for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
+    // the item's coefficient rows (and, later chunks, its group boxes) are requested before its first
+    // points: vmcnt counts in issue order, so staging them into LDS then waits for them alone, not for
+    // the points' HBM latency (the next sub-step's loads go out that much sooner)
     float* gb = group_box + ((int64_t)cur.f * tiles_max + cur.t) * (kTile / kGrp) * 8;
-    if constexpr (!BOX) {  // the tile's group boxes (8 floats each, written by the first chunk) into LDS
-        if (lane < (kTile / kGrp) * 2) wbox[w][lane] = reinterpret_cast<const float4*>(gb)[lane];
+    float4 crow[NST], brow;
+    {
+        const float4* hc = hyp_coef + (int64_t)cur.f * hcap + h0;
+#pragma unroll
+        for (int j = 0; j < NST; ++j) crow[j] = hc[min(lane + 64 * j, max(Hf, 1) - 1)];  // rows past H repeat the last
+        if constexpr (!BOX) brow = reinterpret_cast<const float4*>(gb)[lane];  // the 32 boxes the first chunk wrote
     }
+    load_sub(X, Y, Z, cur.base, lane, P[0]);
+#pragma unroll
+    for (int j = 0; j < NST; ++j) cl[lane + 64 * j] = crow[j];
+    if constexpr (!BOX) wbox[w][lane] = brow;
+    (void)brow;
+    for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
     const uint32_t gsrc = (uint32_t)(uintptr_t)wbox[w];
     float tb = (lane & 15) < 3 ? __builtin_inff() : -__builtin_inff();  // BOX: this lane's tile-box value
     if constexpr (LANE) {  // the first chunk, H <= 32: lane-private counters (score_sub_lane)
@@ -878,13 +923,14 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     // s + 2 < kSubs, the compiler's vmcnt at the join had to assume it was not issued, so the
     // second half-step waited for sub-step s + 2's loads before scoring s + 1 (one exposed HBM
     // latency per pair of sub-steps).
+    float* tbx = tile_box + ((int64_t)cur.f * tiles_max + cur.t) * 8;
     for (int s = 0; s < kSubs; s += 2) {
         load_sub(X, Y, Z, cur.base + (s + 1) * kSub, lane, P[1]);
-        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb + s * kGPS * 8,
-                              gsrc + 128u * s);
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[0], cur.rem - s * kSub, tv, lane, wc, tb, gb, gsrc + 128u * s);
         load_sub(X, Y, Z, cur.base + min(s + 2, kSubs - 1) * kSub, lane, P[0]);
-        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb + (s + 1) * kGPS * 8,
-                              gsrc + 128u * (s + 1));
+        // BOX: the last sub-step writes the item's group and tile boxes before its scoring
+        score_sub<ORDER, BOX, INS>(cl, wl, Hf, P[1], cur.rem - (s + 1) * kSub, tv, lane, wc, tb, gb,
+                                   gsrc + 128u * (s + 1), s + 2 == kSubs, tbx);
     }
 #endif
     // counts: hypothesis h = 16 r + h' sums its four groups' lanes of round r
@@ -893,13 +939,23 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
         const int h = lane + 64 * j;
+#if defined(PITT_SCORE_EXPERIMENT) && (PITT_SCORE_EXPERIMENT == 3 || PITT_SCORE_EXPERIMENT == 4)
+        if (h < Hf && wc[h] == 0x7fffffff) {  // measurement only: no count stores
+#else
         if (h < Hf) {
+#endif
             const int32_t* row = wc + 64 * (h / kRnd) + (h % kRnd);
             out[h] = row[0] + row[16] + row[32] + row[48];
         }
     }
     }  // !LANE
-    if constexpr (BOX) {
+#if PITT_SCORE_DEPTH == 3
+    constexpr bool kBoxesAtEnd = true;
+#else
+    constexpr bool kBoxesAtEnd = LANE;  // the 2-deep loop writes them inside its last sub-step
+#endif
+    if constexpr (BOX && kBoxesAtEnd) {
+        if constexpr (!LANE) reinterpret_cast<float4*>(gb)[lane] = wbox[w][lane];  // the item's 32 group boxes, 1 KB
         // rows -> tile: value i of the four rows combined (xor 16, xor 32)
 #pragma unroll
         for (int off = 16; off <= 32; off <<= 1) {
@@ -2799,7 +2855,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fx, fy, fz, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
-                           tile_box, group_box);
+                           tile_box, group_box, nf);
     PITT_CHECK_LAUNCH("k_score", c, phase);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);

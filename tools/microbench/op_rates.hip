@@ -104,6 +104,73 @@ __global__ __launch_bounds__(256) void k(float* out, float s0, int iters) {
                             "v_cndmask_b32 %3, %3, %8, vcc\n v_cndmask_b32 %4, %4, %8, vcc\n v_cndmask_b32 %5, %5, %8, vcc\n"
                             "v_cndmask_b32 %6, %6, %8, vcc\n v_cndmask_b32 %7, %7, %8, vcc\n")
                          : OUTS : "v"(s0) : "vcc");
+        else if constexpr (MODE == 14)  // 8 x v_permlane32_swap (4 independent pairs, twice)
+            asm volatile(R8("v_permlane32_swap_b32_e32 %0, %1\n v_permlane32_swap_b32_e32 %2, %3\n"
+                            "v_permlane32_swap_b32_e32 %4, %5\n v_permlane32_swap_b32_e32 %6, %7\n"
+                            "v_permlane32_swap_b32_e32 %0, %2\n v_permlane32_swap_b32_e32 %1, %3\n"
+                            "v_permlane32_swap_b32_e32 %4, %6\n v_permlane32_swap_b32_e32 %5, %7\n")
+                         : OUTS);
+        else if constexpr (MODE == 15)  // 8 x v_permlane16_swap
+            asm volatile(R8("v_permlane16_swap_b32_e32 %0, %1\n v_permlane16_swap_b32_e32 %2, %3\n"
+                            "v_permlane16_swap_b32_e32 %4, %5\n v_permlane16_swap_b32_e32 %6, %7\n"
+                            "v_permlane16_swap_b32_e32 %0, %2\n v_permlane16_swap_b32_e32 %1, %3\n"
+                            "v_permlane16_swap_b32_e32 %4, %6\n v_permlane16_swap_b32_e32 %5, %7\n")
+                         : OUTS);
+        else if constexpr (MODE == 16)  // 8 x v_min_f32_dpp row_ror (independent registers)
+            asm volatile(R8("v_min_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %2, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %3, %3, %3 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %4, %4, %4 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %5, %5, %5 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %6, %6, %6 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+                            "v_min_f32_dpp %7, %7, %7 row_ror:8 row_mask:0xf bank_mask:0xf\n")
+                         : OUTS);
+        else if constexpr (MODE == 17)  // 8 x v_min_f32 v,v (VOP2, reference for 16)
+            asm volatile(R8("v_min_f32 %0, %0, %1\n v_min_f32 %1, %1, %2\n v_min_f32 %2, %2, %3\n v_min_f32 %3, %3, %4\n"
+                            "v_min_f32 %4, %4, %5\n v_min_f32 %5, %5, %6\n v_min_f32 %6, %6, %7\n v_min_f32 %7, %7, %0\n")
+                         : OUTS);
+        else if constexpr (MODE == 19)  // 8 x v_cndmask_b32_e64 with an SGPR-pair mask (set once per iteration)
+            asm volatile("s_mov_b32 s40, 0xffff\n s_mov_b32 s41, 0xffff\n" R8("v_cndmask_b32_e64 %0, %0, %8, s[40:41]\n v_cndmask_b32_e64 %1, %1, %8, s[40:41]\n"
+                            "v_cndmask_b32_e64 %2, %2, %8, s[40:41]\n v_cndmask_b32_e64 %3, %3, %8, s[40:41]\n"
+                            "v_cndmask_b32_e64 %4, %4, %8, s[40:41]\n v_cndmask_b32_e64 %5, %5, %8, s[40:41]\n"
+                            "v_cndmask_b32_e64 %6, %6, %8, s[40:41]\n v_cndmask_b32_e64 %7, %7, %8, s[40:41]\n")
+                         : OUTS : "v"(s0) : "s40", "s41");
+        else if constexpr (MODE == 20)  // 8 x v_bfi_b32 with a VGPR mask
+            asm volatile(R8("v_bfi_b32 %0, %9, %0, %8\n v_bfi_b32 %1, %9, %1, %8\n v_bfi_b32 %2, %9, %2, %8\n"
+                            "v_bfi_b32 %3, %9, %3, %8\n v_bfi_b32 %4, %9, %4, %8\n v_bfi_b32 %5, %9, %5, %8\n"
+                            "v_bfi_b32 %6, %9, %6, %8\n v_bfi_b32 %7, %9, %7, %8\n")
+                         : OUTS : "v"(s0), "v"(c0));
+        else if constexpr (MODE == 21)  // 8 x v_min3_f32
+            asm volatile(R8("v_min3_f32 %0, %0, %1, %8\n v_min3_f32 %1, %1, %2, %8\n v_min3_f32 %2, %2, %3, %8\n"
+                            "v_min3_f32 %3, %3, %4, %8\n v_min3_f32 %4, %4, %5, %8\n v_min3_f32 %5, %5, %6, %8\n"
+                            "v_min3_f32 %6, %6, %7, %8\n v_min3_f32 %7, %7, %0, %8\n")
+                         : OUTS : "v"(s0));
+        else if constexpr (MODE == 22)  // 8 x v_mov_b32
+            asm volatile(R8("v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %4\n"
+                            "v_mov_b32 %4, %5\n v_mov_b32 %5, %6\n v_mov_b32 %6, %7\n v_mov_b32 %7, %0\n")
+                         : OUTS);
+        else if constexpr (MODE == 23)  // 8 x v_cndmask_b32_e32 vcc, VCC written by a v_cmp once per iteration
+            asm volatile("v_cmp_lt_f32_e32 vcc, %0, %8\n" R8("v_cndmask_b32 %0, %0, %8, vcc\n v_cndmask_b32 %1, %1, %8, vcc\n v_cndmask_b32 %2, %2, %8, vcc\n"
+                            "v_cndmask_b32 %3, %3, %8, vcc\n v_cndmask_b32 %4, %4, %8, vcc\n v_cndmask_b32 %5, %5, %8, vcc\n"
+                            "v_cndmask_b32 %6, %6, %8, vcc\n v_cndmask_b32 %7, %7, %8, vcc\n")
+                         : OUTS : "v"(s0) : "vcc");
+        else if constexpr (MODE == 24)  // 8 x v_max_f32_e64 |a|, |b|
+            asm volatile(R8("v_max_f32_e64 %0, |%0|, |%1|\n v_max_f32_e64 %1, |%1|, |%2|\n v_max_f32_e64 %2, |%2|, |%3|\n"
+                            "v_max_f32_e64 %3, |%3|, |%4|\n v_max_f32_e64 %4, |%4|, |%5|\n v_max_f32_e64 %5, |%5|, |%6|\n"
+                            "v_max_f32_e64 %6, |%6|, |%7|\n v_max_f32_e64 %7, |%7|, |%0|\n")
+                         : OUTS);
+        else if constexpr (MODE == 25)  // 8 x v_add_f32 (dependency pattern of mode 17)
+            asm volatile(R8("v_add_f32 %0, %0, %1\n v_add_f32 %1, %1, %2\n v_add_f32 %2, %2, %3\n v_add_f32 %3, %3, %4\n"
+                            "v_add_f32 %4, %4, %5\n v_add_f32 %5, %5, %6\n v_add_f32 %6, %6, %7\n v_add_f32 %7, %7, %0\n")
+                         : OUTS);
+        else if constexpr (MODE == 18)  // 8 x ds_swizzle_b32 (row rotate), then one wait
+            asm volatile(R8("ds_swizzle_b32 %0, %0 offset:swizzle(SWAP,8)\n ds_swizzle_b32 %1, %1 offset:swizzle(SWAP,8)\n"
+                            "ds_swizzle_b32 %2, %2 offset:swizzle(SWAP,8)\n ds_swizzle_b32 %3, %3 offset:swizzle(SWAP,8)\n"
+                            "ds_swizzle_b32 %4, %4 offset:swizzle(SWAP,8)\n ds_swizzle_b32 %5, %5 offset:swizzle(SWAP,8)\n"
+                            "ds_swizzle_b32 %6, %6 offset:swizzle(SWAP,8)\n ds_swizzle_b32 %7, %7 offset:swizzle(SWAP,8)\n"
+                            "s_waitcnt lgkmcnt(0)\n")
+                         : OUTS);
     }
     if (v0 + v1 + v2 + v3 + v4 + v5 + v6 + v7 + c0 + c1 == 1.2345f) out[threadIdx.x] = 1.0f;
 }
@@ -132,12 +199,18 @@ int main() {
     const char* names[] = {"v_fma_f32 x8", "v_cmp_e32 vcc x8", "v_writelane x8", "v_sub_e64 |v| x8",
                            "v_pk_fma_f32 x8", "v_addc vcc x8", "entry: current x2 (18 ops)",
                            "entry: fma+cmp+amb x2 (16 ops)", "entry: fma+sq+vcc+pack x2 (14 ops)", "v_bcnt x8",
-                           "v_cmp_e64 sgpr x8", "v_mul_f32 x8", "v_pk_mul_f32 x8", "v_cndmask vcc x8"};
-    float (*fns[14])(float*, int, int) = {run<0>, run<1>, run<2>, run<3>, run<4>, run<5>, run<6>,
-                                           run<7>, run<8>, run<9>, run<10>, run<11>, run<12>, run<13>};
-    for (int wpe : {4, 8}) {
+                           "v_cmp_e64 sgpr x8", "v_mul_f32 x8", "v_pk_mul_f32 x8", "v_cndmask vcc x8",
+                           "v_permlane32_swap x8", "v_permlane16_swap x8", "v_min_f32_dpp row_ror x8",
+                           "v_min_f32 x8", "ds_swizzle x8 + wait", "v_cndmask_e64 sgpr x8", "v_bfi_b32 x8",
+                           "v_min3_f32 x8", "v_mov_b32 x8", "v_cndmask_e32 vcc(cmp) x8", "v_max_f32 |.| x8",
+                           "v_add_f32 (chain 17) x8"};
+    float (*fns[26])(float*, int, int) = {run<0>, run<1>, run<2>, run<3>, run<4>, run<5>, run<6>,
+                                           run<7>, run<8>, run<9>, run<10>, run<11>, run<12>, run<13>,
+                                           run<14>, run<15>, run<16>, run<17>, run<18>, run<19>, run<20>,
+                                           run<21>, run<22>, run<23>, run<24>, run<25>};
+    for (int wpe : {5}) {
         const int blocks = 256 * wpe;
-        for (int m = 0; m < 14; ++m) {
+        for (int m : {11, 25, 17, 21, 24, 22, 13, 19, 23, 20, 14, 16}) {
             printf("%-36s waves/SIMD %d: ", names[m], wpe);
             fflush(stdout);
             const float ms = fns[m](out, blocks, iters);
