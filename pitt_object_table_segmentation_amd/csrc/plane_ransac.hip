@@ -592,7 +592,7 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
                 const float u = *(const __attribute__((address_space(3))) float*)(uintptr_t)(base + 32u * j + 4u * (uint32_t)(i < 6 ? i : 0));
                 t = i < 3 ? vmin(t, u) : vmax(t, u);
             }
-            if (lane < 6) tbox[lane] = t;
+            if (lane < 8) tbox[lane] = t;  // the whole 32-byte sector (values 6, 7: padding)
         }
     } else {
         // later chunks: the boxes the first chunk stored, staged in LDS at the item's start (row g of
@@ -882,7 +882,9 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     for (int j = 0; j < NST; ++j) cl[lane + 64 * j] = crow[j];
     if constexpr (!BOX) wbox[w][lane] = brow;
     (void)brow;
-    for (int r = 0; r < rounds; ++r) wc[64 * r + lane] = 0;
+    // the count rows stored below: whole 32-count lines (rows past the rounds stay zero)
+    const int hw = (Hf + 31) & ~31;
+    for (int r = 0; r < hw / kRnd; ++r) wc[64 * r + lane] = 0;
     const uint32_t gsrc = (uint32_t)(uintptr_t)wbox[w];
     float tb = (lane & 15) < 3 ? __builtin_inff() : -__builtin_inff();  // BOX: this lane's tile-box value
     if constexpr (LANE) {  // the first chunk, H <= 32: lane-private counters (score_sub_lane)
@@ -940,9 +942,9 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     for (int j = 0; j < NST; ++j) {
         const int h = lane + 64 * j;
 #if defined(PITT_SCORE_EXPERIMENT) && (PITT_SCORE_EXPERIMENT == 3 || PITT_SCORE_EXPERIMENT == 4)
-        if (h < Hf && wc[h] == 0x7fffffff) {  // measurement only: no count stores
+        if (h < hw && wc[h] == 0x7fffffff) {  // measurement only: no count stores
 #else
-        if (h < Hf) {
+        if (h < hw) {
 #endif
             const int32_t* row = wc + 64 * (h / kRnd) + (h % kRnd);
             out[h] = row[0] + row[16] + row[32] + row[48];
@@ -962,7 +964,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
             const float o = __shfl_xor(tb, off, 64);
             tb = (lane & 15) < 3 ? vmin(tb, o) : vmax(tb, o);
         }
-        if (lane < 6) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = tb;
+        if (lane < 8) tile_box[((int64_t)cur.f * tiles_max + cur.t) * 8 + lane] = tb;
     }
     }
 }
@@ -2707,8 +2709,9 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     float4* hyp_coef = as<float4>(ctx->buf("hyp_coef", (size_t)nf * hcap * sizeof(float4)));
     int32_t* hyp_attempt = as<int32_t>(ctx->buf("hyp_attempt", (size_t)nf * hcap * 4));
     int32_t* hyp_total = as<int32_t>(ctx->buf("hyp_total", (size_t)nf * hcap * 4));
-    // rows padded by 64 counts: k_score's stores cover ceil(H / 64) * 64 entries unpredicated
-    const int hstride = hcap + 64;
+    // rows padded by 64 counts (k_score's stores may cover up to ceil(H / 64) * 64 entries) and aligned
+    // to 128 B: a chunk's counts (h0 and its stores' extent multiples of 32) fill whole cache lines
+    const int hstride = (hcap + 64 + 31) & ~31;
     int32_t* tile_counts = as<int32_t>(ctx->buf("tile_counts", (size_t)nf * hstride * tiles_max * 4));
     FrameState* st = as<FrameState>(ctx->buf("state", (size_t)nf * sizeof(FrameState)));
     int32_t* lists = as<int32_t>(ctx->buf("lists", (size_t)(nchunks + 1) * nf * 4));
