@@ -294,6 +294,17 @@ struct SubPts {
     float x[kGPS], y[kGPS], z[kGPS];
 };
 
+// One entry of a later chunk's work list, written by the k_replay that lists the frame: everything
+// k_score needs to resolve the frame's items in one load (instead of the list entry, then the frame's
+// metadata and state behind it).
+struct ScoreSlot {
+    int64_t off, n;  // the frame's first point and points
+    int32_t f;       // the frame
+    int32_t tiles;
+    int32_t h;       // hypotheses of the chunk the frame can still need (resolve_item's limit)
+    int32_t pad;
+};
+
 struct ScoreItem {
     int64_t base;  // first point of the tile (global)
     int32_t rem;   // points of the frame from the tile start, clamped to kTile
@@ -474,6 +485,21 @@ __device__ __forceinline__ ScoreItem resolve_item(int it, int tiles_max, const i
         h = max(0, min(h, min(need, st[f].n_avail - h0)));
     }
     r.h = __builtin_amdgcn_readfirstlane(h);
+    return r;
+}
+
+// The same for a later chunk's item from its list slot (k_replay wrote the frame's limit there).
+__device__ __forceinline__ ScoreItem resolve_slot(int it, int tiles_max, const ScoreSlot* __restrict__ slots, int H) {
+    ScoreItem r;
+    const int li = it / tiles_max;
+    const int t = it - li * tiles_max;
+    const ScoreSlot sl = slots[li];
+    const bool ok = t < sl.tiles;
+    r.base = sl.off + (ok ? (int64_t)t * kTile : 0);
+    r.rem = ok ? (int32_t)min(sl.n - (int64_t)t * kTile, (int64_t)kTile) : 0;
+    r.f = sl.f;
+    r.t = t;
+    r.h = __builtin_amdgcn_readfirstlane(ok ? min(sl.h, H) : 0);
     return r;
 }
 
@@ -838,7 +864,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     const FrameMeta* __restrict__ meta, const FrameState* __restrict__ st, const float4* __restrict__ hyp_coef,
     int hcap, int hstride, const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int tiles_max,
     int h0, int H, float thf, int32_t* __restrict__ tile_counts, float* __restrict__ tile_box,
-    float* __restrict__ group_box, int nf) {
+    float* __restrict__ group_box, int nf, const ScoreSlot* __restrict__ slots) {
     PITT_DBG_GUARD();
     __shared__ float4 wcoef[kScoreWaves][NST * 64];
     __shared__ float4 wlist[kScoreWaves][4 * kListRows];  // four survivor lists, one per group
@@ -861,7 +887,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) PITT_SCORE_ATTR void k_score(
     // items strided over the grid: the grid is sized for the whole batch but capped near the chip's
     // resident capacity, so a later chunk with few active frames (or none) retires quickly
     for (int it = blockIdx.x * kScoreWaves + w; it < items; it += gridDim.x * kScoreWaves) {
-    const ScoreItem cur = resolve_item(it, tiles_max, list, meta, st, h0, H, ident);
+    const ScoreItem cur = BOX ? resolve_item(it, tiles_max, list, meta, st, h0, H, ident) : resolve_slot(it, tiles_max, slots, H);
     const int Hf = cur.h;
     if (Hf <= 0) continue;  // an empty item, or a frame that needs none of this chunk
     const int rounds = (Hf + kRnd - 1) / kRnd;
@@ -980,7 +1006,8 @@ __global__ __launch_bounds__(kBlock) void k_replay(
     int32_t* __restrict__ hyp_total, int32_t* __restrict__ next_list, int32_t* __restrict__ next_cnt,
     ChunkStat* __restrict__ next_stat, const float* __restrict__ X, const float* __restrict__ Y,
     const float* __restrict__ Z, const int32_t* __restrict__ tables, int A, int target_next,
-    float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt, unsigned long long* __restrict__ acct) {
+    float4* __restrict__ hyp_coef, int32_t* __restrict__ hyp_attempt, unsigned long long* __restrict__ acct,
+    ScoreSlot* __restrict__ next_slot) {
     PITT_DBG_GUARD();
     __shared__ GenLds G;
     __shared__ int32_t part[kBlock / 64][kMaxChunk];
@@ -1061,6 +1088,10 @@ extend:
         if (!s.done) {
             const int idx = atomicAdd(next_cnt, 1);
             next_list[idx] = f;
+            // the next chunk's limit for this frame (resolve_item's, with the state just decided)
+            const int hn0 = h0 + H, Hn1 = max(0, target_next - hn0);
+            const int need = s.k < (double)(hn0 + Hn1) ? (int)ceil(s.k) - hn0 : Hn1;
+            next_slot[idx] = ScoreSlot{m.off, m.n, f, m.tiles, max(0, min(Hn1, min(need, s.n_avail - hn0))), 0};
             atomicAdd(&next_stat->tiles, m.tiles);
             atomicAdd((unsigned long long*)&next_stat->points, (unsigned long long)m.n);
         }
@@ -2330,25 +2361,32 @@ __global__ __launch_bounds__(kBlock) void k_sel_mark(
     float thf, int n_frames, int tiles_max, const float* __restrict__ tile_box, const float* __restrict__ group_box,
     uint32_t* __restrict__ sel_bits, int32_t* __restrict__ sel_cnt, uint32_t* __restrict__ acct_tile) {
     PITT_DBG_GUARD();
+    (void)tile_box;
     const int lane = threadIdx.x & 63;
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
     if (f >= n_frames) return;
+    const int64_t row = (int64_t)f * tiles_max + t;
+    // the tile's 32 group boxes (lane g: group g), requested with the frame's metadata rather than
+    // behind it and behind a tile-box test: one dependent memory latency per wave instead of three
+    // (a tile whose box misses the slab has every group box missing it too)
+    const float4* gbp = reinterpret_cast<const float4*>(group_box + (row * kSelGroups + (lane & (kSelGroups - 1))) * 8);
+    const float4 b0 = gbp[0], b1 = gbp[1];
     const FrameMeta m = meta[f];
     if (t >= m.tiles || !st[f].has_model) return;
     const float4 c = final_coef[f];
-    const int64_t row = (int64_t)f * tiles_max + t;
     uint32_t word = 0;
-    unsigned long long moved = 32ull + 256ull + 4ull;  // tile box in; predicate bits and count out
-    if (!box_misses_slab(tile_box + row * 8, c, thf)) {
-        const int rem = (int)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
-        const int64_t p0 = m.off + (int64_t)t * kTile + lane;
-        float tv;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
-        // groups whose box certainly misses the slab hold no inlier: not read (lane g tests group g)
-        const bool gact = lane < kSelGroups && !box_misses_slab(group_box + (row * kSelGroups + lane) * 8, c, thf);
-        const uint32_t gm = (uint32_t)__builtin_amdgcn_ballot_w64(gact);
-        moved += 32ull * kSelGroups + 12ull * 64ull * (unsigned long long)__builtin_popcount(gm);
+    const int rem = (int)min(m.n - (int64_t)t * kTile, (int64_t)kTile);
+    const int64_t p0 = m.off + (int64_t)t * kTile + lane;
+    float tv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(thf));
+    // groups whose box certainly misses the slab hold no inlier: not read (lane g tests group g)
+    const float gb6[6] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y};
+    const bool gact = lane < kSelGroups && !box_misses_slab(gb6, c, thf);
+    const uint32_t gm = (uint32_t)__builtin_amdgcn_ballot_w64(gact);
+    const unsigned long long moved = 32ull * kSelGroups + 12ull * 64ull * (unsigned long long)__builtin_popcount(gm) +
+                                     256ull + 4ull;  // group boxes and live groups in; bits and count out
+    if (gm) {
         float px[kSelGroups], py[kSelGroups], pz[kSelGroups];  // the tile's live groups in flight
 #pragma unroll
         for (int g = 0; g < kSelGroups; ++g) {
@@ -2382,6 +2420,8 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
     const int it = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     const int f = it / tiles_max, t = it - f * tiles_max;
     if (f >= n_frames) return;
+    // the tile's predicate bits, requested with the metadata (valid memory for every tile slot)
+    const uint32_t word = sel_bits[((int64_t)f * tiles_max + t) * 64 + lane];
     const FrameMeta m = meta[f];
     if (t >= m.tiles || !st[f].has_model) return;
     const int32_t* cnt = sel_cnt + (int64_t)f * tiles_max;
@@ -2394,7 +2434,6 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(
     if (lane == 0 && acct_tile)
         acct_tile[(int64_t)f * tiles_max + t] = 4u * (uint32_t)(t + 1) + (inliers && mine ? 256u + 4u * (uint32_t)mine : 0u);
     if (!inliers || mine == 0) return;
-    const uint32_t word = sel_bits[((int64_t)f * tiles_max + t) * 64 + lane];
     int32_t* out = inliers + m.off + pre;
     const int32_t i0 = t * kTile + lane;
 #pragma unroll
@@ -2715,6 +2754,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     int32_t* tile_counts = as<int32_t>(ctx->buf("tile_counts", (size_t)nf * hstride * tiles_max * 4));
     FrameState* st = as<FrameState>(ctx->buf("state", (size_t)nf * sizeof(FrameState)));
     int32_t* lists = as<int32_t>(ctx->buf("lists", (size_t)(nchunks + 1) * nf * 4));
+    ScoreSlot* slots = as<ScoreSlot>(ctx->buf("score_slots", (size_t)(nchunks + 1) * nf * sizeof(ScoreSlot)));
     // counters + chunk stats in one zeroed block
     const size_t cnt_bytes = (size_t)(nchunks + 2) * 4;  // + k_xrefine's fallback count
     const size_t stat_off = (cnt_bytes + 15) & ~(size_t)15;
@@ -2742,7 +2782,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
     uint32_t* sel_bits = as<uint32_t>(ctx->buf("sel_bits", (size_t)nf * tiles_max * 64 * 4));
     int32_t* sel_cnt = as<int32_t>(ctx->buf("sel_cnt", (size_t)nf * tiles_max * 4));
     pitt_plane_result* dres = as<pitt_plane_result>(ctx->buf("results", (size_t)nf * sizeof(pitt_plane_result)));
-    if (!hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
+    if (!slots || !hyp_coef || !tile_counts || !n_final || !tile_box || !group_box || !sel_bits || !sel_cnt || !dres) return ctx->fail(PITT_E_NOMEM, "device allocation failed");
     int32_t* xfallback = ctx->xrefine ? as<int32_t>(ctx->buf("xfallback", (size_t)nf * 4)) : nullptr;
     if (ctx->xrefine && !xfallback) return ctx->fail(PITT_E_NOMEM, "refinement flags");
     CovPart* part = nullptr;
@@ -2858,7 +2898,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         const int score_blocks = (int)(c == 0 ? all_blocks : std::min<int64_t>(all_blocks, kScoreGridCap));
         hipLaunchKernelGGL(kern, dim3(score_blocks), dim3(64 * kScoreWaves), 0, sm, fx, fy, fz, meta, st, hyp_coef,
                            hcap, hstride, lists + (size_t)c * nf, counters + c, tiles_max, h0, H, thf, tile_counts,
-                           tile_box, group_box, nf);
+                           tile_box, group_box, nf, slots + (size_t)c * nf);
     PITT_CHECK_LAUNCH("k_score", c, phase);
         ctx->prof_end(rec);
         rec = ctx->prof_begin("k_replay", 0.0);
@@ -2867,7 +2907,7 @@ static int run_plane_batch(pitt_ctx* ctx, const pitt_frames* fr, const pitt_sac_
         hipLaunchKernelGGL((k_replay<ORDER, DIV>), dim3(nf), dim3(kBlock), 0, sm, tile_counts, hcap, hstride,
                            tiles_max, h0, H, max_iter, log_prob, meta, st, hyp_total, lists + (size_t)(c + 1) * nf,
                            counters + c + 1, cstat + c + 1, fx, fy, fz, tables, A, target_next, hyp_coef,
-                           hyp_attempt, acct);
+                           hyp_attempt, acct, slots + (size_t)(c + 1) * nf);
     PITT_CHECK_LAUNCH("k_replay", c, phase);
         ctx->prof_end(rec);
         if (er && c == 0 && c1 >= 2) {

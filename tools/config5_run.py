@@ -81,6 +81,29 @@ def main(reps=5, dev_only=False):
         cloud = np.stack([xs, ys, zs], 1)
         srv = pitt.Services(ctx)
         try:
+            # the C++ handler alone, as a ROS node calls it (SegmentationServices::findSupports through the
+            # flat ABI on a PointXYZ-layout cloud prepared once; its outputs stay in the service object)
+            c16 = np.zeros((len(xs), 4), np.float32)
+            c16[:, 0], c16[:, 1], c16[:, 2] = xs, ys, zs
+            req = L.SrvSupportRequest()
+            for fld in ("min_iterative_cloud_percentual_size", "min_iterative_plane_percentual_size",
+                        "variance_threshold_for_horizontal", "ransac_distance_point_in_shape_threshold",
+                        "ransac_model_normal_distance_weigth"):
+                setattr(req, fld, -1.0)
+            req.ransac_max_iteration_threshold = -1
+            req.n_horizontal_axis, req.n_edge_remove_offset = 1, 1
+            req.horizontal_axis[0] = req.edge_remove_offset[0] = -1.0
+            ns, used = ctypes.c_int32(), np.zeros(13, np.float32)
+            hv = []
+            for r in range(reps + 1):
+                t = time.perf_counter()
+                rc = L.lib.pitt_srv_find_supports(srv.h, fp(c16), len(xs), len(xs), ctypes.byref(req), ctypes.byref(ns),
+                                                  fp(used))
+                if r:
+                    hv.append((time.perf_counter() - t) * 1e3)
+                assert rc >= 0
+            print(f"config5 findSupports service handler (C++ SegmentationServices::findSupports, flat ABI call "
+                  f"only): {np.median(hv):.2f} ms, {ns.value} supports (median of {reps})")
             sv = []
             for r in range(reps + 1):
                 t = time.perf_counter()
