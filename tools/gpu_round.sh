@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 GPU pass: the whole -m gpu suite, then the default bench line.  Every step under its own time
+# A round's GPU pass: the whole -m gpu suite, then the default bench line.  Every step under its own time
 # limit.  Test failures (pytest exit 1) still let the bench run, unless the log holds a GPU fault; a
 # fault, time limit, crash or abort stops the script there (nothing more runs on the GPU).
-#   bash tools/gpu_r05.sh <tag>
+#   bash tools/gpu_round.sh <tag>
 set -o pipefail
-TAG=${1:-r05a}
+TAG=${1:-r06a}
 OUT=gpurun_out
 mkdir -p $OUT
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider \
