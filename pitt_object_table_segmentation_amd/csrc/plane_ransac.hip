@@ -289,6 +289,12 @@ constexpr int kMaxScoreChunk = 256;        // hypotheses per k_score launch (NST
 #define PITT_SCORE_GRID_CAP (256 * 32)
 #endif
 constexpr int kScoreGridCap = PITT_SCORE_GRID_CAP;  // blocks of a later chunk's launch (~ resident capacity)
+// PITT_SCORE_EXPERIMENT (undefined in every library build): measurement-only variants that drop parts
+// of k_score to time the rest, with wrong counts by design: 1 no list walks,
+// 2 the group boxes only, 3 no stores, 4 no count stores.
+#if defined(PITT_SCORE_EXPERIMENT) && (defined(PITT_AB_VARIANTS) || !defined(PITT_MEASUREMENT_ONLY))
+#error "PITT_SCORE_EXPERIMENT builds give wrong counts: build them only with -DPITT_MEASUREMENT_ONLY, outside the product and A/B libraries"
+#endif
 
 struct SubPts {
     float x[kGPS], y[kGPS], z[kGPS];
