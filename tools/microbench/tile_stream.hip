@@ -300,5 +300,11 @@ int main() {
     RUN("BOX store 256 B", (k_regs<2, 0, 0, 1, false, 6>), per_item);
     RUN("BOX tile box only", (k_regs<2, 0, 0, 1, false, 2>), per_item);
     RUN("BOX no store", (k_regs<2, 0, 0, 3, false>), per_item);
+    RUN("regs d2 META", (k_regs<2, 0, 0, 0, true>), per_item);
+    RUN("BOX no store META", (k_regs<2, 0, 0, 3, true>), per_item);
+    RUN("BOX no store W=100", (k_regs<2, 100, 0, 3, false>), per_item);
+    RUN("BOX no store W=200", (k_regs<2, 200, 0, 3, false>), per_item);
+    RUN("BOX no store W=300", (k_regs<2, 300, 0, 3, false>), per_item);
+    RUN("BOX store 1 KB W=300", (k_regs<2, 300, 0, 1, false, 0>), per_item);
     return 0;
 }
