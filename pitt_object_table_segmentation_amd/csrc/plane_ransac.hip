@@ -593,18 +593,21 @@ __device__ __forceinline__ void score_sub(const float4* cl, float4* wl, int Hf, 
         coord_box(P.y[0], P.y[1], P.y[2], P.y[3], B.lo[1], B.hi[1]);
         coord_box(P.z[0], P.z[1], P.z[2], P.z[3], B.lo[2], B.hi[2]);
         row_reduce(B);
-        // the four groups' boxes, for the later chunks and the final selection: lane 16 g + i (i < 6)
-        // holds value i of group g, stages it in the wave's LDS box rows (written to HBM once per item:
-        // a global store here would sit in vmcnt between the sub-steps' loads, and every later wait for
-        // a load would wait for its write acknowledgement too), and folds it into the tile box
+        // the four groups' boxes, for the later chunks and the final selection: row g holds group g's
+        // six values; its first lane stages them in the wave's LDS box rows (written to HBM once per
+        // item: a global store here would sit in vmcnt between the sub-steps' loads, and every later
+        // wait for a load would wait for its write acknowledgement too)
+        if ((lane & 15) == 0) {
+            typedef __attribute__((address_space(3))) float lf;
+            lf* row = (lf*)(uintptr_t)(gsrc + 32u * (uint32_t)(lane >> 4));
+            row[0] = B.lo[0];
+            row[1] = B.lo[1];
+            row[2] = B.lo[2];
+            row[3] = B.hi[0];
+            row[4] = B.hi[1];
+            row[5] = B.hi[2];
+        }
         const int i = lane & 15;
-        float v = B.lo[0];
-        v = i == 1 ? B.lo[1] : v;
-        v = i == 2 ? B.lo[2] : v;
-        v = i == 3 ? B.hi[0] : v;
-        v = i == 4 ? B.hi[1] : v;
-        v = i == 5 ? B.hi[2] : v;
-        if (i < 6) *(__attribute__((address_space(3))) float*)(uintptr_t)(gsrc + 32u * (uint32_t)(lane >> 4) + 4u * (uint32_t)i) = v;
         (void)tb;
 #if defined(PITT_SCORE_EXPERIMENT) && PITT_SCORE_EXPERIMENT == 3
         if (false) {  // measurement only: no box stores
