@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pitt_srv.h"
@@ -320,16 +321,41 @@ bool SegmentationServices::findSupports(pitt_msgs::SupportSegmentation::Request&
 }
 
 namespace {
+// f(i0, i1) over [0, n) in up to 8 host threads (chunks of at least 2^17): the response of a
+// 1.2M-point scene is ~25 MB of copies, ~5 ms on one core
+template <class F>
+void host_parallel(int64_t n, F f) {
+    const int64_t kMin = 1 << 17;
+    const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, n / kMin));
+    if (nt <= 1) {
+        f((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    for (int t = 1; t < nt; ++t) th.emplace_back(f, n * t / nt, n * (t + 1) / nt);
+    f((int64_t)0, n / nt);
+    for (std::thread& x : th) x.join();
+}
+
 // SoA planes (n apart) -> a PointXYZ message cloud (x, y, z, 1), sized once
 void planes_to_cloud(const float* p, int64_t n, pitt_msgs::PointCloud& c) {
     c.data.resize((size_t)n * 4);
     float* d = c.data.data();
-    for (int64_t i = 0; i < n; ++i) {
-        d[4 * i] = p[i];
-        d[4 * i + 1] = p[n + i];
-        d[4 * i + 2] = p[2 * n + i];
-        d[4 * i + 3] = 1.0f;
-    }
+    host_parallel(n, [=](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            d[4 * i] = p[i];
+            d[4 * i + 1] = p[n + i];
+            d[4 * i + 2] = p[2 * n + i];
+            d[4 * i + 3] = 1.0f;
+        }
+    });
+}
+
+void copy_ints(const int32_t* src, int64_t n, std::vector<int32_t>& dst) {
+    dst.resize((size_t)n);
+    int32_t* d = dst.data();
+    host_parallel(n, [=](int64_t i0, int64_t i1) { std::memcpy(d + i0, src + i0, (size_t)(i1 - i0) * 4); });
 }
 }  // namespace
 
@@ -339,8 +365,8 @@ bool SegmentationServices::findSupports(const float* xyz16, size_t n, size_t n_n
     const pitt_support_params sp = resolveSupport(req);
     const float ndw = srvm::getServiceFloatParameter(req.ransac_model_normal_distance_weigth, 0.9f);
 
-    res.supports_description.clear();
     status_ = PITT_OK;
+    size_t found = 0;
     // The first RANSAC call runs with the request's normals: a size mismatch fails it (A1) and the
     // loop exits before any support is found.  Later rounds re-estimate normals of matching size.
     if (n_normals == n) {
@@ -348,21 +374,24 @@ bool SegmentationServices::findSupports(const float* xyz16, size_t n, size_t n_n
         pitt_support_list L;
         status_ = pitt_find_supports_aos(ctx_, xyz16, (int64_t)n, 16, &sp, &L);
         if (status_ == PITT_OK) {
-            res.supports_description.reserve((size_t)L.n_supports);
-            for (int s = 0; s < L.n_supports; ++s) {
+            // a response used again keeps its supports' buffers: assign / resize refill them in place
+            // (a config-5 response is ~25 MB; fresh vectors would fault every page in again)
+            found = (size_t)L.n_supports;
+            if (res.supports_description.size() < found) res.supports_description.resize(found);
+            for (size_t s = 0; s < found; ++s) {
                 const pitt_support& su = L.supports[s];
-                pitt_msgs::Support m;
-                m.inliers.assign(su.idx_map, su.idx_map + su.n_points);
+                pitt_msgs::Support& m = res.supports_description[s];
+                copy_ints(su.idx_map, su.n_points, m.inliers);
                 planes_to_cloud(su.support_xyz, su.n_support, m.support_cloud);
                 planes_to_cloud(su.on_support_xyz, su.n_on_support, m.on_support_cloud);
                 m.support_coefficient_a = su.coefficients[0];
                 m.support_coefficient_b = su.coefficients[1];
                 m.support_coefficient_c = su.coefficients[2];
                 m.support_coefficient_d = su.coefficients[3];
-                res.supports_description.push_back(std::move(m));
             }
         }
     }
+    res.supports_description.resize(found);
     res.used_min_iterative_cloud_percentual_size = sp.min_iterative_cloud_percentage;
     res.used_min_iterative_plane_percentual_size = sp.min_iterative_plane_percentage;
     res.used_max_variance_threshold_for_horizontal = sp.horizontal_variance_threshold;
@@ -383,36 +412,42 @@ bool SegmentationServices::clusterize(pitt_msgs::ClusterSegmentation::Request& r
 
 bool SegmentationServices::clusterize(const float* xyz16, size_t n, pitt_msgs::ClusterSegmentation::Response& res) {
     const pitt_cluster_params cp = clusterParams();
-    res.cluster_objs.clear();
     status_ = PITT_OK;
+    size_t found = 0;
     if (n >= (size_t)(int64_t)cp.min_input_size) {
         const int mn = (int)std::round((double)n * cp.min_rate);
         const int mx = (int)std::round((double)n * cp.max_rate);
         pitt_cluster_list L;
         status_ = pitt_euclidean_clusters_aos(ctx_, xyz16, (int64_t)n, 16, cp.tolerance, mn, mx, &L);
         if (status_ == PITT_OK) {
-            res.cluster_objs.reserve((size_t)L.n_clusters);
+            found = (size_t)L.n_clusters;  // buffers of a response used again are refilled in place
+            if (res.cluster_objs.size() < found) res.cluster_objs.resize(found);
             for (int c = 0; c < L.n_clusters; ++c) {
                 const pitt_cluster& cl = L.clusters[c];
-                pitt_msgs::InliersCluster m;
-                m.inliers.assign(cl.indices, cl.indices + cl.size);
+                pitt_msgs::InliersCluster& m = res.cluster_objs[(size_t)c];
+                m.shape_id.clear();  // as a fresh message
+                copy_ints(cl.indices, cl.size, m.inliers);
                 m.cloud.data.resize((size_t)cl.size * 4);  // the members' points in index order (:85-95)
-                for (int64_t k = 0; k < cl.size; ++k) {
-                    const float* p = xyz16 + 4 * (size_t)cl.indices[k];
-                    float* d = m.cloud.data.data() + 4 * k;
-                    d[0] = p[0];
-                    d[1] = p[1];
-                    d[2] = p[2];
-                    d[3] = 1.0f;
-                }
+                float* dst = m.cloud.data.data();
+                const int32_t* idx = cl.indices;
+                host_parallel(cl.size, [=](int64_t k0, int64_t k1) {
+                    for (int64_t k = k0; k < k1; ++k) {
+                        const float* p = xyz16 + 4 * (size_t)idx[k];
+                        float* d = dst + 4 * k;
+                        d[0] = p[0];
+                        d[1] = p[1];
+                        d[2] = p[2];
+                        d[3] = 1.0f;
+                    }
+                });
                 const int cnt = (int)cl.size + 1;  // Q7: the counter starts at 1
                 m.x_centroid = cl.sum_xyz[0] / cnt;
                 m.y_centroid = cl.sum_xyz[1] / cnt;
                 m.z_centroid = cl.sum_xyz[2] / cnt;
-                res.cluster_objs.push_back(std::move(m));
             }
         }
     }
+    res.cluster_objs.resize(found);
     return true;
 }
 
@@ -707,9 +742,10 @@ int pitt_srv_find_supports(pitt_srv* s, const float* xyz16, int64_t n, int64_t n
     srv.request.horizontal_axis.assign(r->horizontal_axis, r->horizontal_axis + std::max(0, std::min(8, r->n_horizontal_axis)));
     srv.request.support_edge_remove_offset.assign(r->edge_remove_offset,
                                                   r->edge_remove_offset + std::max(0, std::min(8, r->n_edge_remove_offset)));
-    bool ok = s->svc.findSupports(xyz16, (size_t)n, (size_t)n_normals, srv.request, srv.response);
+    // the service object's response is refilled in place (its buffers are reused call after call; a
+    // failed call leaves it with no supports)
+    bool ok = s->svc.findSupports(xyz16, (size_t)n, (size_t)n_normals, srv.request, s->supports);
     if (s->svc.last_status() < 0) return s->svc.last_status();
-    s->supports = std::move(srv.response);
     *n_supports = (int32_t)s->supports.supports_description.size();
     if (used_out) {
         const auto& u = s->supports;
@@ -754,10 +790,9 @@ int pitt_srv_support_cloud(pitt_srv* s, int32_t k, int32_t which, float* out) {
 
 int pitt_srv_clusterize(pitt_srv* s, const float* xyz16, int64_t n, int32_t* n_clusters) {
     if (!s || (n > 0 && !xyz16) || n < 0 || !n_clusters) return PITT_E_INVALID;
-    pitt_msgs::ClusterSegmentation srv;  // the cloud stays in the caller's array
-    bool ok = s->svc.clusterize(xyz16, (size_t)n, srv.response);
+    // the cloud stays in the caller's array; the service object's response is refilled in place
+    bool ok = s->svc.clusterize(xyz16, (size_t)n, s->clusters);
     if (s->svc.last_status() < 0) return s->svc.last_status();
-    s->clusters = std::move(srv.response);
     *n_clusters = (int32_t)s->clusters.cluster_objs.size();
     return ok ? 1 : 0;
 }
