@@ -220,3 +220,28 @@ def test_cone_handler(srv):
     # normals of the wrong size: PCL clears the outputs; the height stays -1 (:132, :195)
     ok, inl, coef, centroid = srv.ransac_cone(P, N, n_normals=len(P) - 1)
     assert ok and len(inl) == 0 and list(coef) == [-1.0] and not centroid.any()
+
+
+def test_handlers_refill_their_responses_in_place(srv):
+    """The flat ABI keeps one response per service object and the handlers refill it in place (assign /
+    resize on the existing vectors): a scene after a larger or smaller one must leave nothing stale."""
+    scenes = [np.stack(pitt.synth_fused(s, v, 160, 120), 1) for s, v in ((51, 2), (52, 1), (51, 2), (53, 4))]
+    for xyz in scenes:
+        ok, sups, _ = srv.find_supports(xyz)
+        ref = orc.find_supports(*xyz.T)
+        assert ok and len(sups) == len(ref)
+        for s, r in zip(sups, ref):
+            assert np.array_equal(s["inliers"], r["idx_map"])
+            assert np.array_equal(s["coefficients"], r["coefficients"])
+            assert np.array_equal(s["on_support_cloud"], r["on_support_cloud"])
+            assert np.array_equal(s["support_cloud"], r["support_cloud"])
+        for r in ref:
+            on = np.ascontiguousarray(r["on_support_cloud"], np.float32)
+            if len(on) < 30:
+                continue
+            ok, cl = srv.clusterize(on)
+            exp = orc.euclidean_clusters(*on.T)
+            assert ok and [list(c["inliers"]) for c in cl] == [list(c["inliers"]) for c in exp]
+            for c, e in zip(cl, exp):
+                assert np.array_equal(c["centroid"], e["centroid"])
+                assert np.array_equal(c["cloud"], on[c["inliers"]])
