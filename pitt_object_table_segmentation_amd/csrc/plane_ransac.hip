@@ -279,6 +279,9 @@ constexpr int kScoreWaves = PITT_SCORE_WAVES;  // waves (items) per k_score bloc
 #ifndef PITT_SCORE_DEPTH
 #define PITT_SCORE_DEPTH 2  // register sets of points in flight in k_score (3: an A/B variant)
 #endif
+#ifndef PITT_LIST_PIPE
+#define PITT_LIST_PIPE 1  // software-pipelined 32-entry list walks (0: a pair's counts before the next pair)
+#endif
 #ifndef PITT_SCORE_MERGE
 #define PITT_SCORE_MERGE 1  // two 16-hypothesis rounds per pass, 32-entry survivor lists (0: one round per pass)
 #endif
@@ -548,6 +551,19 @@ __device__ __forceinline__ void score_list32(uint32_t lb, int c, float x, float 
     float d0, t0, d1, t1;
     uint64_t m0, m1;
     uint32_t n0, n1;
+#if PITT_LIST_PIPE
+    // the software-pipelined walk (gen_score_asm.py, _P): a pair's count chain under the next pair's dots
+    float e0, e1;
+#define PITT_LIST_OPERANDS                                                                              \
+    : [d0] "=&v"(d0), [t0] "=&v"(t0), [d1] "=&v"(d1), [t1] "=&v"(t1), [e0] "=&v"(e0), [e1] "=&v"(e1),  \
+      [m0] "=&s"(m0), [m1] "=&s"(m1), [n0] "=&s"(n0), [n1] "=&s"(n1), [vc] "+v"(vc), [vc2] "+v"(vc2)    \
+    : [base] "v"(base), [c] "s"(c), [x] "v"(x), [y] "v"(y), [z] "v"(z), [tv] "v"(tv), [L] "n"(16 * GR) \
+    : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69",  \
+      "v70", "v71", "scc", "memory"
+    if constexpr (ORDER == 0) asm volatile(PITT_SCORE_LIST32_ASM_P_0 PITT_LIST_OPERANDS);
+    else if constexpr (ORDER == 1) asm volatile(PITT_SCORE_LIST32_ASM_P_1 PITT_LIST_OPERANDS);
+    else asm volatile(PITT_SCORE_LIST32_ASM_P_2 PITT_LIST_OPERANDS);
+#else
 #define PITT_LIST_OPERANDS                                                                              \
     : [d0] "=&v"(d0), [t0] "=&v"(t0), [d1] "=&v"(d1), [t1] "=&v"(t1), [m0] "=&s"(m0), [m1] "=&s"(m1),  \
       [n0] "=&s"(n0), [n1] "=&s"(n1), [vc] "+v"(vc), [vc2] "+v"(vc2)                                    \
@@ -557,6 +573,7 @@ __device__ __forceinline__ void score_list32(uint32_t lb, int c, float x, float 
     if constexpr (ORDER == 0) asm volatile(PITT_SCORE_LIST32_ASM_0 PITT_LIST_OPERANDS);
     else if constexpr (ORDER == 1) asm volatile(PITT_SCORE_LIST32_ASM_1 PITT_LIST_OPERANDS);
     else asm volatile(PITT_SCORE_LIST32_ASM_2 PITT_LIST_OPERANDS);
+#endif
 #undef PITT_LIST_OPERANDS
 }
 

@@ -107,6 +107,98 @@ def path_from(order, first, regs, prefetched):
     return out
 
 
+# ---- software-pipelined walk: the count chain of one pair (v_cmp -> s_bcnt1 -> v_writelane, a
+# VALU -> SALU -> VALU round trip) runs interleaved with the next pair's dot products, so a wave does
+# not stall on it.  Registers: the pairs' results alternate between (d0, d1) and (e0, e1); t0, t1 are
+# the dots' scratch.  Same operations per entry as pair() / single(), so the counts are the same bits.
+def dots_pair(order, ra, rb, ra_out, rb_out):
+    a, b = dot(order, ra_out, "%[t0]", ra), dot(order, rb_out, "%[t1]", rb)
+    return [x for ab in zip(a, b) for x in ab]
+
+
+def chain_parts(x0, x1, k):
+    cmps = [f"v_cmp_lt_f32 %[m0], |{x0}|, %[tv]", f"v_cmp_lt_f32 %[m1], |{x1}|, %[tv]"]
+    rest = ["s_bcnt1_i32_b64 %[n0], %[m0]", "s_bcnt1_i32_b64 %[n1], %[m1]", wl("%[n0]", k), wl("%[n1]", k + 1)]
+    return cmps, rest
+
+
+def interleave(rest, dots):
+    """bcnt0 after 4 dot ops, bcnt1 after 6, writelane0 after 8, writelane1 after 10"""
+    out = []
+    marks = {4: rest[0], 6: rest[1], 8: rest[2], 10: rest[3]}
+    for i, ins in enumerate(dots):
+        if i in marks:
+            out.append(marks[i])
+        out.append(ins)
+    return out
+
+
+def path_from_pipe(order, first, regs, tag):
+    """As path_from, pipelined: pair (k, k+1)'s dots, then for every later pair its reads, the previous
+    pair's compares, the LDS wait, and its dots interleaved with the previous pair's counts.  An exit
+    after pair j jumps to .Lf<tag><j>, which finishes pair j's counts."""
+    out, tails = [], []
+    n = NMAX
+    k = first
+    ra, rb, rc, rd_ = regs
+    names = [("%[d0]", "%[d1]"), ("%[e0]", "%[e1]")]
+    cur = 0
+
+    def reads(k, rc, rd_):
+        r = []
+        if k + 2 < n:
+            r.append(rd(rc, 16 * (k + 2)))
+            if k + 3 < n:
+                r.append(rd(rd_, 16 * (k + 3)))
+                return r, "s_waitcnt lgkmcnt(2)"
+            return r, "s_waitcnt lgkmcnt(1)"
+        return r, "s_waitcnt lgkmcnt(0)"
+
+    if k + 1 >= n:  # a lone last entry: not reached by any list of a valid length
+        r, w = reads(k, rc, rd_)
+        return out + r + [w] + single(order, ra, k), tails
+    r, w = reads(k, rc, rd_)
+    out += r + [w] + dots_pair(order, ra, rb, *names[cur])
+    while True:
+        x0, x1 = names[cur]
+        cmps, rest = chain_parts(x0, x1, k)
+        if k + 2 >= n:
+            out += cmps + rest
+            break
+        lab = f".Lf{tag}{k}_%="
+        out += [f"s_cmp_le_u32 %[c], {k + 2}", f"s_cbranch_scc1 {lab}"]
+        tails += [f"{lab}:"] + cmps + rest + ["s_branch .Lwait%="]
+        k += 2
+        ra, rb, rc, rd_ = rc, rd_, ra, rb
+        r, w = reads(k, rc, rd_)
+        if k + 1 >= n:  # the last entry of a maximal odd-path list alone (never reached)
+            out += r + cmps + [w] + rest + single(order, ra, k)
+            break
+        nxt = 1 - cur
+        out += r + cmps + [w] + interleave(rest, dots_pair(order, ra, rb, *names[nxt]))
+        cur = nxt
+    return out, tails
+
+
+def block_pipe(order, nmax=16):
+    global NMAX
+    NMAX = nmax
+    out = []
+    out += ["s_bitcmp1_b32 %[c], 0", "s_cbranch_scc0 .Leven%="]
+    out += [rd(REGS[0], 0), rd(REGS[1], 16), rd(REGS[2], 32), "s_waitcnt lgkmcnt(2)"]
+    out += single(order, REGS[0], 0)
+    out += ["s_cmp_le_u32 %[c], 1", "s_cbranch_scc1 .Lwait%="]
+    odd, t1 = path_from_pipe(order, 1, [REGS[1], REGS[2], REGS[3], REGS[0]], "o")
+    out += odd
+    out += ["s_branch .Lwait%=", ".Leven%=:"]
+    out += [rd(REGS[0], 0), rd(REGS[1], 16)]
+    even, t2 = path_from_pipe(order, 0, REGS[:], "e")
+    out += even
+    out += ["s_branch .Lwait%="] + t1 + t2
+    out += [".Lwait%=:", "s_waitcnt lgkmcnt(0)"]
+    return out
+
+
 def main():
     lines = ["// GENERATED by tools/gen_score_asm.py -- do not edit by hand.",
              "// k_score's survivor-list loop for one group, per PCL reduction order (A3); see the generator's",
@@ -114,11 +206,15 @@ def main():
              "// 1..16 entries), x, y, z, tv (VGPRs), vc (VGPR, in/out), L (immediate lane base 16 g);",
              "// d0, t0, d1, t1 (VGPR scratch), m0, m1 (SGPR pairs), n0, n1 (SGPRs).  Clobbers v56-v71.",
              "#pragma once", ""]
-    for nmax, name in ((16, "PITT_SCORE_LIST_ASM"), (32, "PITT_SCORE_LIST32_ASM")):
-        if nmax == 32:
+    for nmax, name, gen in ((16, "PITT_SCORE_LIST_ASM", block), (32, "PITT_SCORE_LIST32_ASM", block),
+                            (16, "PITT_SCORE_LIST_ASM_P", block_pipe), (32, "PITT_SCORE_LIST32_ASM_P", block_pipe)):
+        if nmax == 32 and gen is block:
             lines.append("// 32-entry lists (two rounds of hypotheses in one pass): entries 16.. write lane L + k - 16 of vc2.")
+        if name.endswith("_P") and nmax == 16:
+            lines.append("// _P: the same walks software-pipelined (a pair's count chain under the next pair's dots;")
+            lines.append("// e0, e1 VGPR scratch as well).")
         for order in range(3):
-            body = block(order, nmax)
+            body = gen(order, nmax)
             lines.append(f"#define {name}_{order} \\")
             for i, ins in enumerate(body):
                 end = " \\" if i + 1 < len(body) else ""
