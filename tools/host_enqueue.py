@@ -8,7 +8,6 @@ import time
 
 import numpy as np
 
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 os.environ["GPU_MAX_HW_QUEUES"] = "8"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
