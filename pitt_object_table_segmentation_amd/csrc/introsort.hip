@@ -40,9 +40,10 @@ struct ISmall {
 
 constexpr int kIsThreshold = 16;  // _S_threshold
 #ifndef PITT_IS_SMALL
-#define PITT_IS_SMALL 2048
+#define PITT_IS_SMALL 8192
 #endif
-constexpr int kIsSmall = PITT_IS_SMALL;  // segments this short finish in one wave, in LDS
+constexpr int kIsSmall = PITT_IS_SMALL;  // segments this short finish in one block, in LDS
+static_assert(kIsSmall % 256 == 0 && kIsSmall <= 65536, "block segments: whole 256-element windows, 16-bit positions");
 #ifndef PITT_IS_COOP_MAX
 #define PITT_IS_COOP_MAX 64
 #endif    // segments this short finish in one wave, in LDS
@@ -55,7 +56,7 @@ __device__ __forceinline__ void is_swap(uint32_t* key, uint32_t* val, int a, int
     val[b] = va;
 }
 
-// children of <= 16 are final; children of <= kIsSmall go to the one-wave list, larger ones to the next level
+// children of <= 16 are final; children of <= kIsSmall go to the one-block list, larger ones to the next level
 __device__ __forceinline__ int is_child(int f, int l, int d, ISeg* next, int32_t* next_cnt, ISmall* small,
                                         int32_t* small_cnt) {
     if (l - f <= kIsThreshold) return -1;
@@ -79,21 +80,16 @@ __device__ __forceinline__ int is_load_count(const int32_t* p) {
 constexpr int kIsLvT = 1024;  // threads per block of the level kernel
 constexpr int kIsLvW = kIsLvT / 64;
 
-// Exclusive scan of two flags over a kIsLvT-thread block; ta / tb = the block totals.
+// Exclusive scan of two 0/1 flags over a kIsLvT-thread block; ta / tb = the block totals.  Inside a wave
+// the ranks are ballot bit counts (no shuffle chain).
 __device__ __forceinline__ void is_block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* sh) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int ia = a, ib = b;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int xa = __shfl_up(ia, off, 64), xb = __shfl_up(ib, off, 64);
-        if (lane >= off) {
-            ia += xa;
-            ib += xb;
-        }
-    }
-    if (lane == 63) {
-        sh[w] = ia;
-        sh[kIsLvW + w] = ib;
+    const uint64_t ma = __ballot(a), mb = __ballot(b);
+    const int ia = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+    const int ib = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+    if (lane == 0) {
+        sh[w] = __popcll(ma);
+        sh[kIsLvW + w] = __popcll(mb);
     }
     __syncthreads();
     int oa = 0, ob = 0;
@@ -107,8 +103,8 @@ __device__ __forceinline__ void is_block_scan2(int a, int b, int& ea, int& eb, i
         tb += sb;
     }
     __syncthreads();
-    ea = oa + ia - a;
-    eb = ob + ib - b;
+    ea = oa + ia;
+    eb = ob + ib;
 }
 
 // Grid barrier over a monotonically rising arrival counter (zeroed before the launch): barrier j
@@ -153,6 +149,9 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
     const int64_t c0 = min(n, (int64_t)b * chunk), c1 = min(n, c0 + chunk);
     ISeg* cur = segA;
     ISeg* nxt = segB;
+#ifdef PITT_IS_WATCHDOG
+    long long tb[5], ta[5], t_lv = clock64();
+#endif
     for (int v = 0; v < levels; ++v) {
         const int nseg = is_load_count(cnt + 2 + v);  // the same value in every block (after a barrier)
         if (nseg == 0) break;
@@ -184,7 +183,13 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             }
             cur[s] = g;
         }
+#ifdef PITT_IS_WATCHDOG
+        tb[0] = clock64();
+#endif
         is_grid_sync(bar, target);
+#ifdef PITT_IS_WATCHDOG
+        ta[0] = clock64();
+#endif
         // 2 flags and block-local ranks
         int carL = 0, carR = 0;
         for (int64_t base = c0; base < c1; base += kIsLvT) {
@@ -215,14 +220,28 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             bsum[b] = carL;
             bsum[G + b] = carR;
         }
+#ifdef PITT_IS_WATCHDOG
+        tb[1] = clock64();
+#endif
         is_grid_sync(bar, target);
+#ifdef PITT_IS_WATCHDOG
+        ta[1] = clock64();
+#endif
         // 4 stop positions; stop counts.  Global ranks = block-local rank + the prefix of the block
         // totals (every block forms the prefix itself: no separate pass)
-        for (int j = tid; j <= G; j += kIsLvT) {
-            int a = 0, r = 0;
-            for (int q = 0; q < j; ++q) a += bsum[q], r += bsum[G + q];
-            preL[j] = a;
-            preR[j] = r;
+        for (int j = tid; j < G; j += kIsLvT) {  // the block totals into LDS, then each prefix from LDS
+            preL[j + 1] = bsum[j];
+            preR[j + 1] = bsum[G + j];
+        }
+        __syncthreads();
+        int pa = 0, pr2 = 0;
+        if (tid <= G) {
+            for (int q = 1; q <= tid; ++q) pa += preL[q], pr2 += preR[q];
+        }
+        __syncthreads();
+        if (tid <= G) {
+            preL[tid] = pa;
+            preR[tid] = pr2;
         }
         __syncthreads();
         auto gl = [&](int64_t i) { return i >= n ? preL[G] : SL[i] + preL[i / chunk]; };
@@ -241,20 +260,43 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             if (fb & 1) posL[bb + (gl(i) - gl(bb))] = (int32_t)i;
             if (fb & 2) posR[bb + (gr(g.l) - gr(i + 1))] = (int32_t)i;
         }
+#ifdef PITT_IS_WATCHDOG
+        tb[2] = clock64();
+#endif
         is_grid_sync(bar, target);
-        // 5 K by bisection
-        for (int64_t s = gt; s < nseg; s += gstride) {
-            if (!cur[s].active) continue;
-            const int bb = cur[s].f + 1;
-            int lo = 0, hi = min(cur[s].nL, cur[s].nR);
+#ifdef PITT_IS_WATCHDOG
+        ta[2] = clock64();
+#endif
+        // 5 K: one wave per segment, a 64-way search (posL[k] < posR[k] holds on a prefix of k; every k
+        // below lo holds it, and K <= hi)
+        for (int64_t s = gt >> 6; s < nseg; s += gstride >> 6) {
+            const ISeg g = cur[s];
+            if (!g.active) continue;
+            const int bb = g.f + 1;
+            int lo = 0, hi = min(g.nL, g.nR);
             while (lo < hi) {
-                const int mid = lo + ((hi - lo) >> 1);
-                if (posL[bb + mid] < posR[bb + mid]) lo = mid + 1;
-                else hi = mid;
+                const int step = (hi - lo + 63) >> 6;
+                const int k = lo + step * (tid & 63);
+                const bool fail = k < hi && !(posL[bb + k] < posR[bb + k]);
+                const uint64_t fm = __ballot(fail);
+                if (fm == 0) {  // every probe below hi held: so does every k up to the last one
+                    const int np = (hi - lo + step - 1) / step;
+                    lo = lo + (np - 1) * step + 1;
+                } else {
+                    const int f0 = __builtin_ctzll(fm);
+                    hi = lo + step * f0;              // a failing k
+                    if (f0 > 0) lo = lo + step * (f0 - 1) + 1;  // the probe before it held
+                }
             }
-            cur[s].K = lo;
+            if ((tid & 63) == 0) cur[s].K = lo;
         }
+#ifdef PITT_IS_WATCHDOG
+        tb[3] = clock64();
+#endif
         is_grid_sync(bar, target);
+#ifdef PITT_IS_WATCHDOG
+        ta[3] = clock64();
+#endif
         // 6 swaps; cut and children
         for (int64_t j = gt; j < n; j += gstride) {
             const int s = segid[j];
@@ -275,7 +317,20 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             cur[s].childL = is_child(g.f, cut, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
             cur[s].childR = is_child(cut, g.l, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
         }
+#ifdef PITT_IS_WATCHDOG
+        tb[4] = clock64();
+#endif
         is_grid_sync(bar, target);
+#ifdef PITT_IS_WATCHDOG
+        ta[4] = clock64();
+#endif
+#ifdef PITT_IS_WATCHDOG
+        if (b == 0 && tid == 0)
+            printf("is_levels v %d nseg %d phases %lld %lld %lld %lld %lld barriers %lld %lld %lld %lld %lld\n", v, nseg,
+                   tb[0] - t_lv, tb[1] - ta[0], tb[2] - ta[1], tb[3] - ta[2], tb[4] - ta[3], ta[0] - tb[0], ta[1] - tb[1],
+                   ta[2] - tb[2], ta[3] - tb[3], ta[4] - tb[4]);
+        t_lv = ta[4];
+#endif
         ISeg* t = cur;  // phase 7 runs at the top of the next level, over nxt (= this level's segments)
         cur = nxt;
         nxt = t;
@@ -343,8 +398,12 @@ __device__ void is_heap_sort(uint32_t* k, uint32_t* v, int len) {
 constexpr int kHeapLds = 26624;  // 6 B x 26624 = 156 KB of LDS
 
 // Orders one wave's LDS accesses across lanes: LDS executes a wave's accesses in issue order, so a
-// compiler barrier (no reordering of the accesses around it) is enough.
-__device__ __forceinline__ void is_lds_fence() { asm volatile("" ::: "memory"); }
+// compiler barrier (no reordering of the accesses around it) is enough; the wave barrier (convergent)
+// keeps every lane of the wave at this point together, so no lane runs ahead into the next step.
+__device__ __forceinline__ void is_lds_fence() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
 
 template <typename V>
 __device__ void is_sift_lds(uint32_t* sk, V* si, int hole, int len, uint32_t vk, V vi) {
@@ -485,102 +544,255 @@ __global__ __launch_bounds__(256) void k_is_heap(const ISeg* __restrict__ segs, 
     }
 }
 
-// One wave finishes a segment of <= kIsSmall elements in LDS: the same median / unguarded-partition /
-// depth / heapsort steps as the level kernels, run one partition at a time with an explicit stack
-// (right part pushed, left part continued, as __introsort_loop recurses).  Stops are ranked with
-// ballots: left stops forward from first + 1, right stops backward from last - 1.
-__global__ __launch_bounds__(64) void k_is_small(const ISmall* __restrict__ segs, const int32_t* __restrict__ small_cnt,
-                                                 uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
-    __shared__ uint32_t sk[kIsSmall], sv[kIsSmall];
-    __shared__ int32_t pl[kIsSmall], pr[kIsSmall];
-    __shared__ int32_t stk[3 * 72];
+// One block finishes a segment of <= kIsSmall elements in LDS, kIsSmallW waves working on disjoint
+// sub-segments at once: the same median / unguarded-partition / depth / heapsort steps as the level
+// kernels, one partition per wave at a time.  A wave takes a segment from the block's queue, partitions
+// it, queues the right part and goes on with the left one, as __introsort_loop recurses; the segments
+// in flight are disjoint, so each wave's stores touch only its own range (and its own range of pl /
+// pr).  Queue: slot j of a circular list holds the j-th queued segment once ready[j % cap] == j + 1;
+// `open` counts the segments queued and not yet finished (head, tail and open count in units of 64,
+// see is_wave_inc), so a wave whose slot stays empty while open is 0 is done (a queued segment stays
+// open until the wave that took its slot finishes it).
+constexpr int kIsSmallW = 8;  // waves per block
+// segments in flight are disjoint and longer than 16: fewer than kIsSmall / 17 + kIsSmallW at once
+constexpr int kIsQCap = kIsSmall / (kIsThreshold + 1) + kIsSmallW < 256 ? 256 : kIsSmall / (kIsThreshold + 1) + kIsSmallW < 512 ? 512 : 1024;
+static_assert(kIsSmall / (kIsThreshold + 1) + kIsSmallW < kIsQCap, "introsort queue too short");
+
+struct IsQueue {
+    int head, tail, open;
+    int ready[kIsQCap];
+    int f[kIsQCap], l[kIsQCap], depth[kIsQCap];
+};
+
+__device__ __forceinline__ int is_lds_add(int* p, int v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The queue counters count in units of 64: every lane of the wave adds 1 (wave-uniform control flow
+// and a uniform operand, which the compiler folds into one ds_add of 64; a lane-0-only add either
+// needs a lane-conditional branch, around which the compiler may let some lanes run ahead of the
+// readfirstlane broadcasts, or a per-lane operand, which it serialises over the 64 lanes).  Returns
+// the old count, broadcast, in queue entries.
+__device__ __forceinline__ int is_wave_inc(int* p) {
+    return __builtin_amdgcn_readfirstlane(is_lds_add(p, 1)) >> 6;
+}
+
+__device__ __forceinline__ int is_wave_load(int* p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+// queues [f, l) at depth d (open first: the pushing wave's own segment keeps open above 0); every lane
+// stores the same values
+__device__ __forceinline__ void is_queue_push(IsQueue& Q, int f, int l, int d) {
+    is_lds_add(&Q.open, 1);
+    const int j = is_wave_inc(&Q.tail);
+    const int s = j & (kIsQCap - 1);
+    Q.f[s] = f;
+    Q.l[s] = l;
+    Q.depth[s] = d;
+    __hip_atomic_store(&Q.ready[s], j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Partition [f, l) (> 16 elements, depth left) in place by one wave; returns the cut.  One forward
+// pass over 16-byte aligned 256-element windows (lane: four consecutive keys, one ds_read_b128) ranks
+// both kinds of stops: left stops (key >= p) ascending into pl, right stops (key <= p) ascending into pr,
+// so the k-th right stop from the end is pr[nR - 1 - k].  Positions are 16-bit (kIsSmall <= 65536).
+__device__ __forceinline__ int is_partition_wave(uint32_t* sk, uint32_t* sv, uint16_t* pl, uint16_t* pr, int f, int l,
+                                                 int lane) {
+    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const uint32_t ka = sk[a], kb = sk[b], kc = sk[c];
+    int m;
+    if (ka < kb) m = (kb < kc) ? b : (ka < kc) ? c : a;
+    else m = (ka < kc) ? a : (kb < kc) ? c : b;
+    {  // every lane swaps (the same values): no lane-conditional branch
+        const uint32_t tk = sk[f], tv = sv[f], mk = sk[m], mv = sv[m];
+        is_lds_fence();
+        sk[f] = mk;
+        sv[f] = mv;
+        sk[m] = tk;
+        sv[m] = tv;
+    }
+    is_lds_fence();
+    const uint32_t p = sk[f];
+    uint16_t* L = pl + f;
+    uint16_t* Rs = pr + f;
+    int nL = 0, nR = 0;
+    for (int w = (f + 1) & ~3; w < l; w += 256) {
+        const int g0 = w + 4 * lane;
+        uint4 q = make_uint4(0u, 0u, 0u, 0u);
+        if (g0 < l) q = *reinterpret_cast<const uint4*>(sk + g0);
+        const uint32_t kk[4] = {q.x, q.y, q.z, q.w};
+        bool fl[4], fr[4];
+        uint64_t BL[4], BR[4];
+        int below_l = 0, below_r = 0, tot_l = 0, tot_r = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = g0 + j;
+            const bool in = i > f && i < l;
+            fl[j] = in && !(kk[j] < p);
+            fr[j] = in && !(p < kk[j]);
+            BL[j] = __ballot(fl[j]);
+            BR[j] = __ballot(fr[j]);
+            below_l += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(BL[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)BL[j], 0u));
+            below_r += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(BR[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)BR[j], 0u));
+            tot_l += __popcll(BL[j]);
+            tot_r += __popcll(BR[j]);
+        }
+        int rl = nL + below_l, rr = nR + below_r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (fl[j]) L[rl] = (uint16_t)(g0 + j);
+            if (fr[j]) Rs[rr] = (uint16_t)(g0 + j);
+            rl += fl[j];
+            rr += fr[j];
+        }
+        nL += tot_l;
+        nR += tot_r;
+    }
+    is_lds_fence();
+    const int kmax = min(nL, nR);
+    int K = kmax;  // the swaps run while the k-th left stop lies left of the k-th right stop (from the end)
+    for (int k0 = 0; k0 < kmax; k0 += 64) {
+        const int k = k0 + lane;
+        const uint64_t bal = __ballot(k < kmax && !((int)L[k] < (int)Rs[nR - 1 - k]));
+        if (bal) {
+            K = k0 + __builtin_ctzll(bal);
+            break;
+        }
+    }
+    for (int k = lane; k < K; k += 64) {
+        const int x = L[k], y = Rs[nR - 1 - k];
+        const uint32_t tk = sk[x], tv = sv[x];
+        sk[x] = sk[y];
+        sv[x] = sv[y];
+        sk[y] = tk;
+        sv[y] = tv;
+    }
+    const int cut = K < nL ? (K > 0 ? min((int)L[K], (int)Rs[nR - K]) : (int)L[K]) : (int)Rs[nR - K];
+    is_lds_fence();
+    return __builtin_amdgcn_readfirstlane(cut);
+}
+
+__global__ __launch_bounds__(64 * kIsSmallW) void k_is_small(const ISmall* __restrict__ segs,
+                                                              const int32_t* __restrict__ small_cnt,
+                                                              uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+    __shared__ __attribute__((aligned(16))) uint32_t sk[kIsSmall];
+    __shared__ uint32_t sv[kIsSmall];
+    __shared__ uint16_t pl[kIsSmall], pr[kIsSmall];
+    __shared__ IsQueue Q;
     if ((int)blockIdx.x >= *small_cnt) return;
     const ISmall g = segs[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int len = g.l - g.f;
-    for (int i = lane; i < len; i += 64) {
+    for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
         sk[i] = key[g.f + i];
         sv[i] = val[g.f + i];
     }
+    for (int i = threadIdx.x; i < kIsQCap; i += 64 * kIsSmallW) Q.ready[i] = 0;
+    if (threadIdx.x == 0) {
+        Q.head = Q.tail = Q.open = 0;
+    }
     __syncthreads();
-    int sp = 0, f = 0, l = len, depth = g.depth;
+    if (threadIdx.x == 0) {  // the whole segment is the first queued one (counts in units of 64)
+        Q.open = 64;
+        Q.tail = 64;
+        Q.f[0] = 0;
+        Q.l[0] = len;
+        Q.depth[0] = g.depth;
+        Q.ready[0] = 1;
+    }
+    __syncthreads();
+#ifdef PITT_IS_WATCHDOG
+    __shared__ unsigned long long dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait;
+    if (threadIdx.x == 0) dbg_busy = dbg_max = dbg_parts = dbg_elems = dbg_spins = dbg_wait = 0;
+    __syncthreads();
+    const long long t_start = clock64();
+    unsigned long long w_busy = 0, w_parts = 0, w_elems = 0, w_spins = 0, w_wait = 0;
+#endif
     for (;;) {
+#ifdef PITT_IS_WATCHDOG
+        const long long tw = clock64();
+#endif
+        const int j = is_wave_inc(&Q.head);
+        const int s = j & (kIsQCap - 1);
+        bool got = false;
+#ifdef PITT_IS_WATCHDOG
+        unsigned spins = 0;
+#endif
+        for (;;) {
+            if (is_wave_load(&Q.ready[s]) == j + 1) {
+                got = true;
+                break;
+            }
+            // open == 0: every queued segment is finished, and slot j was never filled (its segment would
+            // stay open until this wave finished it)
+            if (is_wave_load(&Q.open) == 0) break;
+            // no s_sleep: a sleeping wave wakes far too late for the next queued segment (the tree's
+            // partitions are short), and a polling wave issues one LDS read per round trip
+#ifdef PITT_IS_WATCHDOG
+            ++w_spins;
+            if (++spins == (1u << 20)) {
+                if (lane == 0)
+                    printf("is_small watchdog: block %d wave %d slot %d head %d tail %d open %d len %d\n",
+                           (int)blockIdx.x, (int)(threadIdx.x >> 6), j, Q.head, Q.tail, Q.open, len);
+                break;
+            }
+#endif
+        }
+#ifdef PITT_IS_WATCHDOG
+        w_wait += clock64() - tw;
+#endif
+        if (!got) break;
+        int f = __builtin_amdgcn_readfirstlane(Q.f[s]);
+        int l = __builtin_amdgcn_readfirstlane(Q.l[s]);
+        int depth = __builtin_amdgcn_readfirstlane(Q.depth[s]);
+#ifdef PITT_IS_WATCHDOG
+        int iters = 0;
+#endif
         while (l - f > kIsThreshold) {
+#ifdef PITT_IS_WATCHDOG
+            if (++iters > 4096) {
+                if (lane == 0) printf("is_small spine watchdog: block %d f %d l %d depth %d\n", (int)blockIdx.x, f, l, depth);
+                break;
+            }
+#endif
             if (depth == 0) {
-                __syncthreads();
                 is_make_heap_lds<64>(sk + f, sv + f, l - f, lane);
                 is_sort_heap_wave(sk + f, sv + f, l - f, lane);
-                __syncthreads();
                 break;
             }
             --depth;
-            const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
-            const uint32_t ka = sk[a], kb = sk[b], kc = sk[c];
-            int m;
-            if (ka < kb) m = (kb < kc) ? b : (ka < kc) ? c : a;
-            else m = (ka < kc) ? a : (kb < kc) ? c : b;
-            __syncthreads();
-            if (lane == 0) {
-                const uint32_t tk = sk[f], tv = sv[f];
-                sk[f] = sk[m];
-                sv[f] = sv[m];
-                sk[m] = tk;
-                sv[m] = tv;
-            }
-            __syncthreads();
-            const uint32_t p = sk[f];
-            int nL = 0, nR = 0;
-            for (int base = f + 1; base < l; base += 64) {
-                const int i = base + lane;
-                const bool st = i < l && !(sk[i] < p);
-                const uint64_t bal = __ballot(st);
-                if (st) pl[nL + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = i;
-                nL += __popcll(bal);
-            }
-            for (int base = l - 1; base > f; base -= 64) {
-                const int i = base - lane;
-                const bool st = i > f && !(p < sk[i]);
-                const uint64_t bal = __ballot(st);
-                if (st) pr[nR + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = i;
-                nR += __popcll(bal);
-            }
-            __syncthreads();
-            const int kmax = min(nL, nR);
-            int K = kmax;  // the swaps run while the k-th left stop lies left of the k-th right stop
-            for (int k0 = 0; k0 < kmax; k0 += 64) {
-                const int k = k0 + lane;
-                const uint64_t bal = __ballot(k < kmax && !(pl[k] < pr[k]));
-                if (bal) {
-                    K = k0 + __builtin_ctzll(bal);
-                    break;
-                }
-            }
-            for (int k = lane; k < K; k += 64) {
-                const int x = pl[k], y = pr[k];
-                const uint32_t tk = sk[x], tv = sv[x];
-                sk[x] = sk[y];
-                sv[x] = sv[y];
-                sk[y] = tk;
-                sv[y] = tv;
-            }
-            const int cut = K < nL ? (K > 0 ? min(pl[K], pr[K - 1]) : pl[K]) : pr[K - 1];
-            __syncthreads();
-            if (l - cut > kIsThreshold) {  // __introsort_loop(cut, last, depth)
-                stk[3 * sp] = cut;
-                stk[3 * sp + 1] = l;
-                stk[3 * sp + 2] = depth;
-                ++sp;
-            }
+#ifdef PITT_IS_WATCHDOG
+            const long long t0 = clock64();
+            const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
+            w_busy += clock64() - t0;
+            ++w_parts;
+            w_elems += l - f;
+#else
+            const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
+#endif
+            if (l - cut > kIsThreshold) is_queue_push(Q, cut, l, depth);  // __introsort_loop(cut, last, depth)
             l = cut;
         }
-        if (sp == 0) break;
-        --sp;
-        f = stk[3 * sp];
-        l = stk[3 * sp + 1];
-        depth = stk[3 * sp + 2];
+        is_lds_fence();
+        __hip_atomic_fetch_add(&Q.open, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // -64: finished
+    }
+#ifdef PITT_IS_WATCHDOG
+    if (lane == 0) {
+        atomicAdd(&dbg_busy, w_busy);
+        atomicMax(&dbg_max, w_busy);
+        atomicAdd(&dbg_parts, w_parts);
+        atomicAdd(&dbg_elems, w_elems);
+        atomicAdd(&dbg_spins, w_spins);
+        atomicAdd(&dbg_wait, w_wait);
     }
     __syncthreads();
-    for (int i = lane; i < len; i += 64) {
+    if (threadIdx.x == 0 && blockIdx.x < 12)
+        printf("is_small block %d len %d cycles %lld busy %llu maxwave %llu parts %llu elems %llu spins %llu wait %llu\n",
+               (int)blockIdx.x, len, clock64() - t_start, dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait);
+#endif
+    __syncthreads();
+    for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
         key[g.f + i] = sk[i];
         val[g.f + i] = sv[i];
     }
@@ -655,7 +867,7 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     }
     PITT_HIP_TRY(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, s));
     PITT_HIP_TRY(hipStreamSynchronize(s));  // the host memcpys above read stack values: complete them too
-    if (hcnt[1] > 0) hipLaunchKernelGGL(k_is_small, dim3(hcnt[1]), dim3(64), 0, s, small, cnt + 1, key, val);
+    if (hcnt[1] > 0) hipLaunchKernelGGL(k_is_small, dim3(hcnt[1]), dim3(64 * kIsSmallW), 0, s, small, cnt + 1, key, val);
     if (hcnt[0] > 0)
         hipLaunchKernelGGL(k_is_heap, dim3(hcnt[0]), dim3(256), kHeapLds * 6, s, heapsegs, cnt, key, val, vtmp);
     PITT_HIP_TRY(hipGetLastError());
