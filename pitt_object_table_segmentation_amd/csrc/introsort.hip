@@ -44,6 +44,11 @@ constexpr int kIsThreshold = 16;  // _S_threshold
 #endif
 constexpr int kIsSmall = PITT_IS_SMALL;  // segments this short finish in one block, in LDS
 static_assert(kIsSmall % 256 == 0 && kIsSmall <= 65536, "block segments: whole 256-element windows, 16-bit positions");
+#ifndef PITT_IS_MEDIUM
+#define PITT_IS_MEDIUM 65536
+#endif
+constexpr int kIsMedium = PITT_IS_MEDIUM;  // segments this short are partitioned by one block (global memory)
+static_assert(kIsMedium >= kIsSmall, "medium segments are longer than the block-in-LDS ones");
 #ifndef PITT_IS_COOP_MAX
 #define PITT_IS_COOP_MAX 64
 #endif    // segments this short finish in one wave, in LDS
@@ -56,12 +61,17 @@ __device__ __forceinline__ void is_swap(uint32_t* key, uint32_t* val, int a, int
     val[b] = va;
 }
 
-// children of <= 16 are final; children of <= kIsSmall go to the one-block list, larger ones to the next level
+// children of <= 16 are final; children of <= kIsSmall go to the one-block (LDS) list, of <= kIsMedium to
+// the one-block (global memory) list, larger ones to the next level
 __device__ __forceinline__ int is_child(int f, int l, int d, ISeg* next, int32_t* next_cnt, ISmall* small,
-                                        int32_t* small_cnt) {
+                                        int32_t* small_cnt, ISmall* med, int32_t* med_cnt) {
     if (l - f <= kIsThreshold) return -1;
     if (l - f <= kIsSmall) {
         small[atomicAdd(small_cnt, 1)] = ISmall{f, l, d, 0};
+        return -1;
+    }
+    if (l - f <= kIsMedium) {
+        med[atomicAdd(med_cnt, 1)] = ISmall{f, l, d, 0};
         return -1;
     }
     const int id = atomicAdd(next_cnt, 1);
@@ -78,6 +88,13 @@ __device__ __forceinline__ int is_load_count(const int32_t* p) {
 }
 
 constexpr int kIsLvT = 1024;  // threads per block of the level kernel
+// cnt[0] heap segments, cnt[1] block (LDS) segments, cnt[2 + v] level v's segments, cnt[kIsMaxLevels + 2]
+// the grid barrier's arrival counter, cnt[kIsMedCnt] block (global memory) segments
+constexpr int kIsMaxLevels = 128;
+constexpr int kIsMedCnt = kIsMaxLevels + 3;
+#ifdef PITT_IS_WATCHDOG
+__device__ long long g_is_lvdbg[64 * 11];
+#endif
 constexpr int kIsLvW = kIsLvT / 64;
 
 // Exclusive scan of two 0/1 flags over a kIsLvT-thread block; ta / tb = the block totals.  Inside a wave
@@ -135,6 +152,7 @@ __device__ __forceinline__ void is_grid_sync(uint32_t* bar, uint32_t& target) {
 //             block has read the next level's segment count.
 __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, ISeg* __restrict__ segB,
                                                    ISeg* __restrict__ heap, ISmall* __restrict__ small,
+                                                   ISmall* __restrict__ med,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ segid,
                                                    uint8_t* __restrict__ F, int32_t* __restrict__ SL,
                                                    int32_t* __restrict__ SR, int32_t* __restrict__ posL,
@@ -151,6 +169,7 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
     ISeg* nxt = segB;
 #ifdef PITT_IS_WATCHDOG
     long long tb[5], ta[5], t_lv = clock64();
+    int nlv = 0;
 #endif
     for (int v = 0; v < levels; ++v) {
         const int nseg = is_load_count(cnt + 2 + v);  // the same value in every block (after a barrier)
@@ -314,8 +333,8 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
             if (K < g.nL) cut = K > 0 ? min(posL[bb + K], posR[bb + K - 1]) : posL[bb + K];
             else cut = posR[bb + K - 1];
             cur[s].cut = cut;  // the swap loop above reads the other fields of cur[s]
-            cur[s].childL = is_child(g.f, cut, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
-            cur[s].childR = is_child(cut, g.l, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1);
+            cur[s].childL = is_child(g.f, cut, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1, med, cnt + kIsMedCnt);
+            cur[s].childR = is_child(cut, g.l, g.depth - 1, nxt, cnt + 3 + v, small, cnt + 1, med, cnt + kIsMedCnt);
         }
 #ifdef PITT_IS_WATCHDOG
         tb[4] = clock64();
@@ -325,16 +344,28 @@ __global__ __launch_bounds__(kIsLvT) void k_is_levels(ISeg* __restrict__ segA, I
         ta[4] = clock64();
 #endif
 #ifdef PITT_IS_WATCHDOG
-        if (b == 0 && tid == 0)
-            printf("is_levels v %d nseg %d phases %lld %lld %lld %lld %lld barriers %lld %lld %lld %lld %lld\n", v, nseg,
-                   tb[0] - t_lv, tb[1] - ta[0], tb[2] - ta[1], tb[3] - ta[2], tb[4] - ta[3], ta[0] - tb[0], ta[1] - tb[1],
-                   ta[2] - tb[2], ta[3] - tb[3], ta[4] - tb[4]);
+        if (b == 0 && tid == 0 && v < 64) {  // printed after the last level (a printf here would stall the grid)
+            long long* d = g_is_lvdbg + v * 11;
+            d[0] = nseg;
+            d[1] = tb[0] - t_lv;
+            for (int q = 1; q < 5; ++q) d[1 + q] = tb[q] - ta[q - 1];
+            for (int q = 0; q < 5; ++q) d[6 + q] = ta[q] - tb[q];
+            nlv = v + 1;
+        }
         t_lv = ta[4];
 #endif
         ISeg* t = cur;  // phase 7 runs at the top of the next level, over nxt (= this level's segments)
         cur = nxt;
         nxt = t;
     }
+#ifdef PITT_IS_WATCHDOG
+    if (b == 0 && tid == 0)
+        for (int v = 0; v < nlv; ++v) {
+            const long long* d = g_is_lvdbg + v * 11;
+            printf("is_levels v %d nseg %lld phases %lld %lld %lld %lld %lld barriers %lld %lld %lld %lld %lld\n", v, d[0], d[1],
+                   d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10]);
+        }
+#endif
 }
 
 // ---- std::__partial_sort(first, last, last): __make_heap + __sort_heap (libstdc++ stl_heap.h) -------
@@ -520,27 +551,31 @@ __global__ __launch_bounds__(256) void k_is_heap(const ISeg* __restrict__ segs, 
                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ val,
                                                  uint32_t* __restrict__ vtmp) {
     extern __shared__ uint32_t is_smem[];
-    if ((int)blockIdx.x >= *heap_cnt) return;
-    const ISeg g = segs[blockIdx.x];
-    const int len = g.l - g.f, tid = threadIdx.x;
-    if (len > kHeapLds) {
-        if (tid == 0) is_heap_sort(key + g.f, val + g.f, len);
-        return;
-    }
-    uint32_t* sk = is_smem;
-    uint16_t* si = reinterpret_cast<uint16_t*>(is_smem + len);
-    for (int i = tid; i < len; i += 256) {
-        sk[i] = key[g.f + i];
-        si[i] = (uint16_t)i;
-        vtmp[g.f + i] = val[g.f + i];
-    }
-    __syncthreads();
-    is_make_heap_lds<256>(sk, si, len, tid);
-    if (tid < 64) is_sort_heap_wave(sk, si, len, tid);
-    __syncthreads();
-    for (int i = tid; i < len; i += 256) {
-        key[g.f + i] = sk[i];
-        val[g.f + i] = vtmp[g.f + si[i]];
+    const int nh = *heap_cnt;  // the count on the device: no host round trip before the launch
+    for (int hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+        const ISeg g = segs[hi];
+        const int len = g.l - g.f, tid = threadIdx.x;
+        if (len > kHeapLds) {
+            if (tid == 0) is_heap_sort(key + g.f, val + g.f, len);
+            __syncthreads();
+            continue;
+        }
+        uint32_t* sk = is_smem;
+        uint16_t* si = reinterpret_cast<uint16_t*>(is_smem + len);
+        for (int i = tid; i < len; i += 256) {
+            sk[i] = key[g.f + i];
+            si[i] = (uint16_t)i;
+            vtmp[g.f + i] = val[g.f + i];
+        }
+        __syncthreads();
+        is_make_heap_lds<256>(sk, si, len, tid);
+        if (tid < 64) is_sort_heap_wave(sk, si, len, tid);
+        __syncthreads();
+        for (int i = tid; i < len; i += 256) {
+            key[g.f + i] = sk[i];
+            val[g.f + i] = vtmp[g.f + si[i]];
+        }
+        __syncthreads();  // the next segment reuses the LDS
     }
 }
 
@@ -680,121 +715,313 @@ __global__ __launch_bounds__(64 * kIsSmallW) void k_is_small(const ISmall* __res
     __shared__ uint32_t sv[kIsSmall];
     __shared__ uint16_t pl[kIsSmall], pr[kIsSmall];
     __shared__ IsQueue Q;
-    if ((int)blockIdx.x >= *small_cnt) return;
-    const ISmall g = segs[blockIdx.x];
-    const int lane = threadIdx.x & 63;
-    const int len = g.l - g.f;
-    for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
-        sk[i] = key[g.f + i];
-        sv[i] = val[g.f + i];
-    }
-    for (int i = threadIdx.x; i < kIsQCap; i += 64 * kIsSmallW) Q.ready[i] = 0;
-    if (threadIdx.x == 0) {
-        Q.head = Q.tail = Q.open = 0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // the whole segment is the first queued one (counts in units of 64)
-        Q.open = 64;
-        Q.tail = 64;
-        Q.f[0] = 0;
-        Q.l[0] = len;
-        Q.depth[0] = g.depth;
-        Q.ready[0] = 1;
-    }
-    __syncthreads();
+    const int ns = *small_cnt;  // the count on the device: no host round trip before the launch
+    for (int si = blockIdx.x; si < ns; si += gridDim.x) {
+        const ISmall g = segs[si];
+        const int lane = threadIdx.x & 63;
+        const int len = g.l - g.f;
+        for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
+            sk[i] = key[g.f + i];
+            sv[i] = val[g.f + i];
+        }
+        for (int i = threadIdx.x; i < kIsQCap; i += 64 * kIsSmallW) Q.ready[i] = 0;
+        if (threadIdx.x == 0) {
+            Q.head = Q.tail = Q.open = 0;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // the whole segment is the first queued one (counts in units of 64)
+            Q.open = 64;
+            Q.tail = 64;
+            Q.f[0] = 0;
+            Q.l[0] = len;
+            Q.depth[0] = g.depth;
+            Q.ready[0] = 1;
+        }
+        __syncthreads();
 #ifdef PITT_IS_WATCHDOG
-    __shared__ unsigned long long dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait;
-    if (threadIdx.x == 0) dbg_busy = dbg_max = dbg_parts = dbg_elems = dbg_spins = dbg_wait = 0;
-    __syncthreads();
-    const long long t_start = clock64();
-    unsigned long long w_busy = 0, w_parts = 0, w_elems = 0, w_spins = 0, w_wait = 0;
-#endif
-    for (;;) {
-#ifdef PITT_IS_WATCHDOG
-        const long long tw = clock64();
-#endif
-        const int j = is_wave_inc(&Q.head);
-        const int s = j & (kIsQCap - 1);
-        bool got = false;
-#ifdef PITT_IS_WATCHDOG
-        unsigned spins = 0;
+        __shared__ unsigned long long dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait;
+        if (threadIdx.x == 0) dbg_busy = dbg_max = dbg_parts = dbg_elems = dbg_spins = dbg_wait = 0;
+        __syncthreads();
+        const long long t_start = clock64();
+        unsigned long long w_busy = 0, w_parts = 0, w_elems = 0, w_spins = 0, w_wait = 0;
 #endif
         for (;;) {
-            if (is_wave_load(&Q.ready[s]) == j + 1) {
-                got = true;
-                break;
-            }
-            // open == 0: every queued segment is finished, and slot j was never filled (its segment would
-            // stay open until this wave finished it)
-            if (is_wave_load(&Q.open) == 0) break;
-            // no s_sleep: a sleeping wave wakes far too late for the next queued segment (the tree's
-            // partitions are short), and a polling wave issues one LDS read per round trip
 #ifdef PITT_IS_WATCHDOG
-            ++w_spins;
-            if (++spins == (1u << 20)) {
-                if (lane == 0)
-                    printf("is_small watchdog: block %d wave %d slot %d head %d tail %d open %d len %d\n",
-                           (int)blockIdx.x, (int)(threadIdx.x >> 6), j, Q.head, Q.tail, Q.open, len);
-                break;
-            }
+            const long long tw = clock64();
 #endif
-        }
+            const int j = is_wave_inc(&Q.head);
+            const int s = j & (kIsQCap - 1);
+            bool got = false;
 #ifdef PITT_IS_WATCHDOG
-        w_wait += clock64() - tw;
+            unsigned spins = 0;
 #endif
-        if (!got) break;
-        int f = __builtin_amdgcn_readfirstlane(Q.f[s]);
-        int l = __builtin_amdgcn_readfirstlane(Q.l[s]);
-        int depth = __builtin_amdgcn_readfirstlane(Q.depth[s]);
+            for (;;) {
+                if (is_wave_load(&Q.ready[s]) == j + 1) {
+                    got = true;
+                    break;
+                }
+                // open == 0: every queued segment is finished, and slot j was never filled (its segment would
+                // stay open until this wave finished it)
+                if (is_wave_load(&Q.open) == 0) break;
+                // no s_sleep: a sleeping wave wakes far too late for the next queued segment (the tree's
+                // partitions are short), and a polling wave issues one LDS read per round trip
 #ifdef PITT_IS_WATCHDOG
-        int iters = 0;
+                ++w_spins;
+                if (++spins == (1u << 20)) {
+                    if (lane == 0)
+                        printf("is_small watchdog: block %d wave %d slot %d head %d tail %d open %d len %d\n",
+                               (int)blockIdx.x, (int)(threadIdx.x >> 6), j, Q.head, Q.tail, Q.open, len);
+                    break;
+                }
 #endif
-        while (l - f > kIsThreshold) {
-#ifdef PITT_IS_WATCHDOG
-            if (++iters > 4096) {
-                if (lane == 0) printf("is_small spine watchdog: block %d f %d l %d depth %d\n", (int)blockIdx.x, f, l, depth);
-                break;
             }
-#endif
-            if (depth == 0) {
-                is_make_heap_lds<64>(sk + f, sv + f, l - f, lane);
-                is_sort_heap_wave(sk + f, sv + f, l - f, lane);
-                break;
-            }
-            --depth;
 #ifdef PITT_IS_WATCHDOG
-            const long long t0 = clock64();
-            const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
-            w_busy += clock64() - t0;
-            ++w_parts;
-            w_elems += l - f;
+            w_wait += clock64() - tw;
+#endif
+            if (!got) break;
+            int f = __builtin_amdgcn_readfirstlane(Q.f[s]);
+            int l = __builtin_amdgcn_readfirstlane(Q.l[s]);
+            int depth = __builtin_amdgcn_readfirstlane(Q.depth[s]);
+#ifdef PITT_IS_WATCHDOG
+            int iters = 0;
+#endif
+            while (l - f > kIsThreshold) {
+#ifdef PITT_IS_WATCHDOG
+                if (++iters > 4096) {
+                    if (lane == 0) printf("is_small spine watchdog: block %d f %d l %d depth %d\n", (int)blockIdx.x, f, l, depth);
+                    break;
+                }
+#endif
+                if (depth == 0) {
+                    is_make_heap_lds<64>(sk + f, sv + f, l - f, lane);
+                    is_sort_heap_wave(sk + f, sv + f, l - f, lane);
+                    break;
+                }
+                --depth;
+#ifdef PITT_IS_WATCHDOG
+                const long long t0 = clock64();
+                const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
+                w_busy += clock64() - t0;
+                ++w_parts;
+                w_elems += l - f;
 #else
-            const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
+                const int cut = is_partition_wave(sk, sv, pl, pr, f, l, lane);
 #endif
-            if (l - cut > kIsThreshold) is_queue_push(Q, cut, l, depth);  // __introsort_loop(cut, last, depth)
-            l = cut;
+                if (l - cut > kIsThreshold) is_queue_push(Q, cut, l, depth);  // __introsort_loop(cut, last, depth)
+                l = cut;
+            }
+            is_lds_fence();
+            __hip_atomic_fetch_add(&Q.open, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // -64: finished
         }
-        is_lds_fence();
-        __hip_atomic_fetch_add(&Q.open, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // -64: finished
-    }
 #ifdef PITT_IS_WATCHDOG
-    if (lane == 0) {
-        atomicAdd(&dbg_busy, w_busy);
-        atomicMax(&dbg_max, w_busy);
-        atomicAdd(&dbg_parts, w_parts);
-        atomicAdd(&dbg_elems, w_elems);
-        atomicAdd(&dbg_spins, w_spins);
-        atomicAdd(&dbg_wait, w_wait);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && blockIdx.x < 12)
-        printf("is_small block %d len %d cycles %lld busy %llu maxwave %llu parts %llu elems %llu spins %llu wait %llu\n",
-               (int)blockIdx.x, len, clock64() - t_start, dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait);
+        if (lane == 0) {
+            atomicAdd(&dbg_busy, w_busy);
+            atomicMax(&dbg_max, w_busy);
+            atomicAdd(&dbg_parts, w_parts);
+            atomicAdd(&dbg_elems, w_elems);
+            atomicAdd(&dbg_spins, w_spins);
+            atomicAdd(&dbg_wait, w_wait);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && blockIdx.x < 12)
+            printf("is_small block %d len %d cycles %lld busy %llu maxwave %llu parts %llu elems %llu spins %llu wait %llu\n",
+                   (int)blockIdx.x, len, clock64() - t_start, dbg_busy, dbg_max, dbg_parts, dbg_elems, dbg_spins, dbg_wait);
 #endif
-    __syncthreads();
-    for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
-        key[g.f + i] = sk[i];
-        val[g.f + i] = sv[i];
+        __syncthreads();
+        for (int i = threadIdx.x; i < len; i += 64 * kIsSmallW) {
+            key[g.f + i] = sk[i];
+            val[g.f + i] = sv[i];
+        }
+        __syncthreads();  // the next segment reuses the LDS
+    }
+}
+
+// One 1024-thread block partitions a segment of <= kIsMedium elements in global memory (L2-resident, no
+// grid barrier) with the level kernel's steps, one partition at a time: the left stops and the right stops
+// are ranked in one pass (block scans of ballots, a running total), posL[f + 1 + k] = the k-th left stop
+// and posR[f + 1 + k] = the k-th right stop ascending (the k-th from the end is posR[f + nR - k]); wave 0
+// finds the swap count by a 64-way search; the block swaps.  The block goes on with the left part and
+// stacks the right one while they are longer than kIsSmall; shorter ones go to the block (LDS) list, and
+// a part whose depth runs out to the heap list.
+constexpr int kIsMdT = 1024;
+constexpr int kIsMdRows = 8;  // rows of kIsMdT elements per step of the medium kernel's stop ranking
+__global__ __launch_bounds__(kIsMdT) void k_is_medium(const ISmall* __restrict__ segs, const int32_t* __restrict__ med_cnt,
+                                                      ISmall* __restrict__ small, int32_t* __restrict__ small_cnt,
+                                                      ISeg* __restrict__ heap, int32_t* __restrict__ heap_cnt,
+                                                      uint32_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                      int32_t* __restrict__ posL, int32_t* __restrict__ posR) {
+    __shared__ int mdL[kIsMdRows * kIsLvW], mdR[kIsMdRows * kIsLvW];
+    __shared__ int stk[3 * 128];
+    __shared__ int bc[2];
+    const int tid = threadIdx.x;
+    const int nm = *med_cnt;
+    for (int mi = blockIdx.x; mi < nm; mi += gridDim.x) {
+        const ISmall g0 = segs[mi];
+        int sp = 0, f = g0.f, l = g0.l, depth = g0.depth;
+        for (;;) {
+            while (l - f > kIsSmall) {
+                if (depth == 0) {  // std::__partial_sort of this part
+                    if (tid == 0) {
+                        ISeg h = {};
+                        h.f = f;
+                        h.l = l;
+                        heap[atomicAdd(heap_cnt, 1)] = h;
+                    }
+                    l = f;  // nothing left of it here
+                    break;
+                }
+                --depth;
+                if (tid == 0) {  // median of (first + 1, mid, last - 1) to first
+                    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+                    const uint32_t ka = key[a], kb = key[b], kc = key[c];
+                    int m;
+                    if (ka < kb) m = (kb < kc) ? b : (ka < kc) ? c : a;
+                    else m = (ka < kc) ? a : (kb < kc) ? c : b;
+                    is_swap(key, val, f, m);
+                    bc[0] = (int)key[f];
+                }
+                __syncthreads();
+                const uint32_t p = (uint32_t)bc[0];
+                int nL = 0, nR = 0;  // block-uniform running totals
+                const int lane = tid & 63, w = tid >> 6;
+                for (int base = f + 1; base < l; base += kIsMdT * kIsMdRows) {
+                    // kIsMdRows rows of 1024 elements: every key load issued first, then per row and wave the
+                    // ballot ranks, one exchange of the (row, wave) totals through LDS
+                    uint32_t kk[kIsMdRows];
+#pragma unroll
+                    for (int u = 0; u < kIsMdRows; ++u) {
+                        const int i = base + u * kIsMdT + tid;
+                        kk[u] = i < l ? key[i] : 0u;
+                    }
+                    uint64_t bl[kIsMdRows], br[kIsMdRows];
+#pragma unroll
+                    for (int u = 0; u < kIsMdRows; ++u) {
+                        const bool in = base + u * kIsMdT + tid < l;
+                        bl[u] = __ballot(in && !(kk[u] < p));
+                        br[u] = __ballot(in && !(p < kk[u]));
+                        if (lane == 0) {
+                            mdL[u * kIsLvW + w] = __popcll(bl[u]);
+                            mdR[u * kIsLvW + w] = __popcll(br[u]);
+                        }
+                    }
+                    __syncthreads();
+                    int offL = nL, offR = nR;  // exclusive prefix in (row, wave) order, then the totals
+                    int totL = 0, totR = 0;
+#pragma unroll
+                    for (int u = 0; u < kIsMdRows; ++u) {
+                        int rl = 0, rr = 0, sl = 0, sr = 0;
+#pragma unroll
+                        for (int q = 0; q < kIsLvW; ++q) {
+                            const int a = mdL[u * kIsLvW + q], b2 = mdR[u * kIsLvW + q];
+                            rl += q < w ? a : 0;
+                            rr += q < w ? b2 : 0;
+                            sl += a;
+                            sr += b2;
+                        }
+                        const int i = base + u * kIsMdT + tid;
+                        const uint32_t lo32 = (uint32_t)bl[u], hi32 = (uint32_t)(bl[u] >> 32);
+                        const uint32_t rlo = (uint32_t)br[u], rhi = (uint32_t)(br[u] >> 32);
+                        if ((bl[u] >> lane) & 1ull)
+                            posL[f + 1 + offL + totL + rl + (int)__builtin_amdgcn_mbcnt_hi(hi32, __builtin_amdgcn_mbcnt_lo(lo32, 0u))] = i;
+                        if ((br[u] >> lane) & 1ull)
+                            posR[f + 1 + offR + totR + rr + (int)__builtin_amdgcn_mbcnt_hi(rhi, __builtin_amdgcn_mbcnt_lo(rlo, 0u))] = i;
+                        totL += sl;
+                        totR += sr;
+                    }
+                    nL += totL;
+                    nR += totR;
+                    __syncthreads();  // mdL / mdR are read before the next rows overwrite them
+                }
+                const int32_t* L = posL + f + 1;
+                const int32_t* R = posR + f + nR;  // R[-k]: the k-th right stop from the end
+                if (tid < 64) {  // the swap count: posL[k] < the k-th right stop from the end holds on a prefix
+                    int lo = 0, hi = min(nL, nR);
+                    while (lo < hi) {
+                        const int step = (hi - lo + 63) >> 6;
+                        const int k = lo + step * tid;
+                        const uint64_t fm = __ballot(k < hi && !(L[k] < R[-k]));
+                        if (fm == 0) {
+                            lo = lo + ((hi - lo + step - 1) / step - 1) * step + 1;
+                        } else {
+                            const int f0 = __builtin_ctzll(fm);
+                            hi = lo + step * f0;
+                            if (f0 > 0) lo = lo + step * (f0 - 1) + 1;
+                        }
+                    }
+                    if (tid == 0) bc[1] = lo;
+                }
+                __syncthreads();
+                const int K = bc[1];
+                for (int k0 = tid; k0 < K; k0 += kIsMdT * 4) {  // disjoint pairs; 4 per thread, loads first
+                    int x[4], y[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kIsMdT;
+                        x[u] = k < K ? L[k] : 0;
+                        y[u] = k < K ? R[-k] : 0;
+                    }
+                    uint32_t kx[4], vx[4], ky[4], vy[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (k0 + u * kIsMdT < K) {
+                            kx[u] = key[x[u]];
+                            vx[u] = val[x[u]];
+                            ky[u] = key[y[u]];
+                            vy[u] = val[y[u]];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (k0 + u * kIsMdT < K) {
+                            key[x[u]] = ky[u];
+                            val[x[u]] = vy[u];
+                            key[y[u]] = kx[u];
+                            val[y[u]] = vx[u];
+                        }
+                    }
+                }
+                const int cut = K < nL ? (K > 0 ? min(L[K], R[-(K - 1)]) : L[K]) : R[-(K - 1)];
+                __syncthreads();  // the swaps are done (and bc is free again)
+                if (l - cut > kIsSmall) {  // __introsort_loop(cut, last, depth): stacked
+                    if (tid == 0) {
+                        stk[3 * sp] = cut;
+                        stk[3 * sp + 1] = l;
+                        stk[3 * sp + 2] = depth;
+                    }
+                    ++sp;
+                } else if (l - cut > kIsThreshold && tid == 0) {
+                    small[atomicAdd(small_cnt, 1)] = ISmall{cut, l, depth, 0};
+                }
+                l = cut;
+            }
+            if (l - f > kIsThreshold && tid == 0) small[atomicAdd(small_cnt, 1)] = ISmall{f, l, depth, 0};
+            __syncthreads();  // the stack entry written by thread 0
+            if (sp == 0) break;
+            --sp;
+            f = stk[3 * sp];
+            l = stk[3 * sp + 1];
+            depth = stk[3 * sp + 2];
+            __syncthreads();
+        }
+    }
+}
+
+// The first segment (the whole array) and its count, written on the device.
+__global__ void k_is_root(ISeg* __restrict__ seg, ISmall* __restrict__ small, ISmall* __restrict__ med,
+                          int32_t* __restrict__ cnt, int32_t n, int32_t depth) {
+    if (n <= kIsSmall) {
+        small[0] = ISmall{0, n, depth, 0};
+        cnt[1] = 1;
+    } else if (n <= kIsMedium) {
+        med[0] = ISmall{0, n, depth, 0};
+        cnt[kIsMedCnt] = 1;
+    } else {
+        ISeg r = {};
+        r.f = 0;
+        r.l = n;
+        r.depth = depth;
+        seg[0] = r;
+        cnt[2] = 1;
     }
 }
 
@@ -806,7 +1033,8 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     if (n > INT32_MAX - 1) return ctx->fail(PITT_E_INVALID, "introsort: n exceeds int32 positions");
     const int64_t cap = n / kIsSmall + 16;            // level segments hold > kIsSmall elements each
     const int64_t cap_small = n / kIsThreshold + 16;  // one-wave segments hold > 16 each
-    const int kMaxLevels = 128;
+    const int kMaxLevels = kIsMaxLevels;
+    const int64_t cap_med = n / kIsSmall + 16;  // block (global memory) segments hold > kIsSmall each
     int lg = 0;
     while (((int64_t)2 << lg) <= n) ++lg;  // std::__lg(n)
     const int depth = depth_limit >= 0 ? depth_limit : 2 * lg;
@@ -815,7 +1043,7 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     // grid barriers need every block resident: at most PITT_IS_COOP_MAX blocks (64), well under one
     // block per CU, each within the occupancy limit (checked once).  A plain launch: the cooperative
     // launch API measured ~3.5 ms of host-side cost per call.
-    static int coop_blocks = 0;
+    static int coop_blocks = 0, cu_count = 0;
     if (coop_blocks == 0) {
         int dev = 0, per_cu = 0;
         hipDeviceProp_t prop;
@@ -825,6 +1053,7 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
         if (per_cu < 1) return ctx->fail(PITT_E_NODEVICE, "introsort: level kernel does not fit a CU");
         PITT_HIP_TRY(hipFuncSetAttribute((const void*)k_is_heap, hipFuncAttributeMaxDynamicSharedMemorySize, kHeapLds * 6));
         coop_blocks = std::max(1, std::min(prop.multiProcessorCount * std::min(per_cu, 1), PITT_IS_COOP_MAX));
+        cu_count = prop.multiProcessorCount;
     }
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(coop_blocks, (n + kIsLvT - 1) / kIsLvT));
     const int64_t chunk = (n + G - 1) / G;
@@ -832,6 +1061,7 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     ISeg* segB = (ISeg*)ctx->buf("is_segB", (size_t)cap * sizeof(ISeg));
     ISeg* heapsegs = (ISeg*)ctx->buf("is_heapsegs", (size_t)cap * sizeof(ISeg));
     ISmall* small = (ISmall*)ctx->buf("is_small", (size_t)cap_small * sizeof(ISmall));
+    ISmall* med = (ISmall*)ctx->buf("is_med", (size_t)cap_med * sizeof(ISmall));
     int32_t* segid = (int32_t*)ctx->buf("is_segid", (size_t)n * 4);
     uint8_t* F = (uint8_t*)ctx->buf("is_F", (size_t)n);
     int32_t* SL = (int32_t*)ctx->buf("is_SL", (size_t)(n + 1) * 4);
@@ -842,34 +1072,30 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     // cnt[0] heap segments, cnt[1] one-wave segments, cnt[2 + v] level v's segment count
     // cnt[kMaxLevels + 2]: the grid barrier's arrival counter
     int32_t* cnt = (int32_t*)ctx->buf("is_cnt", (size_t)(kMaxLevels + 4) * 4);
-    int32_t* hcnt = (int32_t*)ctx->pinned("is_hcnt", 16);
     uint32_t* vtmp = (uint32_t*)ctx->buf("is_vtmp", (size_t)n * 4);
-    if (!vtmp || !segA || !segB || !heapsegs || !small || !segid || !F || !SL || !SR || !posL || !posR || !bsum || !cnt ||
-        !hcnt)
+    if (!vtmp || !segA || !segB || !heapsegs || !small || !med || !segid || !F || !SL || !SR || !posL || !posR || !bsum ||
+        !cnt)
         return ctx->fail(PITT_E_NOMEM, "introsort scratch");
     PITT_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(kMaxLevels + 4) * 4, s));
     uint32_t* bar = (uint32_t*)(cnt + kMaxLevels + 2);
-    const int32_t one = 1;
-    const ISmall sroot = {0, (int32_t)n, depth, 0};
-    ISeg root = {};
-    root.f = 0;
-    root.l = (int32_t)n;
-    root.depth = depth;
-    if (n <= kIsSmall) {
-        PITT_HIP_TRY(hipMemcpyAsync(small, &sroot, sizeof sroot, hipMemcpyHostToDevice, s));
-        PITT_HIP_TRY(hipMemcpyAsync(cnt + 1, &one, 4, hipMemcpyHostToDevice, s));
-    } else {
-        PITT_HIP_TRY(hipMemcpyAsync(segA, &root, sizeof root, hipMemcpyHostToDevice, s));
-        PITT_HIP_TRY(hipMemcpyAsync(cnt + 2, &one, 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_is_root, dim3(1), dim3(1), 0, s, segA, small, med, cnt, (int32_t)n, depth);
+    if (n > kIsMedium) {
         PITT_HIP_TRY(hipMemsetAsync(segid, 0, (size_t)n * 4, s));
-        hipLaunchKernelGGL(k_is_levels, dim3(G), dim3(kIsLvT), 0, s, segA, segB, heapsegs, small, cnt, segid, F, SL, SR,
-                           posL, posR, bsum, key, val, n, chunk, depth + 1, bar);
+        hipLaunchKernelGGL(k_is_levels, dim3(G), dim3(kIsLvT), 0, s, segA, segB, heapsegs, small, med, cnt, segid, F, SL,
+                           SR, posL, posR, bsum, key, val, n, chunk, depth + 1, bar);
     }
-    PITT_HIP_TRY(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, s));
-    PITT_HIP_TRY(hipStreamSynchronize(s));  // the host memcpys above read stack values: complete them too
-    if (hcnt[1] > 0) hipLaunchKernelGGL(k_is_small, dim3(hcnt[1]), dim3(64 * kIsSmallW), 0, s, small, cnt + 1, key, val);
-    if (hcnt[0] > 0)
-        hipLaunchKernelGGL(k_is_heap, dim3(hcnt[0]), dim3(256), kHeapLds * 6, s, heapsegs, cnt, key, val, vtmp);
+    if (n > kIsSmall) {
+        const int med_grid = (int)std::max<int64_t>(1, std::min<int64_t>(cap_med, cu_count));
+        hipLaunchKernelGGL(k_is_medium, dim3(med_grid), dim3(kIsMdT), 0, s, med, cnt + kIsMedCnt, small, cnt + 1, heapsegs,
+                           cnt, key, val, posL, posR);
+    }
+    // the block and heap segments: grids sized for their bounds, every block looping over the counts the
+    // level kernel left on the device (no host round trip)
+    const int small_grid = (int)std::max<int64_t>(1, std::min<int64_t>(cap_small, cu_count));
+    const int heap_grid = (int)std::max<int64_t>(1, std::min<int64_t>(cap, 32));
+    hipLaunchKernelGGL(k_is_small, dim3(small_grid), dim3(64 * kIsSmallW), 0, s, small, cnt + 1, key, val);
+    if (n > kIsSmall)
+        hipLaunchKernelGGL(k_is_heap, dim3(heap_grid), dim3(256), kHeapLds * 6, s, heapsegs, cnt, key, val, vtmp);
     PITT_HIP_TRY(hipGetLastError());
     return PITT_OK;
 }

@@ -162,7 +162,8 @@ def test_hip_voxel_fused_1p2m(ctx):
                                           (1000000, 500000, -1), (1000000, 100, 14),
                                           (26624, 1000, 0), (26625, 7, 0), (60000, 60000, 1),
                                           (8192, 300, -1), (8193, 300, -1), (8192, 50, 3), (8000, 8000, -1),
-                                          (30000, 40, -1)])
+                                          (30000, 40, -1), (65536, 500, -1), (65537, 900, -1), (65536, 30, 4),
+                                          (70000, 3, 5)])
 def test_hip_sort_pairs_is_std_sort(ctx, n, keys, depth):
     """pitt_sort_pairs reproduces std::sort's permutation of equal keys (the library's own sort at
     the default depth; the oracle's restatement, validated against the library, with a forced

@@ -14,7 +14,7 @@ import pitt_object_table_segmentation_amd as pitt  # noqa: E402
 
 with pitt.Context(0) as ctx:
     for n, keys in [(17, 3), (40, 5), (100, 10), (500, 50), (2000, 2), (2000, 300), (2048, 2048), (5000, 100),
-                    (8192, 300), (8193, 7), (8000, 8000), (30000, 40)]:
+                    (8192, 300), (8193, 7), (8000, 8000), (30000, 40), (65536, 500), (65537, 900), (70000, 3)]:
         rng = np.random.default_rng(n + keys)
         k = rng.integers(0, keys, n).astype(np.uint32)
         v = rng.permutation(n).astype(np.uint32)
