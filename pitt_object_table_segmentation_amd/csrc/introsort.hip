@@ -1100,4 +1100,42 @@ int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n,
     return PITT_OK;
 }
 
+// __final_insertion_sort after the partitions: every segment the partitions leave unsorted holds at most
+// kIsThreshold (16) elements, and every element of a segment is <= every element of the next one, so a pair
+// of positions more than 15 apart is already in (stable) order, and the stable order of the whole array
+// puts element i at i + #{j in (i, i + 15] : key_j < key_i} - #{j in [i - 15, i) : key_j > key_i}.  One
+// thread per element counts its window in LDS and scatters (key, value) to that position.
+constexpr int kIsFinT = 256, kIsFinH = kIsThreshold - 1;
+__global__ __launch_bounds__(kIsFinT) void k_is_final(const uint32_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                      int64_t n, uint32_t* __restrict__ ko, uint32_t* __restrict__ vo) {
+    __shared__ uint32_t sk[kIsFinT + 2 * kIsFinH];
+    const int64_t b0 = (int64_t)blockIdx.x * kIsFinT;
+    for (int t = threadIdx.x; t < kIsFinT + 2 * kIsFinH; t += kIsFinT) {
+        const int64_t j = b0 - kIsFinH + t;
+        sk[t] = (j >= 0 && j < n) ? key[j] : 0u;
+    }
+    __syncthreads();
+    const int64_t i = b0 + threadIdx.x;
+    if (i >= n) return;
+    const int c = threadIdx.x + kIsFinH;
+    const uint32_t k = sk[c];
+    int64_t pos = i;
+#pragma unroll
+    for (int d = 1; d <= kIsFinH; ++d) {
+        pos += (i + d < n && sk[c + d] < k) ? 1 : 0;
+        pos -= (i - d >= 0 && sk[c - d] > k) ? 1 : 0;
+    }
+    ko[pos] = k;
+    vo[pos] = val[i];
+}
+
+// After introsort_partitions: std::sort's final order of (key, val) into (ko, vo).
+int introsort_final(pitt_ctx* ctx, const uint32_t* key, const uint32_t* val, int64_t n, uint32_t* ko, uint32_t* vo) {
+    if (n <= 0) return PITT_OK;
+    const int64_t grid = (n + kIsFinT - 1) / kIsFinT;
+    hipLaunchKernelGGL(k_is_final, dim3((unsigned)grid), dim3(kIsFinT), 0, ctx->stream, key, val, n, ko, vo);
+    PITT_HIP_TRY(hipGetLastError());
+    return PITT_OK;
+}
+
 }  // namespace pitt

@@ -217,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_vox_centroid(const float* __restrict
 }
 
 int introsort_partitions(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int64_t n, int depth_limit);
+int introsort_final(pitt_ctx* ctx, const uint32_t* key, const uint32_t* val, int64_t n, uint32_t* ko, uint32_t* vo);
 
 static int voxel_impl(pitt_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, float lx, float ly,
                       float lz, int32_t order, float* ox, float* oy, float* oz, int64_t* n_out, int32_t* flags) {
@@ -276,20 +277,30 @@ static int voxel_impl(pitt_ctx* ctx, const float* x, const float* y, const float
         ctx->prof_end(rec);
         if (irc != PITT_OK) return irc;
     }
-    // stable LSD radix sort of the keys over the bits the grid uses
-    int end_bit = 1;
-    while (end_bit < 32 && ((int64_t)1 << end_bit) < P.cells) ++end_bit;
-    if (P.cells > (int64_t)UINT32_MAX) end_bit = 32;  // wrapped int indices: sort every bit
-    hipcub::DoubleBuffer<uint32_t> kb(key, key2), vb(val, val2);
-    size_t tmp_bytes = 0;
-    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (int)nf, 0, end_bit, s));
-    void* tmp = ctx->buf("vox_sort_tmp", std::max<size_t>(tmp_bytes, 16));
-    if (!tmp) return ctx->fail(PITT_E_NOMEM, "voxel sort scratch");
-    rec = ctx->prof_begin("vox_radix_sort", (double)nf * 16.0);
-    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (int)nf, 0, end_bit, s));
-    ctx->prof_end(rec);
-    const uint32_t* sk = kb.Current();
-    const uint32_t* sv = vb.Current();
+    const uint32_t* sk;
+    const uint32_t* sv;
+    if (order == PITT_VOXEL_ORDER_PCL) {  // __final_insertion_sort: every element is within 15 of its place
+        rec = ctx->prof_begin("vox_final_sort", (double)nf * 16.0);
+        const int frc = introsort_final(ctx, key, val, nf, key2, val2);
+        ctx->prof_end(rec);
+        if (frc != PITT_OK) return frc;
+        sk = key2;
+        sv = val2;
+    } else {  // stable LSD radix sort of the keys over the bits the grid uses
+        int end_bit = 1;
+        while (end_bit < 32 && ((int64_t)1 << end_bit) < P.cells) ++end_bit;
+        if (P.cells > (int64_t)UINT32_MAX) end_bit = 32;  // wrapped int indices: sort every bit
+        hipcub::DoubleBuffer<uint32_t> kb(key, key2), vb(val, val2);
+        size_t tmp_bytes = 0;
+        PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (int)nf, 0, end_bit, s));
+        void* tmp = ctx->buf("vox_sort_tmp", std::max<size_t>(tmp_bytes, 16));
+        if (!tmp) return ctx->fail(PITT_E_NOMEM, "voxel sort scratch");
+        rec = ctx->prof_begin("vox_radix_sort", (double)nf * 16.0);
+        PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (int)nf, 0, end_bit, s));
+        ctx->prof_end(rec);
+        sk = kb.Current();
+        sv = vb.Current();
+    }
     // runs of equal idx: their first positions, ascending
     const int64_t ntf = ctiles(nf);
     int32_t* rc = (int32_t*)ctx->buf("vox_rc", (size_t)(ntf + 1) * 4);
@@ -344,14 +355,10 @@ extern "C" int pitt_sort_pairs(pitt_ctx* ctx, uint32_t* key, uint32_t* val, int6
     uint32_t* k2 = (uint32_t*)ctx->buf("sp_k2", (size_t)n * 4);
     uint32_t* v2 = (uint32_t*)ctx->buf("sp_v2", (size_t)n * 4);
     if (!k2 || !v2) return ctx->fail(PITT_E_NOMEM, "sort scratch");
-    hipcub::DoubleBuffer<uint32_t> kb(key, k2), vb(val, v2);
-    size_t tmp_bytes = 0;
-    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (int)n, 0, 32, s));
-    void* tmp = ctx->buf("sp_tmp", std::max<size_t>(tmp_bytes, 16));
-    if (!tmp) return ctx->fail(PITT_E_NOMEM, "sort scratch");
-    PITT_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kb, vb, (int)n, 0, 32, s));
-    if (kb.Current() != key) PITT_HIP_TRY(hipMemcpyAsync(key, kb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s));
-    if (vb.Current() != val) PITT_HIP_TRY(hipMemcpyAsync(val, vb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    rc = pitt::introsort_final(ctx, key, val, n, k2, v2);  // __final_insertion_sort
+    if (rc != PITT_OK) return rc;
+    PITT_HIP_TRY(hipMemcpyAsync(key, k2, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    PITT_HIP_TRY(hipMemcpyAsync(val, v2, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
     PITT_HIP_TRY(hipStreamSynchronize(s));
     return PITT_OK;
 }
